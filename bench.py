@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""bench.py — FFC-DCGAN generator forward throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json metric "FFC-generator fwd images/sec @ B=256 64x64x3"):
+FFCGenerator(nz=100, nc=3, ngf=64) (models/ffc_generator.py) forward, B=256 per GPU,
+train-mode BatchNorm (the modules' default state; SpectralTransform.bn1 and FourierUnitSN.bn
+use batch statistics), synthetic z ~ N(0,1), weights from the reference's weights_init
+(fgan64_complete.py:22-31: conv N(0, 0.02), BN gamma N(1, 0.02), beta 0).
+One step = one generator forward over one batch; inputs resident in HBM.
+
+N > 1: one process per GPU, each rank a 256-sample shard of one global batch (weak scaling).
+Train-mode BN statistics are all-reduced over RCCL (SyncBN: the sharded result equals the
+global-batch forward); weights are broadcast once at init.  The step is hipGraph-captured.
+
+The JSON line also carries:
+  roofline      live per-kernel HIP-event timing of one eager pass (dominant kernel), MFMA f32 peak
+  cpu_baseline  the oracle's fp32 op-for-op torch CPU path (oracle/ffc_oracle.py, fft="torch"),
+                rank 0 at N=1 only, bounded sample
+  parity        normwise max|GPU - CPU reference| / max|CPU reference| for the same z and weights
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "FFC-generator fwd images/sec @ B=256 64×64×3; % HBM roofline; max |Δ| vs ref"
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32) dense peak
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=256, help="samples per GPU")
+    p.add_argument("--nz", type=int, default=100)
+    p.add_argument("--nc", type=int, default=3)
+    p.add_argument("--ngf", type=int, default=64)
+    p.add_argument("--bn-mode", choices=["train", "eval"], default="train")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=3)
+    return p.parse_args()
+
+
+def weights_init(m):
+    """fgan64_complete.py:22-31"""
+    import torch.nn as nn
+    name = m.__class__.__name__
+    if name.find("Conv") != -1:
+        nn.init.normal_(m.weight.data, 0.0, 0.02)
+    elif name.find("BatchNorm") != -1:
+        nn.init.normal_(m.weight.data, 1.0, 0.02)
+        nn.init.constant_(m.bias.data, 0)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import _runtime as rt
+
+    torch.manual_seed(1234)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G = F.FFCGenerator(args.nz, args.nc, args.ngf)
+    G.apply(weights_init)
+    cpu_state = {k: v.clone() for k, v in G.state_dict().items()}
+    G = G.to(dev).train(args.bn_mode == "train")
+    if world > 1:
+        for t in G.state_dict().values():
+            dist.broadcast(t, 0)
+        if args.bn_mode == "train":
+            rt.set_sync_bn_group(dist.group.WORLD)
+    gen = torch.Generator(device="cpu").manual_seed(100 + rank)
+    z_cpu = torch.randn((args.batch, args.nz, 1, 1), generator=gen)
+    z = z_cpu.to(dev)
+
+    def step():
+        with torch.no_grad():
+            return G(z)
+
+    for _ in range(max(1, args.warmup)):
+        out = step()
+    torch.cuda.synchronize()
+
+    use_graph = not args.no_graph
+    run = step
+    if use_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(graph):
+                gout = G(z)
+            run = graph.replay
+            run()
+            torch.cuda.synchronize()
+        except Exception as e:  # capture unsupported here: time eagerly, say so
+            print(f"[bench] graph capture failed ({e}); timing eagerly", file=sys.stderr)
+            use_graph = False
+            run = step
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    value = args.batch * world * args.steps / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---- live per-kernel roofline: one instrumented eager pass (HIP events on the launch stream)
+    obs = rt.LaunchObserver()
+    rt.set_observer(obs)
+    for _ in range(max(1, args.profile_steps)):
+        out = step()
+    rt.set_observer(None)
+    summ = obs.summary()
+    kernels = {k: {"launches_per_step": v["launches"] / max(1, args.profile_steps),
+                   "ms_per_step": v["ms"] / max(1, args.profile_steps),
+                   "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
+    dom = max(summ, key=lambda k: summ[k]["ms"])
+    d = summ[dom]
+    if d["flops"] > 0:
+        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4)}
+    else:
+        achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4)}
+    roof["traffic"] = None
+    fu = {k: summ[k] for k in ("fu_pass0", "fu_pass1") if k in summ}
+    fft_roof = None
+    if fu:
+        b = sum(v["bytes"] for v in fu.values())
+        ms = sum(v["ms"] for v in fu.values())
+        fft_roof = {"kernel": "fu_pass0+fu_pass1", "bound": "hbm", "achieved": round(b / (ms * 1e-3) / 1e9, 1),
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "algorithmic_bytes_per_step": b / max(1, args.profile_steps)}
+
+    # ---- CPU baseline + parity (rank 0, N=1 only)
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.ffc_oracle import ffc_generator, normwise_err
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        sd = {k: v.clone() for k, v in cpu_state.items()}
+        training = args.bn_mode == "train"
+        if not training:  # eval: use the GPU model's current running stats
+            sd = {k: v.detach().cpu().clone() for k, v in G.state_dict().items()}
+        with torch.no_grad():
+            ref = ffc_generator(z_cpu, sd, args.nz, args.nc, args.ngf, training, fft="torch")
+            iters, t0 = 1, time.perf_counter()
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                ffc_generator(z_cpu, sd, args.nz, args.nc, args.ngf, training, fft="torch")
+                iters += 1
+            cpu_el = time.perf_counter() - t0
+        with torch.no_grad():
+            gpu_out = step().cpu()
+        parity = {"normwise_err_vs_cpu_ref": normwise_err(gpu_out, ref),
+                  "max_abs_diff": float((gpu_out - ref).abs().max()), "tolerance": 1e-4}
+        cpu = {"value": round(args.batch * (iters - 1) / cpu_el, 2), "unit": "images/s", "cores": threads,
+               "kind": "port",
+               "sample": f"oracle fp32 torch-CPU FFCGenerator fwd (op-for-op reference path), B={args.batch}, "
+                         f"{iters - 1} timed iterations in {cpu_el:.1f}s, {args.bn_mode}-mode BN"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
+            "config": {"workload": f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) forward 64x64x{args.nc}",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch, "bn_mode": args.bn_mode,
+                       "hipgraph": use_graph, "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and
+                                                                          args.bn_mode == "train" else "")},
+            "roofline": roof, "fft_roofline": fft_roof, "cpu_baseline": cpu, "parity": parity,
+            "kernels": kernels,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,16 @@
+"""MI355X-native Fast Fourier Convolution: drop-in for the reference's ``layers`` FFC surface.
+
+    from fastfourierconvolution_amd import *      # instead of  `from layers import *`
+
+exports FourierUnitSN, SELayer, SpectralTransform, FFC, FFCTranspose, FFC_BN_ACT, Resizer,
+Print, debug_print, NoiseInjection (the names layers/__init__.py:2-18 exports for this path)
+plus the restated callers FFCModel / FFCGenerator / FFCDiscriminator.  All compute runs in
+the gfx950 HIP library libffc_amd.so (include/ffc_amd.h); there is no CPU fallback.
+"""
+from .config import Config
+from .ffc import FFC, FFC_BN_ACT, FFCTranspose, FourierUnitSN, SELayer, SpectralTransform
+from .layers_misc import NoiseInjection, Print, Resizer, debug_print
+from .models import FFCDiscriminator, FFCGenerator, FFCModel
+
+__all__ = ["FourierUnitSN", "SELayer", "SpectralTransform", "FFC", "FFCTranspose", "FFC_BN_ACT", "Resizer",
+           "Print", "debug_print", "NoiseInjection", "FFCModel", "FFCGenerator", "FFCDiscriminator", "Config"]

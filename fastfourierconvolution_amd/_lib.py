@@ -1,0 +1,107 @@
+"""ctypes binding of the C ABI in include/ffc_amd.h (libffc_amd.so, built in-tree for gfx950).
+
+There is deliberately no fallback: if the library is missing or no HIP device is
+present, every op raises.  The product path never computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libffc_amd.so")
+
+c_int, c_float, c_void_p, c_longlong, c_size_t, c_double = (
+    ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_double)
+
+MAX_SEG = 3
+MAX_PHASE = 16
+
+ACT = {"Identity": 0, "ReLU": 1, "LeakyReLU": 2, "Tanh": 3, "Sigmoid": 4, "GELU": 5}
+
+
+class ConvSeg(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("gate", c_void_p), ("C", c_int), ("IH", c_int), ("IW", c_int),
+                ("mult_y", c_int), ("mult_x", c_int), ("pool", c_int), ("pad_", c_int)]
+
+
+class ConvPhase(ctypes.Structure):
+    _fields_ = [("py", c_int), ("px", c_int), ("PH", c_int), ("PW", c_int), ("K", c_int), ("Kpad", c_int),
+                ("a_off", c_longlong), ("kt_off", c_int), ("pad_", c_int)]
+
+
+class ConvJob(ctypes.Structure):
+    _fields_ = [("seg", ConvSeg * MAX_SEG), ("ph", ConvPhase * MAX_PHASE),
+                ("A", c_void_p), ("ktab", c_void_p), ("out", c_void_p), ("bias", c_void_p),
+                ("addend", c_void_p), ("stats", c_void_p),
+                ("nseg", c_int), ("nphase", c_int), ("B", c_int), ("M", c_int), ("Mpad", c_int),
+                ("OH", c_int), ("OW", c_int), ("Sy", c_int), ("Sx", c_int),
+                ("act", c_int), ("act_param", c_float), ("pad_", c_int)]
+
+
+# (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
+SIGNATURES = [
+    ("ffc_last_error", ctypes.c_char_p, []),
+    ("ffc_abi_version", c_int, []),
+    ("ffc_struct_sizes", c_int, [ctypes.POINTER(c_int), c_int]),
+    ("ffc_conv_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p, c_int, c_int, c_void_p]),
+    ("ffc_conv_stat_rows_per_tile", c_int, [c_int]),
+    ("ffc_conv_pack", c_int, [ctypes.POINTER(ConvJob), ctypes.POINTER(c_void_p), ctypes.POINTER(c_int),
+                              ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_void_p),
+                              c_void_p, c_void_p, c_void_p]),
+    ("ffc_bn_reduce", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    ("ffc_bn_finalize", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    ("ffc_bn_reduce_finalize", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    ("ffc_bn_act_apply", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float,
+                                 c_void_p]),
+    ("ffc_se_gate", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                            c_void_p]),
+    ("ffc_fu_forward", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                               c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_fu_pack_mix", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_fu_lds_bytes", c_size_t, [c_int, c_int, c_int]),
+]
+
+_lock = threading.Lock()
+_lib = None
+
+
+class FFCError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libffc_amd.so (no GPU needed).  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise FFCError(f"{path} not found: build it with `python -m fastfourierconvolution_amd.build` "
+                           "(the HIP path has no CPU fallback)")
+        lib = ctypes.CDLL(path)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        sizes = (c_int * 3)()
+        lib.ffc_struct_sizes(sizes, 3)
+        want = (ctypes.sizeof(ConvSeg), ctypes.sizeof(ConvPhase), ctypes.sizeof(ConvJob))
+        if tuple(sizes) != want:
+            raise FFCError(f"ABI struct layout mismatch: library {tuple(sizes)} vs binding {want}")
+        _lib = lib
+        return lib
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        msg = load().ffc_last_error().decode(errors="replace")
+        raise FFCError(f"{what or 'ffc'} failed ({status}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """device pointer of a tensor (None for None)."""
+    return None if t is None else t.data_ptr()

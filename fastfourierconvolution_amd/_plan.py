@@ -1,0 +1,234 @@
+"""Host-side planning of the implicit-GEMM convolution launches (pure integer bookkeeping).
+
+A *job* computes one output tensor as the sum of up to three convolution segments
+(e.g. FFCTranspose's ``convl2l(x_l) + convg2l(x_g)``, layers/ffc/ffc_transpose.py:96-100,
+or ``convl2g(x_l) + conv2(x + fu(x))``, :104-106 with spectral_transform.py:108).
+
+Output pixels are split into *phases* ``oy = my*Sy + py`` so that all pixels of a phase
+see the same taps: a stride-s transposed conv has s*s phases (4 for the generator's
+ConvT k4 s2 p1), a ConvT on a 1x1 input gets one phase per output pixel (ffc0), an
+ordinary conv has one phase.  Per phase the k-table lists every (segment, channel, tap)
+that can be in bounds; its entry gives the input offset ``iy = my*mult + off``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+BK = 16
+MPAD = 128
+TILE_CFGS = {0: (128, 128, 2), 1: (64, 128, 2), 2: (32, 256, 4)}  # cfg -> (BM, BN, slab rows per tile)
+PAD_ENTRY = (15, 0, 0, 0)
+
+
+@dataclass(frozen=True)
+class Seg:
+    """One convolution segment feeding a job.
+
+    kind: 'conv' (nn.Conv2d), 'convT' (nn.ConvTranspose2d) or 'pw' (1x1, stride 1, at the
+    output resolution: the 1x1 convs of SpectralTransform).
+    C, IH, IW: channels / spatial size seen by the taps (after pooling when pool=True).
+    """
+    kind: str
+    C: int
+    IH: int
+    IW: int
+    k: int = 1
+    s: int = 1
+    p: int = 0
+    d: int = 1
+    op: int = 0
+    pool: bool = False
+
+
+def conv_out(n, k, s, p, d):
+    return (n + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def convT_out(n, k, s, p, d, op):
+    return (n - 1) * s - 2 * p + d * (k - 1) + op + 1
+
+
+def seg_out(sg: Seg):
+    if sg.kind == "conv":
+        return conv_out(sg.IH, sg.k, sg.s, sg.p, sg.d), conv_out(sg.IW, sg.k, sg.s, sg.p, sg.d)
+    if sg.kind == "convT":
+        return convT_out(sg.IH, sg.k, sg.s, sg.p, sg.d, sg.op), convT_out(sg.IW, sg.k, sg.s, sg.p, sg.d, sg.op)
+    return sg.IH, sg.IW
+
+
+@dataclass
+class Phase:
+    py: int
+    px: int
+    PH: int
+    PW: int
+    entries: list = field(default_factory=list)  # (seg | ch<<4, off_y, off_x, ky | kx<<16)
+
+    @property
+    def K(self):
+        return len(self.entries)
+
+    @property
+    def Kpad(self):
+        return max(BK, -(-self.K // BK) * BK)
+
+
+@dataclass
+class JobPlan:
+    B: int
+    M: int
+    OH: int
+    OW: int
+    Sy: int
+    Sx: int
+    segs: tuple
+    mults: list          # per segment (mult_y, mult_x)
+    phases: list
+    ktab: np.ndarray     # int32 [entries, 4]
+    kt_off: list
+    a_off: list
+    a_size: int          # floats in the packed weight buffer
+
+    @property
+    def Mpad(self):
+        return -(-self.M // MPAD) * MPAD
+
+
+def choose_phase_stride(segs, OH, OW):
+    sT = {sg.s for sg in segs if sg.kind == "convT"}
+    if len(sT) > 1:
+        raise ValueError("a job's transposed segments must share one stride")
+    if any(sg.kind == "conv" for sg in segs) and sT and max(sT) > 1:
+        raise ValueError("cannot mix strided transposed and direct convolutions in one job")
+    if sT:
+        s = sT.pop()
+        one_px = all(sg.IH == 1 and sg.IW == 1 for sg in segs if sg.kind == "convT")
+        if s == 1 and one_px and OH * OW <= 16:
+            return OH, OW  # one phase per output pixel: exactly one tap each
+        return s, s
+    return 1, 1
+
+
+def _taps(sg: Seg, S: int, py: int, axis_in: int, PH: int):
+    """valid (k index, off) pairs along one axis for phase offset py."""
+    out = []
+    for kk in range(sg.k):
+        if sg.kind == "convT":
+            num = py + sg.p - kk * sg.d
+            if num % sg.s:
+                continue
+            off, mult = num // sg.s, S // sg.s
+        elif sg.kind == "conv":
+            off, mult = py * sg.s - sg.p + kk * sg.d, S * sg.s
+        else:
+            off, mult = py, S
+        if any(0 <= my * mult + off < axis_in for my in range(PH)):
+            out.append((kk, off))
+    return out
+
+
+def seg_mult(sg: Seg, S: int):
+    if sg.kind == "convT":
+        return S // sg.s
+    if sg.kind == "conv":
+        return S * sg.s
+    return S
+
+
+def plan_job(B: int, M: int, segs) -> JobPlan:
+    segs = tuple(segs)
+    outs = {seg_out(sg) for sg in segs}
+    if len(outs) != 1:
+        raise ValueError(f"segments disagree on the output size: {outs}")
+    OH, OW = outs.pop()
+    if OH <= 0 or OW <= 0:
+        raise ValueError("empty output")
+    Sy, Sx = choose_phase_stride(segs, OH, OW)
+    for sg in segs:
+        if sg.kind == "convT" and (Sy % sg.s or Sx % sg.s):
+            raise ValueError("phase stride must be a multiple of the transposed stride")
+        if sg.kind == "pw" and (sg.IH, sg.IW) != (OH, OW):
+            raise ValueError("pointwise segment must be at the output resolution")
+    if Sy * Sx > 16:
+        raise ValueError("too many phases")
+    phases, ktab, kt_off, a_off = [], [], [], []
+    Mpad = -(-M // MPAD) * MPAD
+    a_total = 0
+    for py in range(Sy):
+        for px in range(Sx):
+            PH = -(-(OH - py) // Sy)
+            PW = -(-(OW - px) // Sx)
+            if PH <= 0 or PW <= 0:
+                continue
+            ph = Phase(py, px, PH, PW)
+            for si, sg in enumerate(segs):
+                ty = _taps(sg, Sy, py, sg.IH, PH)
+                tx = _taps(sg, Sx, px, sg.IW, PW)
+                for ch in range(sg.C):
+                    for ky, oy in ty:
+                        for kx, ox in tx:
+                            ph.entries.append((si | (ch << 4), oy, ox, ky | (kx << 16)))
+            if ph.K == 0:
+                ph.entries.append(PAD_ENTRY)  # all-zero phase (e.g. fully cropped): still write outputs
+            kt_off.append(len(ktab))
+            ktab.extend(ph.entries)
+            ktab.extend([PAD_ENTRY] * (ph.Kpad - ph.K))
+            a_off.append(a_total)
+            a_total += Mpad * ph.Kpad
+            phases.append(ph)
+    mults = [(seg_mult(sg, Sy), seg_mult(sg, Sx)) for sg in segs]
+    return JobPlan(B, M, OH, OW, Sy, Sx, segs, mults, phases, np.asarray(ktab, dtype=np.int32).reshape(-1, 4),
+                   kt_off, a_off, a_total)
+
+
+def pick_tile_cfg(Ms):
+    m = max(Ms)
+    if m >= 128:
+        return 0
+    if m > 32:
+        return 1
+    return 2
+
+
+def xcd_remap(n: int, nxcd: int = 8):
+    """blockIdx -> locality index such that each XCD (blockIdx % 8) gets a contiguous run
+    (bijective for any n; cdna_hip_programming.md 'XCD swizzle must be bijective')."""
+    q, r = divmod(n, nxcd)
+    out = np.empty(n, dtype=np.int64)
+    for b in range(n):
+        x, slot = b % nxcd, b // nxcd
+        base = x * (q + 1) if x < r else r * (q + 1) + (x - r) * q
+        out[b] = base + slot
+    return out
+
+
+def build_tiles(plans, cfg):
+    """int32 [ntiles, 4] {job | phase<<8, m0, n0, slot}; slots per job returned too."""
+    BM, BN, _ = TILE_CFGS[cfg]
+    ordered = []
+    nslots = []
+    for j, pl in enumerate(plans):
+        slot = 0
+        per_phase = []
+        for pi, ph in enumerate(pl.phases):
+            npix = pl.B * ph.PH * ph.PW
+            lst = []
+            for n0 in range(0, npix, BN):
+                lst.append((pi, n0, slot))
+                slot += 1
+            per_phase.append(lst)
+        nslots.append(slot)
+        # locality order: same n-block across phases and m-tiles next to each other
+        depth = max(len(x) for x in per_phase)
+        for t in range(depth):
+            for lst in per_phase:
+                if t < len(lst):
+                    pi, n0, sl = lst[t]
+                    for m0 in range(0, pl.M, BM):
+                        ordered.append((j | (pi << 8), m0, n0, sl))
+    n = len(ordered)
+    remap = xcd_remap(n)
+    tiles = np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)
+    return tiles, nslots

@@ -1,0 +1,317 @@
+"""Execution layer between the drop-in modules and the C ABI.
+
+Owns: plan caches, weight packing (re-packed only when a weight's version changes),
+per-call buffers (allocated from PyTorch's caching allocator, so hipGraph capture via
+torch.cuda.graph works), BatchNorm statistics (optionally all-reduced across ranks for
+sharded train-mode batches) and the launches themselves.  Every launch goes to
+``torch.cuda.current_stream()``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _lib, _plan
+from ._lib import FFCError, check, ptr
+
+# --------------------------------------------------------------------------- device / stream
+
+
+def require(t: torch.Tensor, name: str = "input") -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor, got {type(t).__name__}")
+    if not t.is_cuda:
+        raise FFCError(f"{name}: the FFC hot path runs only on a ROCm/HIP device (tensor is on {t.device}); "
+                       "there is no CPU fallback")
+    if t.dtype != torch.float32:
+        raise FFCError(f"{name}: fp32 required (got {t.dtype})")
+    return t.contiguous()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def lib():
+    return _lib.load()
+
+
+# --------------------------------------------------------------------------- launch observer
+class LaunchObserver:
+    """Records HIP events around every library launch (on the launch stream) with a label and
+    the launch's algorithmic work, for bench.py's live roofline measurement."""
+
+    def __init__(self):
+        self.records = []   # (label, start event, end event, work dict)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for label, e0, e1, work in self.records:
+            a = agg.setdefault(label, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            a["launches"] += 1
+            a["ms"] += e0.elapsed_time(e1)
+            a["flops"] += work.get("flops", 0.0)
+            a["bytes"] += work.get("bytes", 0.0)
+        return agg
+
+
+_OBS = {"obs": None}
+
+
+def set_observer(obs):
+    _OBS["obs"] = obs
+
+
+class observe:
+    """context manager around one launch"""
+
+    def __init__(self, label, **work):
+        self.label, self.work = label, work
+
+    def __enter__(self):
+        obs = _OBS["obs"]
+        if obs is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        obs = _OBS["obs"]
+        if obs is not None and exc[0] is None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            obs.records.append((self.label, self.e0, e1, self.work))
+        return False
+
+
+# --------------------------------------------------------------------------- SyncBN hook
+_SYNC = {"group": None}
+
+
+def set_sync_bn_group(group):
+    """Route train-mode BN moments through torch.distributed.all_reduce (RCCL) over ``group``
+    (None disables).  Set by fastfourierconvolution_amd.distributed.shard_batch users."""
+    _SYNC["group"] = group
+
+
+def _sync_group():
+    g = _SYNC["group"]
+    if g is None:
+        return None
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(g) == 1:
+        return None
+    return g
+
+
+# --------------------------------------------------------------------------- batch norm
+def bn_mode(bn: nn.BatchNorm2d):
+    use_batch = bn.training or (bn.running_mean is None and bn.running_var is None)
+    update = bn.training and bn.track_running_stats and bn.running_mean is not None
+    return use_batch, update
+
+
+def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, stream):
+    """-> (scale, shift) fp32 device tensors of length C, nn.BatchNorm2d semantics."""
+    if bn.num_features != C:
+        raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
+    use_batch, update = bn_mode(bn)
+    L = lib()
+    scale = torch.empty(C, device=device, dtype=torch.float32)
+    shift = torch.empty(C, device=device, dtype=torch.float32)
+    momentum = -1.0 if bn.momentum is None else float(bn.momentum)
+    gamma = ptr(bn.weight.detach()) if bn.weight is not None else None
+    beta = ptr(bn.bias.detach()) if bn.bias is not None else None
+    rm = ptr(bn.running_mean) if bn.running_mean is not None else None
+    rv = ptr(bn.running_var) if bn.running_var is not None else None
+    nbt = ptr(bn.num_batches_tracked) if bn.num_batches_tracked is not None else None
+    if use_batch:
+        moments = torch.empty((C, 3), device=device, dtype=torch.float64)
+        grp = _sync_group()
+        if grp is None:
+            with observe("bn_stats"):
+                check(L.ffc_bn_reduce_finalize(ptr(slab), nrows, C, ptr(moments), gamma, beta, rm, rv, nbt,
+                                               int(update), momentum, float(bn.eps), float(count_mult), ptr(scale),
+                                               ptr(shift), stream), "ffc_bn_reduce_finalize")
+        else:
+            import torch.distributed as dist
+            check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(moments), stream), "ffc_bn_reduce")
+            dist.all_reduce(moments, group=grp)
+            check(L.ffc_bn_finalize(ptr(moments), C, gamma, beta, rm, rv, nbt, 1, int(update), momentum,
+                                    float(bn.eps), float(count_mult), ptr(scale), ptr(shift), stream),
+                  "ffc_bn_finalize")
+    else:
+        check(L.ffc_bn_finalize(None, C, gamma, beta, rm, rv, nbt, 0, 0, momentum, float(bn.eps), 1.0,
+                                ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
+    return scale, shift
+
+
+def act_code(mod: nn.Module):
+    """activation module -> (FFC_ACT_* code, parameter).  layers/ffc/ffc_bn_act.py:63-67."""
+    if isinstance(mod, nn.Identity):
+        return 0, 0.0
+    if isinstance(mod, nn.LeakyReLU):
+        return 2, float(mod.negative_slope)
+    if isinstance(mod, nn.ReLU):
+        return 1, 0.0
+    if isinstance(mod, nn.Tanh):
+        return 3, 0.0
+    if isinstance(mod, nn.Sigmoid):
+        return 4, 0.0
+    if isinstance(mod, nn.GELU) and getattr(mod, "approximate", "none") == "none":
+        return 5, 0.0
+    raise NotImplementedError(f"activation {type(mod).__name__} has no fused HIP epilogue")
+
+
+def bn_act_apply(x, scale, shift, act, param, out=None):
+    B, C = x.shape[:2]
+    HW = x.numel() // (B * C)
+    out = x if out is None else out
+    with observe("bn_act", bytes=8.0 * x.numel()):
+        check(lib().ffc_bn_act_apply(ptr(x), ptr(out), B, C, HW, ptr(scale), ptr(shift), act, float(param),
+                                     stream_of(x)), "ffc_bn_act_apply")
+    return out
+
+
+# --------------------------------------------------------------------------- convolution jobs
+def _wkey(ts):
+    return tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)
+
+
+def algorithmic_flops(plan) -> float:
+    """exact multiply-adds x2 of the job: every (output pixel, in-bounds tap, channel) triple"""
+    total = 0
+    for pi, ph in enumerate(plan.phases):
+        ent = plan.ktab[plan.kt_off[pi]: plan.kt_off[pi] + ph.K]
+        for sx, oy, ox, _ in ent:
+            seg = sx & 15
+            if seg == 15:
+                continue
+            sg = plan.segs[seg]
+            my_, mx_ = plan.mults[seg]
+            ny = sum(1 for m in range(ph.PH) if 0 <= m * my_ + oy < sg.IH)
+            nx = sum(1 for m in range(ph.PW) if 0 <= m * mx_ + ox < sg.IW)
+            total += ny * nx
+    return 2.0 * total * plan.B * plan.M
+
+
+class ConvExec:
+    """One planned + packed job: output = sum of segment convolutions of fixed shapes."""
+
+    def __init__(self, B, M, segs, weights, device):
+        self.plan = _plan.plan_job(B, M, segs)
+        self.device = device
+        self.ktab = torch.from_numpy(self.plan.ktab.copy()).to(device)
+        self.A = torch.empty(max(1, self.plan.a_size), device=device, dtype=torch.float32)
+        self.has_bias = any(w[4] is not None for w in weights)
+        self.bias = torch.empty(M, device=device, dtype=torch.float32) if self.has_bias else None
+        self._packed = None
+        self.flops = algorithmic_flops(self.plan)
+        self.ensure_packed(weights)
+
+    def base_job(self):
+        pl = self.plan
+        job = _lib.ConvJob()
+        job.nseg = len(pl.segs)
+        job.nphase = len(pl.phases)
+        job.B, job.M, job.Mpad, job.OH, job.OW, job.Sy, job.Sx = pl.B, pl.M, pl.Mpad, pl.OH, pl.OW, pl.Sy, pl.Sx
+        for i, (sg, (my, mx)) in enumerate(zip(pl.segs, pl.mults)):
+            s = job.seg[i]
+            s.C, s.IH, s.IW, s.mult_y, s.mult_x, s.pool = sg.C, sg.IH, sg.IW, my, mx, int(sg.pool)
+        for i, ph in enumerate(pl.phases):
+            p = job.ph[i]
+            p.py, p.px, p.PH, p.PW, p.K, p.Kpad = ph.py, ph.px, ph.PH, ph.PW, ph.K, ph.Kpad
+            p.a_off, p.kt_off = pl.a_off[i], pl.kt_off[i]
+        job.A = self.A.data_ptr()
+        job.ktab = self.ktab.data_ptr()
+        job.bias = self.bias.data_ptr() if self.bias is not None else None
+        return job
+
+    def ensure_packed(self, weights):
+        key = _wkey([w[0] for w in weights] + [w[4] for w in weights])
+        if key == self._packed:
+            return
+        n = len(weights)
+        job = self.base_job()
+        wp = (ctypes.c_void_p * _lib.MAX_SEG)(*[w[0].data_ptr() for w in weights], *([None] * (_lib.MAX_SEG - n)))
+        lay = (ctypes.c_int * _lib.MAX_SEG)(*[w[1] for w in weights], *([0] * (_lib.MAX_SEG - n)))
+        kh = (ctypes.c_int * _lib.MAX_SEG)(*[w[2] for w in weights], *([1] * (_lib.MAX_SEG - n)))
+        kw = (ctypes.c_int * _lib.MAX_SEG)(*[w[3] for w in weights], *([1] * (_lib.MAX_SEG - n)))
+        bp = (ctypes.c_void_p * _lib.MAX_SEG)(*[ptr(w[4]) for w in weights], *([None] * (_lib.MAX_SEG - n)))
+        check(lib().ffc_conv_pack(ctypes.byref(job), wp, lay, kh, kw, bp, self.A.data_ptr(),
+                                  ptr(self.bias), torch.cuda.current_stream(self.device).cuda_stream),
+              "ffc_conv_pack")
+        self._packed = key
+
+    def job(self, inputs, out, act=0, act_param=0.0, addend=None, stats=None):
+        job = self.base_job()
+        for i, (x, gate) in enumerate(inputs):
+            job.seg[i].x = x.data_ptr()
+            job.seg[i].gate = ptr(gate)
+        job.out = out.data_ptr()
+        job.addend = ptr(addend)
+        job.stats = ptr(stats)
+        job.act = act
+        job.act_param = act_param
+        return job
+
+
+class LaunchPlan:
+    """tile table for a set of jobs launched together"""
+
+    def __init__(self, execs, device):
+        self.cfg = _plan.pick_tile_cfg([e.plan.M for e in execs])
+        tiles, self.nslots = _plan.build_tiles([e.plan for e in execs], self.cfg)
+        self.ntiles = tiles.shape[0]
+        self.tiles = torch.from_numpy(tiles).to(device)
+        self.rows_per_tile = _plan.TILE_CFGS[self.cfg][2]
+
+    def stat_rows(self, j):
+        return self.nslots[j] * self.rows_per_tile
+
+    def launch(self, jobs, stream, flops=0.0):
+        arr = (_lib.ConvJob * len(jobs))(*jobs)
+        with observe("conv_gemm", flops=flops):
+            check(lib().ffc_conv_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
+                  "ffc_conv_forward")
+
+
+def conv_weight(mod):
+    """(weight, layout, kh, kw, bias) for nn.Conv2d (layout 0) / nn.ConvTranspose2d (layout 1)."""
+    w = mod.weight.detach()
+    kh, kw = w.shape[2], w.shape[3]
+    b = mod.bias.detach() if mod.bias is not None else None
+    return (require(w, "weight"), 1 if isinstance(mod, nn.ConvTranspose2d) else 0, kh, kw,
+            require(b, "bias") if b is not None else None)
+
+
+def _square(v, what):
+    if isinstance(v, (tuple, list)):
+        if len(set(v)) != 1:
+            raise NotImplementedError(f"non-square {what} {v}")
+        return int(v[0])
+    return int(v)
+
+
+def conv_seg(mod, x: torch.Tensor):
+    """Seg for an nn.Conv2d / nn.ConvTranspose2d applied to x."""
+    if mod.groups != 1:
+        raise NotImplementedError("grouped convolutions are not on the FFC hot path (groups=1 in every caller)")
+    if getattr(mod, "padding_mode", "zeros") != "zeros":
+        raise NotImplementedError("only zero padding")
+    if isinstance(mod.padding, str):
+        raise NotImplementedError("string padding")
+    B, C, H, W = x.shape
+    if C != mod.in_channels:
+        raise RuntimeError(f"expected input with {mod.in_channels} channels, got {C}")
+    k = _square(mod.kernel_size, "kernel")
+    s = _square(mod.stride, "stride")
+    p = _square(mod.padding, "padding")
+    d = _square(mod.dilation, "dilation")
+    if isinstance(mod, nn.ConvTranspose2d):
+        op = _square(mod.output_padding, "output_padding")
+        return _plan.Seg("convT", C, H, W, k, s, p, d, op)
+    return _plan.Seg("conv", C, H, W, k, s, p, d)

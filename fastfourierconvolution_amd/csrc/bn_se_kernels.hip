@@ -1,0 +1,258 @@
+// Batch-norm statistics / apply and the SE gate for gfx950.
+//
+// BN: partial slabs {n, mean, M2} (written by the GEMM and FU epilogues) are merged in
+// fp64 in a fixed order -> deterministic; nn.BatchNorm2d running-stat semantics
+// (torch/nn/modules/batchnorm.py as called from layers/ffc/*.py) are reproduced exactly.
+// SE: SELayer (layers/ffc/spectral_transform.py:12-28).
+#include "ffc_internal.h"
+
+#include <cmath>
+
+namespace {
+
+constexpr int RED_THREADS = 256;
+
+// one block per channel: merge rows of a {n, mean, M2} slab into fp64 raw moments
+__device__ void reduce_channel(const float4* __restrict__ slab, int nrows, int C, int c, double* out3) {
+    __shared__ double sh[3][RED_THREADS];
+    double n = 0.0, s = 0.0, q = 0.0;
+    for (int r = threadIdx.x; r < nrows; r += RED_THREADS) {
+        const float4 e = slab[(size_t)r * C + c];
+        const double en = e.x, em = e.y;
+        n += en;
+        s += en * em;
+        q += (double)e.z + en * em * em;
+    }
+    sh[0][threadIdx.x] = n;
+    sh[1][threadIdx.x] = s;
+    sh[2][threadIdx.x] = q;
+    __syncthreads();
+    for (int w = RED_THREADS / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            sh[0][threadIdx.x] += sh[0][threadIdx.x + w];
+            sh[1][threadIdx.x] += sh[1][threadIdx.x + w];
+            sh[2][threadIdx.x] += sh[2][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out3[0] = sh[0][0];
+        out3[1] = sh[1][0];
+        out3[2] = sh[2][0];
+    }
+}
+
+struct FinalizeArgs {
+    const float* gamma;
+    const float* beta;
+    float* running_mean;
+    float* running_var;
+    int64_t* nbt;
+    int use_batch_stats, update_running;
+    float momentum, eps, count_mult;
+    float* scale;
+    float* shift;
+};
+
+__device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a) {
+    float mean, var;
+    if (a.use_batch_stats) {
+        const double n = m3[0];
+        const double mu = m3[1] / n;
+        double v = m3[2] / n - mu * mu;
+        if (v < 0.0) v = 0.0;
+        mean = (float)mu;
+        var = (float)v;
+        if (a.update_running) {
+            float f = a.momentum;
+            if (f < 0.0f) f = 1.0f / (float)(*a.nbt + 1);  // momentum=None: cumulative average
+            const double nfull = n * (double)a.count_mult;
+            const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
+            a.running_mean[c] = (1.0f - f) * a.running_mean[c] + f * mean;
+            a.running_var[c] = (1.0f - f) * a.running_var[c] + f * (float)unb;
+        }
+    } else {
+        mean = a.running_mean[c];
+        var = a.running_var[c];
+    }
+    const float inv = 1.0f / sqrtf(var + a.eps);
+    const float g = a.gamma ? a.gamma[c] : 1.0f;
+    const float bb = a.beta ? a.beta[c] : 0.0f;
+    const float sc = g * inv;
+    a.scale[c] = sc;
+    a.shift[c] = bb - mean * sc;
+}
+
+__global__ void bn_reduce_kernel(const float4* __restrict__ slab, int nrows, int C, double* moments) {
+    reduce_channel(slab, nrows, C, blockIdx.x, moments + 3 * blockIdx.x);
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ moments, int C, FinalizeArgs a) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) finalize_channel(moments + 3 * c, c, a);
+}
+
+// nbt is bumped after every block has read it (stream order: separate tiny kernel)
+__global__ void bn_bump_kernel(int64_t* nbt) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *nbt += 1;
+}
+
+__global__ void bn_reduce_finalize_kernel(const float4* __restrict__ slab, int nrows, int C, double* moments,
+                                          FinalizeArgs a) {
+    const int c = blockIdx.x;
+    reduce_channel(slab, nrows, C, c, moments + 3 * c);
+    __syncthreads();
+    if (threadIdx.x == 0) finalize_channel(moments + 3 * c, c, a);
+}
+
+__global__ void bn_act_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW, long long total4,
+                              const float* __restrict__ scale, const float* __restrict__ shift, int act, float p) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += stride) {
+        const long long e = i * 4;
+        float4 v = reinterpret_cast<const float4*>(x)[i];
+        float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = (int)(((e + j) / HW) % C);
+            r[j] = ffc::apply_act(fmaf(r[j], scale[c], shift[c]), act, p);
+        }
+        reinterpret_cast<float4*>(y)[i] = make_float4(r[0], r[1], r[2], r[3]);
+    }
+}
+
+__global__ void bn_act_scalar_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
+                                     long long total, const float* __restrict__ scale,
+                                     const float* __restrict__ shift, int act, float p) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int c = (int)((i / HW) % C);
+        y[i] = ffc::apply_act(fmaf(x[i], scale[c], shift[c]), act, p);
+    }
+}
+
+// SE gate: one block per sample; 256 threads
+__global__ void se_gate_kernel(const float* __restrict__ x, int C, int H, int W, int pool,
+                               const float* __restrict__ w1, const float* __restrict__ w2, int hid,
+                               float* __restrict__ gate) {
+    extern __shared__ float sm[];
+    float* mean = sm;       // C
+    float* hv = sm + C;     // hid
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int Hc = pool ? (H / 2) * 2 : H;  // AvgPool2d(2,2) floors: odd last row/col dropped
+    const int Wc = pool ? (W / 2) * 2 : W;
+    const float inv = 1.0f / (float)(Hc * Wc);
+    for (int c = wave; c < C; c += nw) {
+        const float* p = x + ((size_t)b * C + c) * H * W;
+        float s = 0.0f;
+        for (int i = lane; i < Hc * Wc; i += 64) {
+            const int yy = i / Wc, xx = i - yy * Wc;
+            s += p[yy * W + xx];
+        }
+        s = ffc::wave_sum(s);
+        if (lane == 0) mean[c] = s * inv;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < hid; j += blockDim.x) {
+        float s = 0.0f;
+        for (int c = 0; c < C; ++c) s = fmaf(w1[(size_t)j * C + c], mean[c], s);
+        hv[j] = fmaxf(s, 0.0f);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (int j = 0; j < hid; ++j) s = fmaf(w2[(size_t)c * hid + j], hv[j], s);
+        gate[(size_t)b * C + c] = 1.0f / (1.0f + expf(-s));
+    }
+}
+
+}  // namespace
+
+extern "C" int ffc_bn_reduce(const float* slab, int nrows, int C, double* moments, void* stream) {
+    FFC_CHECK_ARG(slab && moments && nrows > 0 && C > 0, "ffc_bn_reduce: bad args");
+    hipLaunchKernelGGL(bn_reduce_kernel, dim3(C), dim3(RED_THREADS), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(slab), nrows, C, moments);
+    return ffc::launch_status("ffc_bn_reduce");
+}
+
+static FinalizeArgs make_finalize(const float* gamma, const float* beta, float* rm, float* rv, int64_t* nbt,
+                                  int use_batch_stats, int update_running, float momentum, float eps,
+                                  float count_mult, float* scale, float* shift) {
+    FinalizeArgs a;
+    a.gamma = gamma;
+    a.beta = beta;
+    a.running_mean = rm;
+    a.running_var = rv;
+    a.nbt = nbt;
+    a.use_batch_stats = use_batch_stats;
+    a.update_running = update_running;
+    a.momentum = momentum;
+    a.eps = eps;
+    a.count_mult = count_mult;
+    a.scale = scale;
+    a.shift = shift;
+    return a;
+}
+
+extern "C" int ffc_bn_finalize(const double* moments, int C, const float* gamma, const float* beta,
+                               float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                               int use_batch_stats, int update_running, float momentum, float eps, float count_mult,
+                               float* scale, float* shift, void* stream) {
+    FFC_CHECK_ARG(C > 0 && scale && shift, "ffc_bn_finalize: bad args");
+    FFC_CHECK_ARG(!use_batch_stats || moments, "ffc_bn_finalize: batch stats need moments");
+    FFC_CHECK_ARG(use_batch_stats || (running_mean && running_var), "ffc_bn_finalize: eval needs running stats");
+    FFC_CHECK_ARG(!update_running || (running_mean && running_var && num_batches_tracked),
+                  "ffc_bn_finalize: update needs running buffers");
+    FinalizeArgs a = make_finalize(gamma, beta, running_mean, running_var, num_batches_tracked, use_batch_stats,
+                                   update_running, momentum, eps, count_mult, scale, shift);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, moments, C, a);
+    if (update_running && use_batch_stats)
+        hipLaunchKernelGGL(bn_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, num_batches_tracked);
+    return ffc::launch_status("ffc_bn_finalize");
+}
+
+// fused single-rank path (no cross-rank all-reduce between reduce and finalize)
+extern "C" int ffc_bn_reduce_finalize(const float* slab, int nrows, int C, double* moments, const float* gamma,
+                                      const float* beta, float* running_mean, float* running_var,
+                                      int64_t* num_batches_tracked, int update_running, float momentum, float eps,
+                                      float count_mult, float* scale, float* shift, void* stream) {
+    FFC_CHECK_ARG(slab && moments && nrows > 0 && C > 0 && scale && shift, "ffc_bn_reduce_finalize: bad args");
+    FFC_CHECK_ARG(!update_running || (running_mean && running_var && num_batches_tracked),
+                  "ffc_bn_reduce_finalize: update needs running buffers");
+    FinalizeArgs a = make_finalize(gamma, beta, running_mean, running_var, num_batches_tracked, 1, update_running,
+                                   momentum, eps, count_mult, scale, shift);
+    hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(C), dim3(RED_THREADS), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(slab), nrows, C, moments, a);
+    if (update_running)
+        hipLaunchKernelGGL(bn_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, num_batches_tracked);
+    return ffc::launch_status("ffc_bn_reduce_finalize");
+}
+
+extern "C" int ffc_bn_act_apply(const float* x, float* y, int B, int C, int HW, const float* scale,
+                                const float* shift, int act, float act_param, void* stream) {
+    FFC_CHECK_ARG(x && y && scale && shift && B > 0 && C > 0 && HW > 0, "ffc_bn_act_apply: bad args");
+    const long long total = (long long)B * C * HW;
+    const bool vec = (total % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0);
+    if (vec) {
+        const long long t4 = total / 4;
+        const int grid = (int)std::min<long long>((t4 + 255) / 256, 2048);
+        hipLaunchKernelGGL(bn_act_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, y, C, HW, t4, scale,
+                           shift, act, act_param);
+    } else {
+        const int grid = (int)std::min<long long>((total + 255) / 256, 2048);
+        hipLaunchKernelGGL(bn_act_scalar_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, y, C, HW, total,
+                           scale, shift, act, act_param);
+    }
+    return ffc::launch_status("ffc_bn_act_apply");
+}
+
+extern "C" int ffc_se_gate(const float* x, int B, int C, int H, int W, int pool, const float* w1, const float* w2,
+                           int hidden, float* gate, void* stream) {
+    FFC_CHECK_ARG(x && gate && B > 0 && C > 0 && H > 0 && W > 0 && hidden >= 0, "ffc_se_gate: bad args");
+    FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_se_gate: null weights");
+    const size_t lds = sizeof(float) * (C + hidden);
+    hipLaunchKernelGGL(se_gate_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, x, C, H, W, pool, w1, w2,
+                       hidden, gate);
+    return ffc::launch_status("ffc_se_gate");
+}

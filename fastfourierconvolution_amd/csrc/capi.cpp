@@ -1,0 +1,36 @@
+// C-ABI plumbing: thread-local error text and launch checks.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "ffc_internal.h"
+
+namespace ffc {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+int launch_status(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        return FFC_E_LAUNCH;
+    }
+    return FFC_OK;
+}
+
+}  // namespace ffc
+
+extern "C" const char* ffc_last_error(void) { return ffc::g_err.c_str(); }
+
+extern "C" int ffc_abi_version(void) { return 1; }
+
+// sizes of the ABI structs, so bindings can verify their mirror layouts
+extern "C" int ffc_struct_sizes(int* out, int n) {
+    if (!out || n < 3) return FFC_E_INVALID;
+    out[0] = (int)sizeof(ffc_conv_seg);
+    out[1] = (int)sizeof(ffc_conv_phase);
+    out[2] = (int)sizeof(ffc_conv_job);
+    return FFC_OK;
+}

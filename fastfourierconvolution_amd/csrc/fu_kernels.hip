@@ -1,0 +1,402 @@
+// Fused Fourier unit for gfx950: one workgroup (8 waves) per sample.
+//
+// Replaces FourierUnitSN.forward (layers/ffc/fourier_unity.py:32-56) and, through the
+// input transform, the bn1/act1/Upsample prologue of SpectralTransform.forward
+// (layers/ffc/spectral_transform.py:79-91) plus the residual add of :108.
+//
+//   HBM  --row loads-->  regs: real W-point FFT per (channel,row)  --> LDS Z planes (Re, Im)
+//   LDS  column H-point FFT per (channel, k_w), ortho scale            (in place)
+//   LDS  spectral mix  Y = Wmix . Z  on v_mfma_f32_32x32x2_f32 (exact fp32), K = 2C
+//        pass 0: per-tile Chan partials of Y -> one {n, mean, M2} per channel -> HBM slab
+//        pass 1: BN scale/shift + ReLU -> LDS Y planes
+//   LDS  inverse column FFT; per-row C2R (Im of k_w = 0, W/2 ignored) + residual --> HBM
+//
+// Train-mode BN needs batch statistics between the mix and its apply; the kernel is run
+// twice (pass 0 then pass 1) and recomputes the cheap FFT+mix instead of spilling Y to HBM,
+// so a train-mode FU moves 2 reads + 1 write of the activation (SURVEY.md §8d "12*N_r").
+#include "ffc_internal.h"
+
+#include <cmath>
+#include <mutex>
+#include <set>
+
+#include "twiddles.inc"
+
+namespace {
+
+constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n >> 1); }
+constexpr int brevc(int i, int bits) {
+    int r = 0;
+    for (int b = 0; b < bits; ++b) r |= ((i >> b) & 1) << (bits - 1 - b);
+    return r;
+}
+
+// In-register radix-2 DIT FFT, fully unrolled.  INV=false: exp(-2 pi i kn/N); INV=true: exp(+..).
+template <int N, bool INV>
+__device__ __forceinline__ void fft_reg(float (&re)[N], float (&im)[N]) {
+    constexpr int L = ilog2c(N);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const int j = brevc(i, L);
+        if (j > i) {
+            float t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+#pragma unroll
+    for (int half = 1; half < N; half <<= 1) {
+        const int step = 128 / (2 * half);
+#pragma unroll
+        for (int j = 0; j < half; ++j) {
+            float wr = 1.0f, wi = 0.0f;
+            if (j != 0) {
+                wr = c_twc[j * step];
+                wi = INV ? c_tws[j * step] : -c_tws[j * step];
+            }
+#pragma unroll
+            for (int i = j; i < N; i += 2 * half) {
+                const float xr = re[i + half] * wr - im[i + half] * wi;
+                const float xi = re[i + half] * wi + im[i + half] * wr;
+                re[i + half] = re[i] - xr;
+                im[i + half] = im[i] - xi;
+                re[i] += xr;
+                im[i] += xi;
+            }
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, float (&v)[N]) {
+    if constexpr (N % 4 == 0) {
+#pragma unroll
+        for (int i = 0; i < N / 4; ++i) {
+            const float4 q = reinterpret_cast<const float4*>(p)[i];
+            v[4 * i] = q.x; v[4 * i + 1] = q.y; v[4 * i + 2] = q.z; v[4 * i + 3] = q.w;
+        }
+    } else if constexpr (N % 2 == 0) {
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i) {
+            const float2 q = reinterpret_cast<const float2*>(p)[i];
+            v[2 * i] = q.x; v[2 * i + 1] = q.y;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = p[i];
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void store_row(float* __restrict__ p, const float (&v)[N]) {
+    static_assert(N % 4 == 0, "rows are >= 4 wide");
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i)
+        reinterpret_cast<float4*>(p)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+struct FuArgs {
+    const float* t;
+    const float* in_scale;
+    const float* in_shift;
+    const float* wmixT;
+    float* slab;
+    const float* bn_scale;
+    const float* bn_shift;
+    float* out;
+    int C, Mpad, in_relu, residual, has_in_affine;
+    float norm;
+};
+
+constexpr int FU_THREADS = 512;
+
+// s row (channel ch, output row y) = transform(t) nearest-upsampled by UP
+template <int W, int UP>
+__device__ __forceinline__ void load_s_row(const FuArgs& a, int b, int ch, int y, int H, float (&s)[W]) {
+    constexpr int tW = W / UP;
+    const int tH = H / UP;
+    const float* trow = a.t + ((size_t)(b * a.C + ch) * tH + y / UP) * tW;
+    float tv[tW];
+    load_row<tW>(trow, tv);
+    float sc = 1.0f, sh = 0.0f;
+    if (a.has_in_affine) {
+        sc = a.in_scale[ch];
+        sh = a.in_shift[ch];
+    }
+#pragma unroll
+    for (int x = 0; x < W; ++x) {
+        float v = tv[x / UP];
+        v = fmaf(v, sc, sh);
+        if (a.in_relu) v = fmaxf(v, 0.0f);
+        s[x] = v;
+    }
+}
+
+template <int H, int W, int UP, int PASS>
+__global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
+    constexpr int WP = W / 2 + 1;
+    constexpr int NB = H * WP;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int C = a.C;
+    const int C2 = 2 * C;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    float* Zre = smem;
+    float* Zim = Zre + C * NB;
+    float* Yre = Zim + C * NB;
+    float* Yim = Yre + C * NB;
+
+    // 1. row R2C (real W-point FFT per (channel,row)), input transform fused
+    for (int r = tid; r < C * H; r += FU_THREADS) {
+        const int ch = r / H, y = r - ch * H;
+        float re[W], im[W];
+        load_s_row<W, UP>(a, b, ch, y, H, re);
+#pragma unroll
+        for (int x = 0; x < W; ++x) im[x] = 0.0f;
+        fft_reg<W, false>(re, im);
+        float* zr = Zre + (ch * H + y) * WP;
+        float* zi = Zim + (ch * H + y) * WP;
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+            zr[k] = re[k];
+            zi[k] = im[k];
+        }
+    }
+    __syncthreads();
+
+    // 2. column C2C over H, ortho scale 1/sqrt(HW)
+    for (int q = tid; q < C * WP; q += FU_THREADS) {
+        const int ch = q / WP, k = q - ch * WP;
+        float* zr = Zre + ch * NB + k;
+        float* zi = Zim + ch * NB + k;
+        float re[H], im[H];
+#pragma unroll
+        for (int y = 0; y < H; ++y) {
+            re[y] = zr[y * WP];
+            im[y] = zi[y * WP];
+        }
+        fft_reg<H, false>(re, im);
+#pragma unroll
+        for (int y = 0; y < H; ++y) {
+            zr[y * WP] = re[y] * a.norm;
+            zi[y * WP] = im[y] * a.norm;
+        }
+    }
+    __syncthreads();
+
+    // 3. spectral mix on MFMA: Y[o][n] = sum_i Wmix[o][i] Z[i][n], Z[2c+h] = (h ? Im : Re)(channel c)
+    //    k-step s feeds k-slot h = lane>>5 with channel s, component h.
+    const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
+    const int MT = (C2 + 31) >> 5, NTL = (NB + 31) >> 5;
+    for (int tile = wave; tile < MT * NTL; tile += FU_THREADS / 64) {
+        const int mt = tile % MT, nt = tile / MT;
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        const float* wp = a.wmixT + (size_t)h * a.Mpad + mt * 32 + col;
+        const float* zp = (h ? Zim : Zre) + nt * 32 + col;
+        const size_t wstep = (size_t)2 * a.Mpad;
+#pragma unroll 8
+        for (int s = 0; s < C; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[s * wstep], zp[s * NB], acc, 0, 0, 0);
+        const int n = nt * 32 + col;
+        const bool nvalid = n < NB;
+        if constexpr (PASS == 0) {
+            const float cnt = (float)min(32, NB - nt * 32);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float v = nvalid ? acc[r] : 0.0f;
+                const float mean = ffc::half_wave_sum(v) / cnt;
+                const float d = nvalid ? acc[r] - mean : 0.0f;
+                const float m2 = ffc::half_wave_sum(d * d);
+                if (col == 0 && o < C2) {
+                    float* st = Yre + (nt * C2 + o) * 3;
+                    st[0] = cnt;
+                    st[1] = mean;
+                    st[2] = m2;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (nvalid && o < C2) {
+                    const float v = fmaxf(fmaf(acc[r], a.bn_scale[o], a.bn_shift[o]), 0.0f);
+                    ((o & 1) ? Yim : Yre)[(o >> 1) * NB + n] = v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    if constexpr (PASS == 0) {
+        // merge the per-tile partials of each channel (Chan et al.) -> one slab row per sample
+        for (int o = tid; o < C2; o += FU_THREADS) {
+            float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+            for (int nt = 0; nt < NTL; ++nt) {
+                const float* st = Yre + (nt * C2 + o) * 3;
+                const float cn = st[0], cm = st[1], cq = st[2];
+                const float tot = nn + cn;
+                const float delta = cm - mean;
+                mean += delta * (cn / tot);
+                m2 += cq + delta * delta * (nn * cn / tot);
+                nn = tot;
+            }
+            reinterpret_cast<float4*>(a.slab)[(size_t)b * C2 + o] = make_float4(nn, mean, m2, 0.0f);
+        }
+        return;
+    } else {
+        // 4. inverse column C2C over H, ortho scale
+        for (int q = tid; q < C * WP; q += FU_THREADS) {
+            const int ch = q / WP, k = q - ch * WP;
+            float* yr = Yre + ch * NB + k;
+            float* yi = Yim + ch * NB + k;
+            float re[H], im[H];
+#pragma unroll
+            for (int y = 0; y < H; ++y) {
+                re[y] = yr[y * WP];
+                im[y] = yi[y * WP];
+            }
+            fft_reg<H, true>(re, im);
+#pragma unroll
+            for (int y = 0; y < H; ++y) {
+                yr[y * WP] = re[y] * a.norm;
+                yi[y * WP] = im[y] * a.norm;
+            }
+        }
+        __syncthreads();
+
+        // 5. per-row C2R over W (imaginary part of bins 0 and W/2 ignored) + residual
+        for (int r = tid; r < C * H; r += FU_THREADS) {
+            const int ch = r / H, y = r - ch * H;
+            const float* yr = Yre + (ch * H + y) * WP;
+            const float* yi = Yim + (ch * H + y) * WP;
+            float re[W], im[W];
+            re[0] = yr[0];
+            im[0] = 0.0f;
+#pragma unroll
+            for (int k = 1; k < W / 2; ++k) {
+                const float vr = yr[k], vi = yi[k];
+                re[k] = vr;
+                im[k] = vi;
+                re[W - k] = vr;
+                im[W - k] = -vi;
+            }
+            re[W / 2] = yr[W / 2];
+            im[W / 2] = 0.0f;
+            fft_reg<W, true>(re, im);
+            if (a.residual) {
+                float s[W];
+                load_s_row<W, UP>(a, b, ch, y, H, s);
+#pragma unroll
+                for (int x = 0; x < W; ++x) re[x] += s[x];
+            }
+            store_row<W>(a.out + ((size_t)(b * C + ch) * H + y) * W, re);
+        }
+    }
+}
+
+__global__ void fu_pack_mix_kernel(const float* __restrict__ w, int C2, int Mpad, float* __restrict__ wt) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= C2 * Mpad) return;
+    const int i = idx / Mpad, o = idx - i * Mpad;
+    wt[idx] = (o < C2) ? w[(size_t)o * C2 + i] : 0.0f;
+}
+
+typedef void (*FuKernel)(FuArgs);
+
+template <int H, int W>
+FuKernel pick_up_pass(int up, int pass) {
+    if (up == 1) return pass == 0 ? fu_kernel<H, W, 1, 0> : fu_kernel<H, W, 1, 1>;
+    return pass == 0 ? fu_kernel<H, W, 2, 0> : fu_kernel<H, W, 2, 1>;
+}
+
+template <int H>
+FuKernel pick_w(int W, int up, int pass) {
+    switch (W) {
+        case 4: return pick_up_pass<H, 4>(up, pass);
+        case 8: return pick_up_pass<H, 8>(up, pass);
+        case 16: return pick_up_pass<H, 16>(up, pass);
+        case 32: return pick_up_pass<H, 32>(up, pass);
+    }
+    return nullptr;
+}
+
+FuKernel pick_kernel(int H, int W, int up, int pass) {
+    switch (H) {
+        case 4: return pick_w<4>(W, up, pass);
+        case 8: return pick_w<8>(W, up, pass);
+        case 16: return pick_w<16>(W, up, pass);
+        case 32: return pick_w<32>(W, up, pass);
+    }
+    return nullptr;
+}
+
+bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
+
+}  // namespace
+
+extern "C" size_t ffc_fu_lds_bytes(int C, int H, int W) {
+    if (C <= 0 || !pow2_in(H, 4, 32) || !pow2_in(W, 4, 32)) return 0;
+    const size_t bytes = (size_t)16 * C * H * (W / 2 + 1);
+    return bytes <= 160 * 1024 ? bytes : 0;
+}
+
+extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                              const float* in_shift, int in_relu, const float* wmixT, int pass,
+                              float* stats_slab, const float* bn_scale, const float* bn_shift, int residual,
+                              float* out, void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu_forward: B and C must be positive");
+    FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu_forward: up must be 1 or 2");
+    FFC_CHECK_ARG(pass == 0 || pass == 1, "ffc_fu_forward: pass must be 0 or 1");
+    const size_t lds = ffc_fu_lds_bytes(C, H, W);
+    FFC_CHECK_ARG(lds > 0, "ffc_fu_forward: unsupported (C,H,W): H,W must be powers of two in [4,32] "
+                           "and 16*C*H*(W/2+1) <= 160 KiB");
+    FFC_CHECK_ARG(t && wmixT, "ffc_fu_forward: null input");
+    FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu_forward: in_scale/in_shift pairing");
+    if (pass == 0) FFC_CHECK_ARG(stats_slab != nullptr, "ffc_fu_forward: pass 0 needs stats_slab");
+    if (pass == 1) FFC_CHECK_ARG(bn_scale && bn_shift && out, "ffc_fu_forward: pass 1 needs bn_scale/shift/out");
+    FuKernel k = pick_kernel(H, W, up, pass);
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu_forward: no kernel instance");
+    FuArgs a;
+    a.t = t;
+    a.in_scale = in_scale;
+    a.in_shift = in_shift;
+    a.has_in_affine = in_scale != nullptr;
+    a.in_relu = in_relu;
+    a.wmixT = wmixT;
+    a.slab = stats_slab;
+    a.bn_scale = bn_scale;
+    a.bn_shift = bn_shift;
+    a.out = out;
+    a.C = C;
+    a.Mpad = (2 * C + 31) / 32 * 32;
+    a.residual = residual;
+    a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
+    if (lds > 64 * 1024) {
+        // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
+        static std::mutex mu;
+        static std::set<const void*> raised;
+        std::lock_guard<std::mutex> g(mu);
+        if (!raised.count(reinterpret_cast<const void*>(k))) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) {
+                ffc::set_error(std::string("ffc_fu_forward: hipFuncSetAttribute: ") + hipGetErrorString(e));
+                return FFC_E_LAUNCH;
+            }
+            raised.insert(reinterpret_cast<const void*>(k));
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(B), dim3(FU_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu_forward");
+}
+
+extern "C" int ffc_fu_pack_mix(const float* w, int C2, float* wmixT, void* stream) {
+    FFC_CHECK_ARG(w && wmixT && C2 > 0, "ffc_fu_pack_mix: bad args");
+    const int Mpad = (C2 + 31) / 32 * 32;
+    const int n = C2 * Mpad;
+    hipLaunchKernelGGL(fu_pack_mix_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, C2, Mpad,
+                       wmixT);
+    return ffc::launch_status("ffc_fu_pack_mix");
+}

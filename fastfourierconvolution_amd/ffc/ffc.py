@@ -1,0 +1,185 @@
+"""Drop-in ``FFC`` (reference: layers/ffc/ffc.py:10-99) and the shared HIP executor that
+FFCTranspose (ffc_transpose.py) and FFC_BN_ACT (ffc_bn_act.py) also use.
+
+Each output branch is ONE implicit-GEMM launch (both branches share it):
+  out_l = convl2l(x_l) + convg2l(x_g)                      segments: conv, conv
+  out_g = convl2g(x_l) + conv2(v),  v = s + fu(s)          segments: conv, 1x1 at output res
+with the FFC_BN_ACT activation fused into the epilogue (or BN partials, then one
+BN+activation pass when norm_layer is BatchNorm2d).  ``nn.Identity`` sub-convs keep the
+reference semantics: they return their input (usually the int 0 of the tuple protocol).
+"""
+import torch
+import torch.nn as nn
+
+from .. import _plan
+from .. import _runtime as rt
+from .spectral_transform import SpectralTransform
+
+
+class _FFCExec:
+    """mixin: fused execution of an FFC / FFCTranspose layer"""
+
+    def _ffc_cache(self):
+        c = self.__dict__.get("_exec_cache")
+        if c is None:
+            c = self.__dict__["_exec_cache"] = {}
+        return c
+
+    def _branch(self, parts):
+        """parts: list of (module, input) whose outputs are summed.  -> (segments, weights, inputs, addends)"""
+        segs, weights, inputs, addends = [], [], [], []
+        for mod, inp in parts:
+            if isinstance(mod, (nn.Conv2d, nn.ConvTranspose2d)):
+                if not isinstance(inp, torch.Tensor):
+                    raise TypeError(f"{type(mod).__name__} got {type(inp).__name__} input")
+                segs.append(rt.conv_seg(mod, inp))
+                weights.append(rt.conv_weight(mod))
+                inputs.append((inp, None))
+            elif isinstance(mod, nn.Identity):
+                if isinstance(inp, torch.Tensor):
+                    addends.append(inp)       # Identity passes a tensor through
+            else:
+                raise NotImplementedError(f"{type(mod).__name__} in an FFC branch")
+        return segs, weights, inputs, addends
+
+    def _run(self, x, y=None, act_l=(0, 0.0), act_g=(0, 0.0), bn_l=None, bn_g=None):
+        x_l, x_g = x if type(x) is tuple else (x, 0)
+        if isinstance(x_l, torch.Tensor):
+            x_l = rt.require(x_l, "x_l")
+        if isinstance(x_g, torch.Tensor):
+            x_g = rt.require(x_g, "x_g")
+        ref = x_l if isinstance(x_l, torch.Tensor) else x_g
+        if not isinstance(ref, torch.Tensor):
+            raise TypeError("FFC input has no tensor branch")
+        B, dev = ref.shape[0], ref.device
+        stream = rt.stream_of(ref)
+        branches = []  # (name, segs, weights, inputs, addends, act, bn, M)
+        if self.ratio_gout != 1:
+            segs, w, inp, add = self._branch([(self.convl2l, x_l), (self.convg2l, x_g)])
+            M = self.convl2l.out_channels if isinstance(self.convl2l, (nn.Conv2d, nn.ConvTranspose2d)) else (
+                self.convg2l.out_channels if isinstance(self.convg2l, (nn.Conv2d, nn.ConvTranspose2d)) else None)
+            branches.append(("l", segs, w, inp, add, act_l, bn_l, M))
+        if self.ratio_gout != 0:
+            segs, w, inp, add = self._branch([(self.convl2g, x_l)])
+            if not isinstance(self.convg2g, nn.Identity):
+                if isinstance(self.convg2g, SpectralTransform):
+                    if y is not None:
+                        raise TypeError("FFC: the conditional (y) path is not supported (the reference raises in "
+                                        "FourierUnitSN, fourier_unity.py:46-47)")
+                    if not isinstance(x_g, torch.Tensor):
+                        raise TypeError("spectral branch needs a tensor x_g")
+                    v = self.convg2g.spectral(x_g)
+                    st = self.convg2g
+                    segs.append(_plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]))
+                    w.append(rt.conv_weight(st.conv2))
+                    inp.append((v, None))
+                else:
+                    raise NotImplementedError(type(self.convg2g).__name__)
+            M = self.convl2g.out_channels if isinstance(self.convl2g, (nn.Conv2d, nn.ConvTranspose2d)) else (
+                self.convg2g.conv2.out_channels if isinstance(self.convg2g, SpectralTransform) else None)
+            branches.append(("g", segs, w, inp, add, act_g, bn_g, M))
+
+        outs = {"l": 0, "g": 0}
+        execs, jobs, post = [], [], []
+        for name, segs, w, inp, add, act, bn, M in branches:
+            if len(add) > 1:
+                raise NotImplementedError("more than one identity pass-through in a branch")
+            addend = add[0] if add else None
+            if not segs:
+                # no convolution: the branch is its pass-through (or the int 0)
+                if addend is None:
+                    continue
+                out = addend.clone()
+                outs[name] = out
+                post.append((out, act, bn, None, 0))
+                continue
+            key = (name, B, tuple(segs), str(dev))
+            cache = self._ffc_cache()
+            ex = cache.get(key)
+            if ex is None:
+                ex = cache[key] = rt.ConvExec(B, M, segs, w, dev)
+            ex.ensure_packed(w)
+            pl = ex.plan
+            out = torch.empty((B, pl.M, pl.OH, pl.OW), device=dev, dtype=torch.float32)
+            if addend is not None and tuple(addend.shape) != tuple(out.shape):
+                raise RuntimeError(f"shape mismatch adding pass-through {tuple(addend.shape)} to {tuple(out.shape)}")
+            outs[name] = out
+            execs.append(ex)
+            jobs.append((ex, inp, out, act, bn, addend))
+        if jobs:
+            lkey = ("launch",) + tuple(id(j[0]) for j in jobs)
+            cache = self._ffc_cache()
+            lp = cache.get(lkey)
+            if lp is None:
+                lp = cache[lkey] = rt.LaunchPlan([j[0] for j in jobs], dev)
+            structs = []
+            for ji, (ex, inp, out, act, bn, addend) in enumerate(jobs):
+                slab = None
+                if bn is not None and rt.bn_mode(bn)[0]:
+                    slab = torch.empty((lp.stat_rows(ji), ex.plan.M, 4), device=dev, dtype=torch.float32)
+                fused_act = act if bn is None else (0, 0.0)
+                structs.append(ex.job(inp, out, fused_act[0], fused_act[1], addend, slab))
+                if bn is not None:
+                    post.append((out, act, bn, slab, lp.stat_rows(ji)))
+            lp.launch(structs, stream, flops=sum(j[0].flops for j in jobs))
+        for out, act, bn, slab, nrows in post:
+            C = out.shape[1]
+            if bn is not None:
+                sc, sh = rt.bn_scale_shift(bn, C, slab, nrows, 1.0, dev, stream) if slab is not None or \
+                    not rt.bn_mode(bn)[0] else self._bn_from_tensor(bn, out, stream)
+            else:
+                if act[0] == 0:
+                    continue
+                sc = torch.ones(C, device=dev, dtype=torch.float32)
+                sh = torch.zeros(C, device=dev, dtype=torch.float32)
+            rt.bn_act_apply(out, sc, sh, act[0], act[1])
+        return outs["l"], outs["g"]
+
+    def _bn_from_tensor(self, bn, out, stream):
+        """batch statistics of a pass-through branch (no GEMM epilogue to collect them)"""
+        B, C = out.shape[:2]
+        ex = self._ffc_cache().get(("bnstats", tuple(out.shape), str(out.device)))
+        if ex is None:
+            seg = _plan.Seg("pw", C, out.shape[2], out.shape[3])
+            eye = nn.Conv2d(C, C, 1, bias=False).to(out.device)
+            with torch.no_grad():
+                eye.weight.zero_()
+                eye.weight[:, :, 0, 0] = torch.eye(C, device=out.device)
+            ex = (rt.ConvExec(B, C, [seg], [rt.conv_weight(eye)], out.device), eye)
+            self._ffc_cache()[("bnstats", tuple(out.shape), str(out.device))] = ex
+        cexec, _ = ex
+        lp = rt.LaunchPlan([cexec], out.device)
+        slab = torch.empty((lp.stat_rows(0), C, 4), device=out.device, dtype=torch.float32)
+        tmp = torch.empty_like(out)
+        lp.launch([cexec.job([(out, None)], tmp, stats=slab)], stream)
+        return rt.bn_scale_shift(bn, C, slab, lp.stat_rows(0), 1.0, out.device, stream)
+
+
+class FFC(_FFCExec, nn.Module):
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int,
+                 ratio_gin: float, ratio_gout: float, stride: int = 1, padding: int = 0,
+                 dilation: int = 1, groups: int = 1, bias: bool = False, enable_lfu: bool = True,
+                 attention: bool = False, num_classes: int = 1):
+        super().__init__()
+        assert stride == 1 or stride == 2, "Stride should be 1 or 2."
+        self.stride = stride
+        in_cg = int(in_channels * ratio_gin)
+        in_cl = in_channels - in_cg
+        out_cg = int(out_channels * ratio_gout)
+        out_cl = out_channels - out_cg
+        print("in_cl, in_cg, out_cl, out_cg")   # the reference prints at construction (ffc.py:38-39)
+        print(in_cl, in_cg, out_cl, out_cg)
+        self.ratio_gin = ratio_gin
+        self.ratio_gout = ratio_gout
+        module = nn.Identity if (in_cl == 0 or out_cl == 0) else nn.Conv2d
+        self.convl2l = module(in_cl, out_cl, kernel_size, stride, padding, dilation, groups, bias)
+        module = nn.Identity if (in_cl == 0 or out_cg == 0) else nn.Conv2d
+        self.convl2g = module(in_cl, out_cg, kernel_size, stride, padding, dilation, groups, bias)
+        module = nn.Identity if (in_cg == 0 or out_cl == 0) else nn.Conv2d
+        self.convg2l = module(in_cg, out_cl, kernel_size, stride, padding, dilation, groups, bias)
+        module = nn.Identity if in_cg == 0 or out_cg == 0 else SpectralTransform
+        self.convg2g = module(in_cg, out_cg, stride, 1 if groups == 1 else groups // 2, enable_lfu, False,
+                              num_classes)
+
+    def forward(self, x, y=None):
+        return self._run(x, y)

@@ -1,0 +1,76 @@
+"""Drop-in ``FourierUnitSN`` (reference: layers/ffc/fourier_unity.py:17-56).
+
+Same constructor, attribute names (``conv_layer``, ``bn``, ``relu``) and state_dict keys;
+forward runs the fused HIP Fourier unit (csrc/fu_kernels.hip) instead of
+rfftn -> 1x1 conv -> BatchNorm2d -> ReLU -> irfftn.
+"""
+import torch
+import torch.nn as nn
+
+from .. import _runtime as rt
+from .._lib import check, ptr
+
+
+class FourierUnitSN(nn.Module):
+    def __init__(self, in_channels, out_channels, groups: int = 1, num_classes: int = 1):
+        super().__init__()
+        self.groups = groups
+        self.conv_layer = torch.nn.Conv2d(in_channels=in_channels * 2, out_channels=out_channels * 2,
+                                          kernel_size=1, stride=1, padding=0, groups=self.groups, bias=False)
+        self.bn = torch.nn.BatchNorm2d(out_channels * 2)
+        self.relu = torch.nn.ReLU(inplace=True)
+        self._mix_key = None
+        self._mixT = None
+
+    # ------------------------------------------------------------------ internals
+    def _check(self, C):
+        if self.groups != 1:
+            raise NotImplementedError("grouped FourierUnitSN mix (groups != 1) is not on the hot path")
+        if self.conv_layer.in_channels != 2 * C or self.conv_layer.out_channels != 2 * C:
+            raise NotImplementedError("FourierUnitSN with in_channels != out_channels")
+
+    def _packed_mix(self, device, stream):
+        w = self.conv_layer.weight.detach()
+        w = rt.require(w, "conv_layer.weight")
+        key = (w.data_ptr(), w._version)
+        if key != self._mix_key or self._mixT is None or self._mixT.device != w.device:
+            C2 = w.shape[0]
+            mpad = -(-C2 // 32) * 32
+            self._mixT = torch.empty((C2, mpad), device=device, dtype=torch.float32)
+            check(rt.lib().ffc_fu_pack_mix(ptr(w), C2, ptr(self._mixT), stream), "ffc_fu_pack_mix")
+            self._mix_key = key
+        return self._mixT
+
+    def _run(self, t, up=1, in_scale=None, in_shift=None, in_relu=False, residual=False):
+        """fused FU over s = transform(t) (see include/ffc_amd.h ffc_fu_forward)."""
+        B, C, th, tw = t.shape
+        H, W = th * up, tw * up
+        self._check(C)
+        L = rt.lib()
+        if L.ffc_fu_lds_bytes(C, H, W) == 0:
+            raise NotImplementedError(f"fused Fourier unit supports H,W in {{4,8,16,32}} with "
+                                      f"16*C*H*(W/2+1) <= 160 KiB; got C={C}, {H}x{W}")
+        dev = t.device
+        stream = rt.stream_of(t)
+        mixT = self._packed_mix(dev, stream)
+        use_batch, _ = rt.bn_mode(self.bn)
+        n_r = float(B * C * H * W)              # fused FU moves 4*N_r per read/write
+        if use_batch:
+            slab = torch.empty((B, 2 * C, 4), device=dev, dtype=torch.float32)
+            with rt.observe("fu_pass0", bytes=4.0 * n_r):
+                check(L.ffc_fu_forward(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
+                                     0, ptr(slab), None, None, 0, None, stream), "ffc_fu_forward(pass 0)")
+            sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, B, 1.0, dev, stream)
+        else:
+            sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
+        out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
+        with rt.observe("fu_pass1", bytes=8.0 * n_r):
+            check(L.ffc_fu_forward(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
+                                 1, None, ptr(sc), ptr(sh), int(residual), ptr(out), stream), "ffc_fu_forward(pass 1)")
+        return out
+
+    def forward(self, x, y=None):
+        if y is not None:
+            # reference: self.bn(ffted, y) -> BatchNorm2d.forward() takes 1 input (fourier_unity.py:46-47)
+            raise TypeError("FourierUnitSN: the conditional (y) path is not supported (the reference raises here)")
+        return self._run(rt.require(x, "x"))

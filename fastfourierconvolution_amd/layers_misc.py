@@ -1,0 +1,62 @@
+"""Caller helpers of the FFC block: Resizer (layers/resizer.py:10-24), Print / debug_print
+(layers/print_layer.py:10-32), NoiseInjection (layers/noise_injection.py:20-32).
+
+They only move tuples around, print shapes or add learned noise (fgan128 train mode); they
+stay plain PyTorch with the reference's exact semantics.
+"""
+import torch
+import torch.nn as nn
+
+from .config import Config
+
+
+def debug_print(*txt):
+    if Config.shared().DEBUG:
+        print(*txt)
+
+
+class Print(nn.Module):
+    def __init__(self, debug=False):
+        super().__init__()
+        self.debug = debug
+
+    def forward(self, x):
+        if self.debug:
+            if type(x) == tuple:
+                if type(x[1]) == int:
+                    print(x[0].shape, "global = 0")
+                else:
+                    aux = torch.cat(list(x), dim=1)
+                    aux = aux.view(aux.shape[0], -1, *aux.shape[3:])
+                    print(aux.shape)
+            else:
+                print(x.shape)
+        return x
+
+
+class Resizer(nn.Module):
+    def __init__(self, debug=False):
+        super().__init__()
+        self.print_size = Print(debug=debug)
+
+    def forward(self, x):
+        output = x
+        if type(x) == tuple:
+            if type(x[1]) == int:
+                output = x[0]
+            else:
+                output = torch.cat(list(x), dim=1)
+                self.print_size(output)
+        return output
+
+
+class NoiseInjection(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(1, channels, 1, 1))
+
+    def forward(self, x, noise=None):
+        if noise is None:
+            batch, _, height, width = x.shape
+            noise = x.new_empty(batch, 1, height, width).normal_()
+        return x + self.weight * noise

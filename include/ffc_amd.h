@@ -1,0 +1,151 @@
+/*
+ * ffc_amd.h — C ABI of the MI355X-native Fast Fourier Convolution hot path.
+ *
+ * The reference (phbgomes22/FastFourierConvolution) is pure PyTorch: its hot path
+ * (BASELINE.json north_star) is the layers/ffc operator surface whose arithmetic
+ * runs inside ATen.  It has no FFI of its own; the entry points below are what a
+ * binding for that surface needs, and each names the reference interface it
+ * replaces.  Every entry point:
+ *   - takes plain device pointers, sizes and a hipStream_t (passed as void*),
+ *   - launches asynchronously on that stream only (no allocation, no host sync,
+ *     so callers may capture it into a hipGraph),
+ *   - returns 0 on success or a negative FFC_E_* code; ffc_last_error() then
+ *     returns a thread-local message.
+ * All tensors are fp32, NCHW, contiguous.  PyTorch owns every buffer.
+ */
+#ifndef FFC_AMD_H
+#define FFC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FFC_OK 0
+#define FFC_E_INVALID (-1)     /* bad argument / unsupported shape */
+#define FFC_E_LAUNCH (-2)      /* hipLaunchKernel failed */
+
+#define FFC_MAX_SEG 3
+#define FFC_MAX_PHASE 16
+
+/* activation codes (layers/ffc/ffc_bn_act.py:63-67; LeakyReLU slope 0.1 passed in act_param) */
+#define FFC_ACT_IDENTITY 0
+#define FFC_ACT_RELU 1
+#define FFC_ACT_LEAKY_RELU 2
+#define FFC_ACT_TANH 3
+#define FFC_ACT_SIGMOID 4
+#define FFC_ACT_GELU 5
+
+const char* ffc_last_error(void);
+int ffc_abi_version(void);
+/* sizeof(ffc_conv_seg), sizeof(ffc_conv_phase), sizeof(ffc_conv_job) -> out[0..2] */
+int ffc_struct_sizes(int* out, int n);
+
+/* ------------------------------------------------------------------ local branch
+ * Implicit-GEMM convolution / transposed convolution with several input segments
+ * summed into one output (FFC.forward's convl2l(x_l)+convg2l(x_g),
+ * layers/ffc/ffc.py:89-97; FFCTranspose.forward, layers/ffc/ffc_transpose.py:96-106;
+ * and SpectralTransform's 1x1 conv1 / conv2, layers/ffc/spectral_transform.py:89,108).
+ * Output pixels are split into phases (oy = my*Sy + py); within a phase the taps are
+ * uniform, so each phase is one GEMM  out[m, n] = sum_k A[phase][m][k] * B(k, n),
+ * B gathered on the fly from the segments through the per-phase k-table.
+ */
+typedef struct ffc_conv_seg {
+    const float* x;      /* (B, C, IH, IW) or (B, C, 2IH, 2IW) when pool=1 */
+    const float* gate;   /* optional (B, C) multiplier (SE gate), or NULL */
+    int C, IH, IW;       /* logical input dims seen by the taps */
+    int mult_y, mult_x;  /* input coord = m*mult + off */
+    int pool;            /* 1: 2x2 average pool applied on the fly (AvgPool2d(2,2)) */
+    int pad_;
+} ffc_conv_seg;
+
+typedef struct ffc_conv_phase {
+    int py, px;          /* output offset of the phase */
+    int PH, PW;          /* phase grid extent */
+    int K;               /* valid k-table rows */
+    int Kpad;            /* rows rounded up to the 16-deep k chunk */
+    long long a_off;     /* float offset of this phase's packed weights [Mpad][Kpad] */
+    int kt_off;          /* int4 offset of this phase's k-table */
+    int pad_;
+} ffc_conv_phase;
+
+typedef struct ffc_conv_job {
+    ffc_conv_seg seg[FFC_MAX_SEG];
+    ffc_conv_phase ph[FFC_MAX_PHASE];
+    const float* A;      /* packed weights */
+    const int* ktab;     /* int4 per k: {seg | ch<<4, off_y, off_x, ky | kx<<16}; seg 15 = pad */
+    float* out;          /* (B, M, OH, OW) */
+    const float* bias;   /* (M) or NULL (already summed over segments) */
+    const float* addend; /* (B, M, OH, OW) added before stats/activation, or NULL */
+    float* stats;        /* BN partial slab [slots*WN][M] float4 {n, mean, M2, 0}, or NULL */
+    int nseg, nphase;
+    int B, M, Mpad, OH, OW, Sy, Sx;
+    int act;             /* FFC_ACT_*, applied in the epilogue (use IDENTITY when a BN follows) */
+    float act_param;
+    int pad_;
+} ffc_conv_job;
+
+/* tiles: device int4 per workgroup {job | phase<<8, m0, n0, stats_slot}; tile_cfg selects
+ * the (BM, BN) instantiation: 0 = 128x128, 1 = 64x128, 2 = 32x256. */
+int ffc_conv_forward(const ffc_conv_job* jobs, int njobs, const int* tiles, int ntiles,
+                     int tile_cfg, void* stream);
+/* number of BN slab rows each tile writes (waves along N) for a tile_cfg */
+int ffc_conv_stat_rows_per_tile(int tile_cfg);
+
+/* Weight packing for one job: A[phase][Mpad][Kpad] (zero padded), bias_out[M] = sum of
+ * segment biases.  w_layout[s]: 0 = Conv2d (O, I, kh, kw), 1 = ConvTranspose2d (I, O, kh, kw).
+ * ktab/phase tables as in ffc_conv_job (host job struct is passed by pointer). */
+int ffc_conv_pack(const ffc_conv_job* job, const float* const* seg_weight, const int* w_layout,
+                  const int* kh, const int* kw, const float* const* seg_bias,
+                  float* A_out, float* bias_out, void* stream);
+
+/* ------------------------------------------------------------------ batch norm
+ * nn.BatchNorm2d semantics (train: biased var normalises, unbiased var -> running_var,
+ * num_batches_tracked += 1, momentum<0 means cumulative average; eval: running stats).
+ * Used for SpectralTransform.bn1 (spectral_transform.py:57,89), FourierUnitSN.bn
+ * (fourier_unity.py:28,49) and FFC_BN_ACT.bn_l/bn_g (ffc_bn_act.py:49-60,73-81). */
+/* merge a partial slab [nrows][C] float4 {n, mean, M2} into moments[C][3] = {n, sum, sumsq} (fp64) */
+int ffc_bn_reduce(const float* slab, int nrows, int C, double* moments, void* stream);
+/* moments (possibly all-reduced across ranks) -> scale/shift; updates running stats */
+int ffc_bn_finalize(const double* moments, int C, const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                    int use_batch_stats, int update_running, float momentum, float eps,
+                    float count_mult, float* scale, float* shift, void* stream);
+/* single-rank fusion of ffc_bn_reduce + ffc_bn_finalize (use_batch_stats = 1) */
+int ffc_bn_reduce_finalize(const float* slab, int nrows, int C, double* moments, const float* gamma,
+                           const float* beta, float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, int update_running, float momentum, float eps,
+                           float count_mult, float* scale, float* shift, void* stream);
+/* y = act(x*scale[c] + shift[c]) elementwise (in place allowed) */
+int ffc_bn_act_apply(const float* x, float* y, int B, int C, int HW, const float* scale,
+                     const float* shift, int act, float act_param, void* stream);
+
+/* ------------------------------------------------------------------ spectral branch
+ * SELayer gate (spectral_transform.py:12-28): gate[b][c] = sigmoid(W2 relu(W1 mean_hw x)),
+ * hidden may be 0 (gate = 0.5).  pool=1: mean over the 2x2-avg-pooled input. */
+int ffc_se_gate(const float* x, int B, int C, int H, int W, int pool, const float* w1,
+                const float* w2, int hidden, float* gate, void* stream);
+
+/* Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56), fused per sample:
+ *   s   = in_relu ? relu(t*in_scale + in_shift) : t, nearest-upsampled by `up` (1|2)
+ *         (SpectralTransform's bn1/act1 + Upsample, spectral_transform.py:44-45,79,89)
+ *   Z   = rfftn(s, ortho) as interleaved Re/Im channels;  Y = Wmix Z  (1x1 conv_layer)
+ *   pass 0: write per-sample BN partials of Y to stats_slab [B][2C] float4
+ *   pass 1: out = (residual ? s : 0) + irfftn(relu(Y*bn_scale + bn_shift), s=(H,W), ortho)
+ * wmixT: (2C, Mpad) transposed, zero-padded copy of conv_layer.weight (Mpad = ceil32(2C)).
+ * H, W: powers of two in [4, 32] (the sizes of the FFC-DCGAN generator/discriminator). */
+int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                   const float* in_shift, int in_relu, const float* wmixT, int pass,
+                   float* stats_slab, const float* bn_scale, const float* bn_shift,
+                   int residual, float* out, void* stream);
+/* transposed zero-padded mix weight: wmixT[i][o] = w[o][i] (w: (2C, 2C, 1, 1)) */
+int ffc_fu_pack_mix(const float* w, int C2, float* wmixT, void* stream);
+/* LDS bytes the fused FU kernel needs (0 if unsupported) */
+size_t ffc_fu_lds_bytes(int C, int H, int W);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FFC_AMD_H */

@@ -41,3 +41,41 @@ def load_case(case):
 @pytest.fixture(scope="session")
 def manifest():
     return load_manifest()
+
+
+def build_dropin(case, state, device="cuda"):
+    """the drop-in module for a golden case, loaded with the case's state (numpy arrays)."""
+    import contextlib
+    import io
+
+    import torch
+    import torch.nn as nn
+
+    import fastfourierconvolution_amd as F
+    kw = dict(case["ctor"])
+    for k in ("norm_layer", "activation_layer"):
+        if k in kw:
+            kw[k] = getattr(nn, kw[k])
+    with contextlib.redirect_stdout(io.StringIO()):
+        mod = getattr(F, case["kind"])(**kw)
+    mod.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in state.items()})
+    mod = mod.to(device)
+    mod.train(case["mode"] == "train")
+    return mod
+
+
+def call_dropin(case, mod, inputs):
+    """run a case's forward; -> dict like the fixture outputs (out / out_l / out_g)."""
+    import torch
+    t = {k: torch.from_numpy(v).cuda() for k, v in inputs.items()}
+    with torch.no_grad():
+        if case["kind"] == "FFC_BN_ACT":
+            x = (t["x_l"], t["x_g"]) if "x_l" in t else t["x"]
+            ol, og = mod(x)
+            res = {}
+            if isinstance(ol, torch.Tensor):
+                res["out_l"] = ol
+            if isinstance(og, torch.Tensor):
+                res["out_g"] = og
+            return res
+        return {"out": mod(next(iter(t.values())))}

@@ -1,0 +1,167 @@
+"""GPU parity of the HIP path (through the C ABI) against the reference's golden vectors and
+the fp64 oracle.  Tolerance (BASELINE.json north_star): normwise
+max|got - ref| / max|ref| <= 1e-4 in fp32."""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import build_dropin, call_dropin, golden_cases, load_case
+from oracle.ffc_oracle import ffc_generator, normwise_err, run_fixture_case
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+CASES = golden_cases()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_golden(case):
+    state, inputs, data = load_case(case)
+    mod = build_dropin(case, state)
+    out = call_dropin(case, mod, inputs)
+    assert sorted("ref." + k for k in out) == case["outputs"]
+    torch.cuda.synchronize()
+    for k, v in out.items():
+        err = normwise_err(v.cpu(), torch.from_numpy(data["ref." + k]))
+        assert err <= TOL, (k, err)
+    # BN running statistics / num_batches_tracked after the forward
+    sd = mod.state_dict()
+    for k in data.files:
+        if k.startswith("after."):
+            key = k[len("after."):]
+            got = sd[key].cpu().numpy()
+            if data[k].dtype.kind == "i":
+                assert int(got) == int(data[k]), key
+            else:
+                np.testing.assert_allclose(got, data[k], rtol=1e-4, atol=1e-5, err_msg=key)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["kind"] == "FourierUnitSN"][:4],
+                         ids=lambda c: c["name"])
+def test_deterministic(case):
+    """two runs on the same inputs are bitwise identical (no atomics on the path)"""
+    state, inputs, _ = load_case(case)
+    a = call_dropin(case, build_dropin(case, state), inputs)["out"]
+    b = call_dropin(case, build_dropin(case, state), inputs)["out"]
+    assert torch.equal(a, b)
+
+
+def _gen_state(nz, nc, ngf, seed=5):
+    import fastfourierconvolution_amd as F
+    with contextlib.redirect_stdout(io.StringIO()):
+        g = F.FFCGenerator(nz, nc, ngf)
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, v in g.state_dict().items():
+        if k.endswith("num_batches_tracked"):
+            sd[k] = v.clone()
+        elif k.endswith("running_var"):
+            sd[k] = torch.ones_like(v)
+        elif k.endswith("running_mean"):
+            sd[k] = torch.zeros_like(v)
+        elif v.dim() == 1:   # BN affine
+            sd[k] = (1.0 if k.endswith("weight") else 0.0) + 0.1 * torch.randn(v.shape, generator=gen)
+        else:
+            fan = v[0].numel() if v.dim() > 1 else 1
+            sd[k] = torch.randn(v.shape, generator=gen) / max(1.0, fan) ** 0.5
+    g.load_state_dict(sd)
+    return g, sd
+
+
+@pytest.mark.parametrize("nc,B", [(1, 256), (3, 256), (3, 7)])
+def test_generator_full_batch_vs_oracle(nc, B):
+    """BASELINE config 2 (nc=1) / metric shape (nc=3) at the full batch, train-mode BN,
+    against the fp64 oracle; also running statistics."""
+    g, sd = _gen_state(100, nc, 64)
+    g = g.cuda().train()
+    z = torch.randn((B, 100, 1, 1), generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        out = g(z.cuda()).cpu()
+    osd = {k: v.double() if v.is_floating_point() else v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        ref = ffc_generator(z.double(), osd, 100, nc, 64, True)
+    err = normwise_err(out, ref)
+    assert err <= TOL, err
+    gsd = g.state_dict()
+    for k, v in osd.items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            np.testing.assert_allclose(gsd[k].cpu().double().numpy(), v.numpy(), rtol=2e-4, atol=1e-5, err_msg=k)
+
+
+def test_generator_eval_matches_oracle():
+    g, sd = _gen_state(100, 3, 64, seed=9)
+    # realistic running stats: one train step with momentum 1
+    for m in g.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = 1.0
+    g = g.cuda().train()
+    with torch.no_grad():
+        g(torch.randn(16, 100, 1, 1, device="cuda"))
+    g.eval()
+    z = torch.randn((32, 100, 1, 1), generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        out = g(z.cuda()).cpu()
+    osd = {k: (v.detach().cpu().double() if v.is_floating_point() else v.cpu()) for k, v in g.state_dict().items()}
+    with torch.no_grad():
+        ref = ffc_generator(z.double(), osd, 100, 3, 64, False)
+    assert normwise_err(out, ref) <= TOL
+
+
+def test_fu_sizes_vs_oracle():
+    """every supported FU plane size, train + eval, several channel counts"""
+    import fastfourierconvolution_amd as F
+    from oracle.ffc_oracle import fourier_unit
+    gen = torch.Generator().manual_seed(11)
+    for (c, h, w) in [(1, 4, 4), (5, 8, 32), (24, 32, 8), (96, 8, 8), (40, 16, 16), (2, 32, 32)]:
+        for train in (True, False):
+            fu = F.FourierUnitSN(c, c)
+            with torch.no_grad():
+                fu.conv_layer.weight.copy_(torch.randn(fu.conv_layer.weight.shape, generator=gen) / (2 * c) ** 0.5)
+                fu.bn.weight.copy_(1 + 0.1 * torch.randn(2 * c, generator=gen))
+                fu.bn.bias.copy_(0.1 * torch.randn(2 * c, generator=gen))
+                fu.bn.running_mean.copy_(0.1 * torch.randn(2 * c, generator=gen))
+                fu.bn.running_var.copy_(1 + torch.rand(2 * c, generator=gen))
+            sd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in fu.state_dict().items()}
+            fu = fu.cuda().train(train)
+            x = torch.randn((3, c, h, w), generator=gen)
+            with torch.no_grad():
+                got = fu(x.cuda()).cpu()
+                ref = fourier_unit(x.double(), sd, "", train)
+            err = normwise_err(got, ref)
+            assert err <= TOL, (c, h, w, train, err)
+
+
+def test_unsupported_plane_raises():
+    import fastfourierconvolution_amd as F
+    fu = F.FourierUnitSN(4, 4).cuda()
+    with pytest.raises(NotImplementedError):
+        fu(torch.randn(1, 4, 64, 64, device="cuda"))
+
+
+def test_conditional_path_raises_like_reference():
+    import fastfourierconvolution_amd as F
+    fu = F.FourierUnitSN(4, 4).cuda()
+    with pytest.raises(TypeError):
+        fu(torch.randn(1, 4, 8, 8, device="cuda"), torch.zeros(1, dtype=torch.long, device="cuda"))
+
+
+def test_graph_capture_replays():
+    """the whole generator forward captures into one hipGraph and replays to the same result"""
+    g, _ = _gen_state(100, 3, 64, seed=2)
+    g = g.cuda().eval()
+    z = torch.randn(64, 100, 1, 1, device="cuda")
+    with torch.no_grad():
+        ref = g(z).clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g(z)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = g(z)
+        graph.replay()
+        torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -1,0 +1,151 @@
+"""CPU checks of the host-side conv planner (fastfourierconvolution_amd/_plan.py).
+
+The GEMM the HIP kernel runs is emulated here with exactly the kernel's index math
+(k-table entry -> input coordinate my*mult + off, weight index (ky, kx)) and compared to
+torch's CPU conv2d / conv_transpose2d in fp64.  This pins the phase decomposition and
+tap tables without a GPU.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fastfourierconvolution_amd import _plan
+
+
+def emulate(plan, xs, ws, layouts):
+    """out[b, m, oy, ox] via the plan's per-phase GEMMs (float64)."""
+    B, M = plan.B, plan.M
+    out = torch.zeros((B, M, plan.OH, plan.OW), dtype=torch.float64)
+    for pi, ph in enumerate(plan.phases):
+        ent = plan.ktab[plan.kt_off[pi]: plan.kt_off[pi] + ph.K]
+        K = len(ent)
+        A = torch.zeros((M, K), dtype=torch.float64)
+        Bm = torch.zeros((K, B, ph.PH, ph.PW), dtype=torch.float64)
+        my = torch.arange(ph.PH)[:, None]
+        mx = torch.arange(ph.PW)[None, :]
+        for k, (sx, oy, ox, kk) in enumerate(ent):
+            seg = sx & 15
+            if seg == 15:
+                continue
+            ch = sx >> 4
+            ky, kx = kk & 0xFFFF, kk >> 16
+            sg = plan.segs[seg]
+            w = ws[seg]
+            A[:, k] = w[:, ch, ky, kx] if layouts[seg] == 0 else w[ch, :, ky, kx]
+            mul_y, mul_x = plan.mults[seg]
+            iy = my * mul_y + oy
+            ix = mx * mul_x + ox
+            valid = (iy >= 0) & (iy < sg.IH) & (ix >= 0) & (ix < sg.IW)
+            x = xs[seg]
+            if sg.pool:
+                x = F.avg_pool2d(x, 2, 2)
+            vals = x[:, ch][:, iy.clamp(0, sg.IH - 1), ix.clamp(0, sg.IW - 1)]
+            Bm[k] = torch.where(valid[None], vals, torch.zeros(()))
+        res = torch.einsum("mk,kbyx->bmyx", A, Bm)
+        out[:, :, ph.py::plan.Sy, ph.px::plan.Sx] = res
+    return out
+
+
+def ref_out(sg, x, w):
+    if sg.pool:
+        x = F.avg_pool2d(x, 2, 2)
+    if sg.kind == "convT":
+        return F.conv_transpose2d(x, w, None, sg.s, sg.p, sg.op, 1, sg.d)
+    if sg.kind == "conv":
+        return F.conv2d(x, w, None, sg.s, sg.p, sg.d)
+    return F.conv2d(x, w)
+
+
+def make(sg, B, M, gen):
+    H, W = (2 * sg.IH, 2 * sg.IW) if sg.pool else (sg.IH, sg.IW)
+    x = torch.randn((B, sg.C, H, W), generator=gen, dtype=torch.float64)
+    if sg.kind == "convT":
+        w = torch.randn((sg.C, M, sg.k, sg.k), generator=gen, dtype=torch.float64)
+        return x, w, 1
+    return x, torch.randn((M, sg.C, sg.k, sg.k), generator=gen, dtype=torch.float64), 0
+
+
+CASES = {
+    "convT_k4s2p1": [_plan.Seg("convT", 5, 4, 4, 4, 2, 1)],
+    "convT_k4s2p1_two_inputs": [_plan.Seg("convT", 3, 8, 8, 4, 2, 1), _plan.Seg("convT", 4, 8, 8, 4, 2, 1)],
+    "convT_plus_pw": [_plan.Seg("convT", 3, 8, 8, 4, 2, 1), _plan.Seg("pw", 2, 16, 16)],
+    "convT_1x1_input_ffc0": [_plan.Seg("convT", 7, 1, 1, 4, 1, 0)],
+    "convT_k3s2p1_op1": [_plan.Seg("convT", 3, 5, 7, 3, 2, 1, 1, 1)],
+    "convT_k4s1p0_dil2": [_plan.Seg("convT", 2, 5, 5, 4, 1, 0, 2)],
+    "conv_k4s2p1": [_plan.Seg("conv", 3, 16, 16, 4, 2, 1)],
+    "conv_k4s2p1_odd": [_plan.Seg("conv", 3, 9, 11, 4, 2, 1)],
+    "conv_k4s1p0_to1x1": [_plan.Seg("conv", 6, 4, 4, 4, 1, 0)],
+    "conv_k3s1p1_two_inputs": [_plan.Seg("conv", 4, 8, 8, 3, 1, 1), _plan.Seg("conv", 5, 8, 8, 3, 1, 1)],
+    "conv_k3s2p1_dil2": [_plan.Seg("conv", 3, 12, 12, 3, 2, 2, 2)],
+    "conv_plus_pw_stride2": [_plan.Seg("conv", 3, 16, 16, 4, 2, 1), _plan.Seg("pw", 5, 8, 8)],
+    "pw_pool": [_plan.Seg("pw", 6, 4, 4, pool=True)],
+    "three_segments": [_plan.Seg("conv", 2, 6, 6, 3, 1, 1), _plan.Seg("conv", 3, 6, 6, 3, 1, 1),
+                       _plan.Seg("pw", 4, 6, 6)],
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_plan_matches_torch(name):
+    segs = CASES[name]
+    gen = torch.Generator().manual_seed(1)
+    B, M = 2, 5
+    plan = _plan.plan_job(B, M, segs)
+    xs, ws, lays = [], [], []
+    ref = 0
+    for sg in segs:
+        x, w, lay = make(sg, B, M, gen)
+        xs.append(x)
+        ws.append(w)
+        lays.append(lay)
+        ref = ref + ref_out(sg, x, w)
+    got = emulate(plan, xs, ws, lays)
+    assert got.shape == ref.shape
+    assert torch.allclose(got, ref, atol=1e-10, rtol=1e-10)
+    # every Kpad is a multiple of the k chunk, pads are marked
+    for pi, ph in enumerate(plan.phases):
+        assert ph.Kpad % _plan.BK == 0 and ph.Kpad >= ph.K
+        pads = plan.ktab[plan.kt_off[pi] + ph.K: plan.kt_off[pi] + ph.Kpad]
+        assert (pads[:, 0] == 15).all()
+
+
+def test_generator_layer_plans():
+    """FFCGenerator ffc1 shapes: 4 phases, 4 taps per input channel per phase."""
+    segs = [_plan.Seg("convT", 256, 4, 4, 4, 2, 1), _plan.Seg("convT", 256, 4, 4, 4, 2, 1)]
+    plan = _plan.plan_job(256, 128, segs)
+    assert (plan.Sy, plan.Sx) == (2, 2) and len(plan.phases) == 4
+    assert all(ph.K == 512 * 4 for ph in plan.phases)
+    ffc0 = _plan.plan_job(256, 256, [_plan.Seg("convT", 100, 1, 1, 4, 1, 0)])
+    assert len(ffc0.phases) == 16 and all(ph.K == 100 for ph in ffc0.phases)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 63, 64, 100, 257, 1000])
+def test_xcd_remap_bijective(n):
+    r = _plan.xcd_remap(n)
+    assert sorted(r.tolist()) == list(range(n))
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_tiles_cover_every_output_once(cfg):
+    pa = _plan.plan_job(3, 70, [_plan.Seg("convT", 4, 5, 5, 4, 2, 1)])
+    pb = _plan.plan_job(3, 33, [_plan.Seg("convT", 4, 5, 5, 4, 2, 1), _plan.Seg("pw", 2, 10, 10)])
+    tiles, nslots = _plan.build_tiles([pa, pb], cfg)
+    BM, BN, _ = _plan.TILE_CFGS[cfg]
+    seen = set()
+    for jx, m0, n0, slot in tiles.tolist():
+        j, p = jx & 0xFF, jx >> 8
+        key = (j, p, m0, n0)
+        assert key not in seen
+        seen.add(key)
+        assert 0 <= slot < nslots[j]
+    for j, pl in enumerate((pa, pb)):
+        for p, ph in enumerate(pl.phases):
+            for n0 in range(0, pl.B * ph.PH * ph.PW, BN):
+                for m0 in range(0, pl.M, BM):
+                    assert (j, p, m0, n0) in seen
+    assert len(seen) == len(tiles)
+
+
+def test_rejects_mixed_strides():
+    with pytest.raises(ValueError):
+        _plan.plan_job(1, 4, [_plan.Seg("convT", 2, 4, 4, 4, 2, 1), _plan.Seg("conv", 2, 8, 8, 3, 1, 1)])
