@@ -40,6 +40,28 @@ class ConvJob(ctypes.Structure):
                 ("act", c_int), ("act_param", c_float), ("pad_", c_int)]
 
 
+class ConvPSeg(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("gate", c_void_p), ("C", c_int), ("Cpad", c_int), ("IH", c_int), ("IW", c_int),
+                ("mult_y", c_int), ("mult_x", c_int), ("org_y", c_int), ("org_x", c_int), ("PR", c_int),
+                ("PC", c_int), ("pool", c_int), ("pad_", c_int)]
+
+
+class ConvPPhase(ctypes.Structure):
+    _fields_ = [("py", c_int), ("px", c_int), ("PH", c_int), ("PW", c_int), ("Kpad", c_int),
+                ("T", c_int * MAX_SEG), ("kseg", c_int * MAX_SEG), ("tap_base", c_int * MAX_SEG),
+                ("a_off", c_longlong)]
+
+
+class ConvPJob(ctypes.Structure):
+    _fields_ = [("seg", ConvPSeg * MAX_SEG), ("ph", ConvPPhase * 4),
+                ("A", c_void_p), ("taptab", c_void_p), ("out", c_void_p), ("bias", c_void_p),
+                ("addend", c_void_p), ("stats", c_void_p),
+                ("nseg", c_int), ("nphase", c_int), ("B", c_int), ("M", c_int), ("Mpad", c_int),
+                ("OH", c_int), ("OW", c_int), ("Sy", c_int), ("Sx", c_int),
+                ("NS", c_int), ("TR", c_int), ("TC", c_int), ("nrb", c_int), ("ncb", c_int),
+                ("act", c_int), ("act_param", c_float)]
+
+
 # (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
 SIGNATURES = [
     ("ffc_last_error", ctypes.c_char_p, []),
@@ -47,6 +69,7 @@ SIGNATURES = [
     ("ffc_struct_sizes", c_int, [ctypes.POINTER(c_int), c_int]),
     ("ffc_conv_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p, c_int, c_int, c_void_p]),
     ("ffc_conv_stat_rows_per_tile", c_int, [c_int]),
+    ("ffc_convp_forward", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_int, c_void_p]),
     ("ffc_conv_pack", c_int, [ctypes.POINTER(ConvJob), ctypes.POINTER(c_void_p), ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_void_p),
                               c_void_p, c_void_p, c_void_p]),
@@ -87,9 +110,10 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (c_int * 3)()
-        lib.ffc_struct_sizes(sizes, 3)
-        want = (ctypes.sizeof(ConvSeg), ctypes.sizeof(ConvPhase), ctypes.sizeof(ConvJob))
+        sizes = (c_int * 6)()
+        lib.ffc_struct_sizes(sizes, 6)
+        want = (ctypes.sizeof(ConvSeg), ctypes.sizeof(ConvPhase), ctypes.sizeof(ConvJob),
+                ctypes.sizeof(ConvPSeg), ctypes.sizeof(ConvPPhase), ctypes.sizeof(ConvPJob))
         if tuple(sizes) != want:
             raise FFCError(f"ABI struct layout mismatch: library {tuple(sizes)} vs binding {want}")
         _lib = lib

@@ -232,3 +232,150 @@ def build_tiles(plans, cfg):
     remap = xcd_remap(n)
     tiles = np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)
     return tiles, nslots
+
+
+# --------------------------------------------------------------------------- LDS-patch plans
+PATCH_CC = 16
+PATCH_PMAX = 32
+PATCH_CFGS = {0: (4, 4), 1: (4, 2), 2: (1, 2), 3: (1, 1)}   # cfg -> (phases per block, N-tiles per wave)
+
+
+@dataclass
+class PatchPlan:
+    B: int
+    M: int
+    OH: int
+    OW: int
+    Sy: int
+    Sx: int
+    segs: tuple
+    mults: list
+    cpad: list
+    org: list            # per segment (org_y, org_x)
+    prc: list            # per segment (PR, PC)
+    phases: list         # dicts: py, px, PH, PW, T[s], kseg[s], tap_base[s], Kpad, a_off, kt_off, K
+    ktab: np.ndarray     # packing table (same format as JobPlan.ktab)
+    taptab: np.ndarray   # int32 patch-relative tap offsets
+    a_size: int
+    cfg: int
+    NS: int
+    TR: int
+    TC: int
+    nrb: int
+    ncb: int
+
+    @property
+    def Mpad(self):
+        return -(-self.M // MPAD) * MPAD
+
+    @property
+    def npb(self):
+        return -(-self.B // self.NS) * self.nrb * self.ncb
+
+
+def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
+    """LDS-patch plan, or None when the job does not fit the patch kernel."""
+    segs = tuple(segs)
+    base = plan_job(B, M, segs)      # validates shapes, picks the phase stride
+    NP = base.Sy * base.Sx
+    if NP not in (1, 4) or len(base.phases) != NP:
+        return None
+    if cfg is None:
+        cfg = 0 if NP == 4 else 2
+    np_, ntw = PATCH_CFGS[cfg]
+    if np_ != NP:
+        return None
+    npix = (4 // NP) * ntw * 32
+    PHm = max(ph.PH for ph in base.phases)
+    PWm = max(ph.PW for ph in base.phases)
+    TC = min(PWm, npix)
+    TR = min(PHm, max(1, npix // TC))
+    NS = max(1, min(B, npix // (TR * TC)))
+    nrb, ncb = -(-PHm // TR), -(-PWm // TC)
+    cpad = [-(-sg.C // PATCH_CC) * PATCH_CC for sg in segs]
+    # taps per (phase, segment)
+    taps = []
+    for ph in base.phases:
+        row = []
+        for si, sg in enumerate(segs):
+            ty = _taps(sg, base.Sy, ph.py, sg.IH, ph.PH)
+            tx = _taps(sg, base.Sx, ph.px, sg.IW, ph.PW)
+            T = len(ty) * len(tx)
+            if T and 16 % T:
+                return None
+            row.append((ty, tx))
+        taps.append(row)
+    org, prc = [], []
+    for si, sg in enumerate(segs):
+        oys = [o for row in taps for (k, o) in row[si][0]]
+        oxs = [o for row in taps for (k, o) in row[si][1]]
+        if not oys or not oxs:
+            oys, oxs = [0], [0]
+        my_, mx_ = base.mults[si]
+        oy0, ox0 = min(oys), min(oxs)
+        PR = (TR - 1) * my_ + (max(oys) - oy0) + 1
+        PC = (TC - 1) * mx_ + (max(oxs) - ox0) + 1
+        if PC > 256 or NS * PATCH_CC * PR > (256 // PC) * PATCH_PMAX or NS * PATCH_CC * PR * PC > 16384:
+            return None
+        org.append((oy0, ox0))
+        prc.append((PR, PC))
+    phases, ktab, taptab = [], [], []
+    a_total = 0
+    Mpad = -(-M // MPAD) * MPAD
+    for pi, ph in enumerate(base.phases):
+        d = dict(py=ph.py, px=ph.px, PH=ph.PH, PW=ph.PW, T=[], kseg=[], tap_base=[])
+        k = 0
+        kt_off = len(ktab)
+        for si, sg in enumerate(segs):
+            ty, tx = taps[pi][si]
+            T = len(ty) * len(tx)
+            d["T"].append(T)
+            d["kseg"].append(k)
+            d["tap_base"].append(len(taptab))
+            PR, PC = prc[si]
+            for (ky, oy) in ty:
+                for (kx, ox) in tx:
+                    taptab.append((oy - org[si][0]) * PC + (ox - org[si][1]))
+            for ch in range(cpad[si]):
+                for (ky, oy) in ty:
+                    for (kx, ox) in tx:
+                        ktab.append((si | (ch << 4), oy, ox, ky | (kx << 16)) if ch < sg.C else PAD_ENTRY)
+            k += cpad[si] * T
+        if k == 0:
+            return None
+        d["Kpad"] = k
+        d["K"] = k
+        d["kt_off"] = kt_off
+        d["a_off"] = a_total
+        a_total += Mpad * k
+        phases.append(d)
+    return PatchPlan(B, M, base.OH, base.OW, base.Sy, base.Sx, segs, base.mults, cpad, org, prc, phases,
+                     np.asarray(ktab, dtype=np.int32).reshape(-1, 4), np.asarray(taptab or [0], dtype=np.int32),
+                     a_total, cfg, NS, TR, TC, nrb, ncb)
+
+
+def pick_patch_cfg(B, M, segs):
+    """4-phase jobs: NTW=4 unless that leaves fewer than ~2 workgroups per CU."""
+    p = plan_patch_job(B, M, segs)
+    if p is None:
+        return None
+    if p.cfg == 0:
+        blocks = p.npb * (-(-M // 32))
+        if blocks < 512:
+            q = plan_patch_job(B, M, segs, 1)
+            if q is not None:
+                return q
+    return p
+
+
+def build_patch_tiles(plans):
+    """int32 [ntiles, 4] {job, m0, pixel block, 0}: blocks sharing a pixel block adjacent, XCD-remapped."""
+    ordered = []
+    npb = max(pl.npb for pl in plans)
+    for pb in range(npb):
+        for j, pl in enumerate(plans):
+            if pb < pl.npb:
+                for m0 in range(0, pl.M, 32):
+                    ordered.append((j, m0, pb, 0))
+    remap = xcd_remap(len(ordered))
+    return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)

@@ -184,25 +184,45 @@ def _wkey(ts):
 def algorithmic_flops(plan) -> float:
     """exact multiply-adds x2 of the job: every (output pixel, in-bounds tap, channel) triple"""
     total = 0
-    for pi, ph in enumerate(plan.phases):
-        ent = plan.ktab[plan.kt_off[pi]: plan.kt_off[pi] + ph.K]
+    phases = plan.phases
+    for pi, ph in enumerate(phases):
+        if isinstance(ph, dict):
+            ent = plan.ktab[ph["kt_off"]: ph["kt_off"] + ph["K"]]
+            PH, PW = ph["PH"], ph["PW"]
+        else:
+            ent = plan.ktab[plan.kt_off[pi]: plan.kt_off[pi] + ph.K]
+            PH, PW = ph.PH, ph.PW
         for sx, oy, ox, _ in ent:
             seg = sx & 15
             if seg == 15:
                 continue
             sg = plan.segs[seg]
             my_, mx_ = plan.mults[seg]
-            ny = sum(1 for m in range(ph.PH) if 0 <= m * my_ + oy < sg.IH)
-            nx = sum(1 for m in range(ph.PW) if 0 <= m * mx_ + ox < sg.IW)
+            ny = sum(1 for m in range(PH) if 0 <= m * my_ + oy < sg.IH)
+            nx = sum(1 for m in range(PW) if 0 <= m * mx_ + ox < sg.IW)
             total += ny * nx
     return 2.0 * total * plan.B * plan.M
 
 
+USE_PATCH = True   # LDS-patch kernel where it applies (tests flip this to cover the generic kernel)
+
+
 class ConvExec:
-    """One planned + packed job: output = sum of segment convolutions of fixed shapes."""
+    """One planned + packed job: output = sum of segment convolutions of fixed shapes.
+
+    kind 'patch' -> ffc_convp_forward (LDS input patch, all phases per workgroup),
+    kind 'gemm'  -> ffc_conv_forward (generic phase GEMM with gathered B)."""
 
     def __init__(self, B, M, segs, weights, device):
-        self.plan = _plan.plan_job(B, M, segs)
+        pp = _plan.pick_patch_cfg(B, M, segs) if USE_PATCH else None
+        if pp is not None:
+            self.kind, self.plan = "patch", pp
+            self.launch_key = ("patch", pp.cfg)
+            self.taptab = torch.from_numpy(pp.taptab.copy()).to(device)
+        else:
+            self.kind, self.plan = "gemm", _plan.plan_job(B, M, segs)
+            self.launch_key = ("gemm",)
+            self.taptab = None
         self.device = device
         self.ktab = torch.from_numpy(self.plan.ktab.copy()).to(device)
         self.A = torch.empty(max(1, self.plan.a_size), device=device, dtype=torch.float32)
@@ -212,21 +232,52 @@ class ConvExec:
         self.flops = algorithmic_flops(self.plan)
         self.ensure_packed(weights)
 
-    def base_job(self):
+    def pack_job(self):
+        """ffc_conv_job describing the packed-weight layout (used by ffc_conv_pack for both kinds)"""
         pl = self.plan
         job = _lib.ConvJob()
         job.nseg = len(pl.segs)
         job.nphase = len(pl.phases)
         job.B, job.M, job.Mpad, job.OH, job.OW, job.Sy, job.Sx = pl.B, pl.M, pl.Mpad, pl.OH, pl.OW, pl.Sy, pl.Sx
         for i, (sg, (my, mx)) in enumerate(zip(pl.segs, pl.mults)):
-            s = job.seg[i]
-            s.C, s.IH, s.IW, s.mult_y, s.mult_x, s.pool = sg.C, sg.IH, sg.IW, my, mx, int(sg.pool)
+            sgs = job.seg[i]
+            sgs.C, sgs.IH, sgs.IW, sgs.mult_y, sgs.mult_x, sgs.pool = sg.C, sg.IH, sg.IW, my, mx, int(sg.pool)
         for i, ph in enumerate(pl.phases):
             p = job.ph[i]
-            p.py, p.px, p.PH, p.PW, p.K, p.Kpad = ph.py, ph.px, ph.PH, ph.PW, ph.K, ph.Kpad
-            p.a_off, p.kt_off = pl.a_off[i], pl.kt_off[i]
+            if isinstance(ph, dict):
+                p.py, p.px, p.PH, p.PW, p.K, p.Kpad = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["K"], ph["Kpad"]
+                p.a_off, p.kt_off = ph["a_off"], ph["kt_off"]
+            else:
+                p.py, p.px, p.PH, p.PW, p.K, p.Kpad = ph.py, ph.px, ph.PH, ph.PW, ph.K, ph.Kpad
+                p.a_off, p.kt_off = pl.a_off[i], pl.kt_off[i]
         job.A = self.A.data_ptr()
         job.ktab = self.ktab.data_ptr()
+        job.bias = self.bias.data_ptr() if self.bias is not None else None
+        return job
+
+    def base_job(self):
+        if self.kind == "gemm":
+            return self.pack_job()
+        pl = self.plan
+        job = _lib.ConvPJob()
+        job.nseg = len(pl.segs)
+        job.nphase = len(pl.phases)
+        job.B, job.M, job.Mpad, job.OH, job.OW, job.Sy, job.Sx = pl.B, pl.M, pl.Mpad, pl.OH, pl.OW, pl.Sy, pl.Sx
+        job.NS, job.TR, job.TC, job.nrb, job.ncb = pl.NS, pl.TR, pl.TC, pl.nrb, pl.ncb
+        for i, sg in enumerate(pl.segs):
+            s = job.seg[i]
+            s.C, s.Cpad, s.IH, s.IW = sg.C, pl.cpad[i], sg.IH, sg.IW
+            s.mult_y, s.mult_x = pl.mults[i]
+            s.org_y, s.org_x = pl.org[i]
+            s.PR, s.PC = pl.prc[i]
+            s.pool = int(sg.pool)
+        for i, ph in enumerate(pl.phases):
+            p = job.ph[i]
+            p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]
+            for si in range(len(pl.segs)):
+                p.T[si], p.kseg[si], p.tap_base[si] = ph["T"][si], ph["kseg"][si], ph["tap_base"][si]
+        job.A = self.A.data_ptr()
+        job.taptab = self.taptab.data_ptr()
         job.bias = self.bias.data_ptr() if self.bias is not None else None
         return job
 
@@ -235,7 +286,7 @@ class ConvExec:
         if key == self._packed:
             return
         n = len(weights)
-        job = self.base_job()
+        job = self.pack_job()
         wp = (ctypes.c_void_p * _lib.MAX_SEG)(*[w[0].data_ptr() for w in weights], *([None] * (_lib.MAX_SEG - n)))
         lay = (ctypes.c_int * _lib.MAX_SEG)(*[w[1] for w in weights], *([0] * (_lib.MAX_SEG - n)))
         kh = (ctypes.c_int * _lib.MAX_SEG)(*[w[2] for w in weights], *([1] * (_lib.MAX_SEG - n)))
@@ -260,23 +311,39 @@ class ConvExec:
 
 
 class LaunchPlan:
-    """tile table for a set of jobs launched together"""
+    """tile table for a set of jobs of the same kind launched together"""
 
     def __init__(self, execs, device):
-        self.cfg = _plan.pick_tile_cfg([e.plan.M for e in execs])
-        tiles, self.nslots = _plan.build_tiles([e.plan for e in execs], self.cfg)
+        kinds = {e.launch_key for e in execs}
+        if len(kinds) != 1:
+            raise ValueError("jobs of one launch must share a kernel configuration")
+        self.key = kinds.pop()
+        if self.key[0] == "patch":
+            self.cfg = self.key[1]
+            tiles = _plan.build_patch_tiles([e.plan for e in execs])
+            self._rows = [e.plan.npb * 4 for e in execs]
+        else:
+            self.cfg = _plan.pick_tile_cfg([e.plan.M for e in execs])
+            tiles, nslots = _plan.build_tiles([e.plan for e in execs], self.cfg)
+            rpt = _plan.TILE_CFGS[self.cfg][2]
+            self._rows = [n * rpt for n in nslots]
         self.ntiles = tiles.shape[0]
         self.tiles = torch.from_numpy(tiles).to(device)
-        self.rows_per_tile = _plan.TILE_CFGS[self.cfg][2]
 
     def stat_rows(self, j):
-        return self.nslots[j] * self.rows_per_tile
+        return self._rows[j]
 
     def launch(self, jobs, stream, flops=0.0):
-        arr = (_lib.ConvJob * len(jobs))(*jobs)
+        L = lib()
         with observe("conv_gemm", flops=flops):
-            check(lib().ffc_conv_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
-                  "ffc_conv_forward")
+            if self.key[0] == "patch":
+                arr = (_lib.ConvPJob * len(jobs))(*jobs)
+                check(L.ffc_convp_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
+                      "ffc_convp_forward")
+            else:
+                arr = (_lib.ConvJob * len(jobs))(*jobs)
+                check(L.ffc_conv_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
+                      "ffc_conv_forward")
 
 
 def conv_weight(mod):

@@ -28,9 +28,12 @@ extern "C" int ffc_abi_version(void) { return 1; }
 
 // sizes of the ABI structs, so bindings can verify their mirror layouts
 extern "C" int ffc_struct_sizes(int* out, int n) {
-    if (!out || n < 3) return FFC_E_INVALID;
+    if (!out || n < 6) return FFC_E_INVALID;
     out[0] = (int)sizeof(ffc_conv_seg);
     out[1] = (int)sizeof(ffc_conv_phase);
     out[2] = (int)sizeof(ffc_conv_job);
+    out[3] = (int)sizeof(ffc_convp_seg);
+    out[4] = (int)sizeof(ffc_convp_phase);
+    out[5] = (int)sizeof(ffc_convp_job);
     return FFC_OK;
 }

@@ -106,14 +106,17 @@ class _FFCExec:
             outs[name] = out
             execs.append(ex)
             jobs.append((ex, inp, out, act, bn, addend))
-        if jobs:
-            lkey = ("launch",) + tuple(id(j[0]) for j in jobs)
-            cache = self._ffc_cache()
+        groups = {}
+        for jb in jobs:
+            groups.setdefault(jb[0].launch_key, []).append(jb)
+        cache = self._ffc_cache()
+        for gjobs in groups.values():
+            lkey = ("launch",) + tuple(id(j[0]) for j in gjobs)
             lp = cache.get(lkey)
             if lp is None:
-                lp = cache[lkey] = rt.LaunchPlan([j[0] for j in jobs], dev)
+                lp = cache[lkey] = rt.LaunchPlan([j[0] for j in gjobs], dev)
             structs = []
-            for ji, (ex, inp, out, act, bn, addend) in enumerate(jobs):
+            for ji, (ex, inp, out, act, bn, addend) in enumerate(gjobs):
                 slab = None
                 if bn is not None and rt.bn_mode(bn)[0]:
                     slab = torch.empty((lp.stat_rows(ji), ex.plan.M, 4), device=dev, dtype=torch.float32)
@@ -121,7 +124,7 @@ class _FFCExec:
                 structs.append(ex.job(inp, out, fused_act[0], fused_act[1], addend, slab))
                 if bn is not None:
                     post.append((out, act, bn, slab, lp.stat_rows(ji)))
-            lp.launch(structs, stream, flops=sum(j[0].flops for j in jobs))
+            lp.launch(structs, stream, flops=sum(j[0].flops for j in gjobs))
         for out, act, bn, slab, nrows in post:
             C = out.shape[1]
             if bn is not None:

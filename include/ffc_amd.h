@@ -40,7 +40,8 @@ extern "C" {
 
 const char* ffc_last_error(void);
 int ffc_abi_version(void);
-/* sizeof(ffc_conv_seg), sizeof(ffc_conv_phase), sizeof(ffc_conv_job) -> out[0..2] */
+/* sizeof(ffc_conv_seg), (ffc_conv_phase), (ffc_conv_job), (ffc_convp_seg), (ffc_convp_phase),
+ * (ffc_convp_job) -> out[0..5] */
 int ffc_struct_sizes(int* out, int n);
 
 /* ------------------------------------------------------------------ local branch
@@ -93,6 +94,55 @@ int ffc_conv_forward(const ffc_conv_job* jobs, int njobs, const int* tiles, int 
                      int tile_cfg, void* stream);
 /* number of BN slab rows each tile writes (waves along N) for a tile_cfg */
 int ffc_conv_stat_rows_per_tile(int tile_cfg);
+
+/* ---- LDS-patch variant (the hot path for FFCTranspose k4 s2 and strided convs) ----
+ * A workgroup owns one M-tile of 32 output channels x a pixel block (NS samples x TR x TC
+ * phase-grid pixels) x all phases.  For each 16-channel chunk of each segment the input patch
+ * the block needs (NS x 16 x PR x PC, zero outside the input) is staged once in LDS; every
+ * (phase, tap) B fragment is then read from that patch, so an input element is fetched from
+ * HBM/L2 once per block instead of once per (phase, tap).  Requires the taps per phase of each
+ * segment to divide 16 (ConvT k4 s2: 4; 1x1: 1; conv k4: 16).  A is packed with every
+ * segment's channels padded to a multiple of 16 (k = (seg, ch, tap)). */
+#define FFC_PATCH_CC 16
+typedef struct ffc_convp_seg {
+    const float* x;      /* (B, C, IH, IW), or (B, C, 2IH, 2IW) when pool=1 */
+    const float* gate;   /* optional (B, C) multiplier */
+    int C, Cpad, IH, IW;
+    int mult_y, mult_x;  /* input coord = m*mult + off */
+    int org_y, org_x;    /* patch origin relative to r0*mult_y / c0*mult_x (the minimum tap offset) */
+    int PR, PC;          /* patch rows / cols per channel */
+    int pool, pad_;
+} ffc_convp_seg;
+
+typedef struct ffc_convp_phase {
+    int py, px, PH, PW;
+    int Kpad;            /* sum over segments of Cpad * T[s] */
+    int T[FFC_MAX_SEG];  /* taps of each segment in this phase (each divides 16, or 0) */
+    int kseg[FFC_MAX_SEG];   /* k offset of each segment inside the phase's packed rows */
+    int tap_base[FFC_MAX_SEG];  /* offset of the segment's patch-relative tap offsets in taptab */
+    long long a_off;     /* float offset of the phase's packed weights [Mpad][Kpad] */
+} ffc_convp_phase;
+
+typedef struct ffc_convp_job {
+    ffc_convp_seg seg[FFC_MAX_SEG];
+    ffc_convp_phase ph[4];
+    const float* A;
+    const int* taptab;   /* patch-relative tap offsets (dy*PC + dx) */
+    float* out;
+    const float* bias;
+    const float* addend;
+    float* stats;        /* [pixel blocks * 4][M] float4 {n, mean, M2, 0}, or NULL */
+    int nseg, nphase;
+    int B, M, Mpad, OH, OW, Sy, Sx;
+    int NS, TR, TC, nrb, ncb;   /* pixel block: NS samples x TR rows x TC cols; row/col blocks per sample */
+    int act;
+    float act_param;
+} ffc_convp_job;
+
+/* tiles: int4 {job, m0, pixel block, 0}; cfg: 0 = 4 phases x 4 N-tiles/wave, 1 = 4 x 2,
+ * 2 = 1 phase x 2 N-tiles/wave, 3 = 1 x 1 */
+int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
+                      void* stream);
 
 /* Weight packing for one job: A[phase][Mpad][Kpad] (zero padded), bias_out[M] = sum of
  * segment biases.  w_layout[s]: 0 = Conv2d (O, I, kh, kw), 1 = ConvTranspose2d (I, O, kh, kw).

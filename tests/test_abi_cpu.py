@@ -35,9 +35,10 @@ def test_every_declared_symbol_is_exported():
 
 def test_struct_layout_matches_binding():
     lib = _lib.load()
-    out = (ctypes.c_int * 3)()
-    assert lib.ffc_struct_sizes(out, 3) == 0
-    assert tuple(out) == (ctypes.sizeof(_lib.ConvSeg), ctypes.sizeof(_lib.ConvPhase), ctypes.sizeof(_lib.ConvJob))
+    out = (ctypes.c_int * 6)()
+    assert lib.ffc_struct_sizes(out, 6) == 0
+    assert tuple(out) == (ctypes.sizeof(_lib.ConvSeg), ctypes.sizeof(_lib.ConvPhase), ctypes.sizeof(_lib.ConvJob),
+                          ctypes.sizeof(_lib.ConvPSeg), ctypes.sizeof(_lib.ConvPPhase), ctypes.sizeof(_lib.ConvPJob))
 
 
 def test_argument_validation_without_gpu():

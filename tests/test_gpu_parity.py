@@ -165,3 +165,19 @@ def test_graph_capture_replays():
         graph.replay()
         torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["kind"] in ("FFC_BN_ACT", "FFCGenerator")],
+                         ids=lambda c: c["name"])
+def test_golden_generic_conv_kernel(case):
+    """the same cases with the LDS-patch kernel disabled (generic phase-GEMM kernel)"""
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.USE_PATCH
+    rt.USE_PATCH = False
+    try:
+        state, inputs, data = load_case(case)
+        out = call_dropin(case, build_dropin(case, state), inputs)
+        for k, v in out.items():
+            assert normwise_err(v.cpu(), torch.from_numpy(data["ref." + k])) <= TOL, k
+    finally:
+        rt.USE_PATCH = old

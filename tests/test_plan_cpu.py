@@ -149,3 +149,82 @@ def test_tiles_cover_every_output_once(cfg):
 def test_rejects_mixed_strides():
     with pytest.raises(ValueError):
         _plan.plan_job(1, 4, [_plan.Seg("convT", 2, 4, 4, 4, 2, 1), _plan.Seg("conv", 2, 8, 8, 3, 1, 1)])
+
+
+def emulate_patch(plan, xs, ws, layouts):
+    """the LDS-patch kernel's index math: A from the packing table, B from taptab offsets"""
+    B, M = plan.B, plan.M
+    out = torch.zeros((B, M, plan.OH, plan.OW), dtype=torch.float64)
+    for ph in plan.phases:
+        K = ph["Kpad"]
+        ent = plan.ktab[ph["kt_off"]: ph["kt_off"] + K]
+        A = torch.zeros((M, K), dtype=torch.float64)
+        Bm = torch.zeros((K, B, ph["PH"], ph["PW"]), dtype=torch.float64)
+        my = torch.arange(ph["PH"])[:, None]
+        mx = torch.arange(ph["PW"])[None, :]
+        for s, sg in enumerate(plan.segs):
+            T = ph["T"][s]
+            PR, PC = plan.prc[s]
+            mul_y, mul_x = plan.mults[s]
+            x = F.avg_pool2d(xs[s], 2, 2) if sg.pool else xs[s]
+            for kk in range(plan.cpad[s] * T):
+                k = ph["kseg"][s] + kk
+                ch, t = divmod(kk, T)
+                sx, oy, ox, kyx = ent[k]
+                if ch >= sg.C:
+                    assert sx == 15
+                    continue
+                assert sx == (s | (ch << 4))
+                tt = plan.taptab[ph["tap_base"][s] + t]
+                dy, dx = divmod(int(tt), PC)
+                assert (dy, dx) == (oy - plan.org[s][0], ox - plan.org[s][1])
+                # every in-block pixel stays inside the patch
+                assert (plan.TR - 1) * mul_y + dy < PR and (plan.TC - 1) * mul_x + dx < PC
+                ky, kx = kyx & 0xFFFF, kyx >> 16
+                A[:, k] = ws[s][:, ch, ky, kx] if layouts[s] == 0 else ws[s][ch, :, ky, kx]
+                iy = my * mul_y + plan.org[s][0] + dy
+                ix = mx * mul_x + plan.org[s][1] + dx
+                valid = (iy >= 0) & (iy < sg.IH) & (ix >= 0) & (ix < sg.IW)
+                vals = x[:, ch][:, iy.clamp(0, sg.IH - 1), ix.clamp(0, sg.IW - 1)]
+                Bm[k] = torch.where(valid[None], vals, torch.zeros(()))
+        out[:, :, ph["py"]::plan.Sy, ph["px"]::plan.Sx] = torch.einsum("mk,kbyx->bmyx", A, Bm)
+    return out
+
+
+PATCH_CASES = {
+    "gen_ffc1_l": [_plan.Seg("convT", 20, 4, 4, 4, 2, 1), _plan.Seg("convT", 18, 4, 4, 4, 2, 1)],
+    "gen_ffc2_g": [_plan.Seg("convT", 17, 8, 8, 4, 2, 1), _plan.Seg("pw", 5, 16, 16)],
+    "gen_ffc4": [_plan.Seg("convT", 6, 32, 32, 4, 2, 1)],
+    "odd_sizes": [_plan.Seg("convT", 3, 5, 7, 4, 2, 1)],
+    "conv_k4s1p0": [_plan.Seg("conv", 5, 4, 4, 4, 1, 0)],
+    "pw_pool_gate_shape": [_plan.Seg("pw", 7, 4, 6, pool=True)],
+}
+
+
+@pytest.mark.parametrize("name", sorted(PATCH_CASES))
+@pytest.mark.parametrize("cfg", [None, 1, 3])
+def test_patch_plan_matches_torch(name, cfg):
+    segs = PATCH_CASES[name]
+    gen = torch.Generator().manual_seed(2)
+    B, M = 3, 7
+    plan = _plan.plan_patch_job(B, M, segs, cfg)
+    if plan is None:
+        pytest.skip("configuration not applicable to this job")
+    xs, ws, lays, ref = [], [], [], 0
+    for sg in segs:
+        x, w, lay = make(sg, B, M, gen)
+        xs.append(x)
+        ws.append(w)
+        lays.append(lay)
+        ref = ref + ref_out(sg, x, w)
+    got = emulate_patch(plan, xs, ws, lays)
+    assert torch.allclose(got, ref, atol=1e-10, rtol=1e-10)
+    tiles = _plan.build_patch_tiles([plan])
+    assert len({tuple(t) for t in tiles.tolist()}) == len(tiles) == plan.npb * (-(-M // 32))
+
+
+def test_generator_layers_use_patch_kernel():
+    for M, segs in [(128, [_plan.Seg("convT", 256, 4, 4, 4, 2, 1)] * 2),
+                    (64, [_plan.Seg("convT", 128, 8, 8, 4, 2, 1), _plan.Seg("pw", 32, 16, 16)]),
+                    (32, [_plan.Seg("convT", 64, 16, 16, 4, 2, 1), _plan.Seg("pw", 16, 32, 32)])]:
+        assert _plan.pick_patch_cfg(256, M, segs) is not None

@@ -16,11 +16,11 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step gpu_tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step gpu_tests 500 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300
+  step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 600 python bench.py --steps 50 --warmup 5 --cpu-seconds 10
+  step bench 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 10
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline
