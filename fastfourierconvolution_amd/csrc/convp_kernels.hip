@@ -17,15 +17,49 @@
 //   * v_mfma_f32_32x32x2_f32: exact fp32.  Lane half h of k-step s carries k = 16g + 8h + s.
 #include "ffc_internal.h"
 
+#include <string>
+
 namespace {
 
 constexpr int CC = FFC_PATCH_CC;  // channels per chunk
-constexpr int PMAX = 32;          // patch elements staged per thread (patch <= 256 * PMAX floats)
 
 struct ConvPArgs {
     ffc_convp_job jobs[2];
     const int4* tiles;
+    int ebuf;                      // floats per LDS patch buffer (multiple of 256)
 };
+
+__device__ float g_zero_src[64];   // source of the zero fill for out-of-bounds patch elements
+
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __forceinline__ unsigned magic_div(unsigned d) { return 0xFFFFFFFFu / d + 1u; }
+
+// Stage one 16-channel chunk of segment S into LDS `dst` with LDS-DMA (global_load_lds_dword):
+// element n of the patch image [ns][ch][pr][pc] comes from lane n % 64 of wave-instruction n / 64;
+// out-of-range elements read a zero word.  No VGPR staging, no branches.
+__device__ __forceinline__ void stage_chunk(const ffc_convp_seg& S, int NS, int B, int b0, int r0, int c0,
+                                            int ch0, float* dst, int tid, int wave) {
+    const int PR = S.PR, PC = S.PC;
+    const int E = NS * CC * PR * PC;
+    const unsigned mPC = magic_div((unsigned)PC), mPR = magic_div((unsigned)PR);
+    const int iy0 = r0 * S.mult_y + S.org_y, ix0 = c0 * S.mult_x + S.org_x;
+    const int nE = (E + 255) >> 8;
+    for (int e = 0; e < nE; ++e) {
+        const unsigned n = (unsigned)(e * 256 + tid);
+        const unsigned q1 = __umulhi(n, mPC);
+        const int pc = (int)(n - q1 * PC);
+        const unsigned q2 = __umulhi(q1, mPR);
+        const int pr = (int)(q1 - q2 * PR);
+        const int ns = (int)(q2 >> 4), ch = (int)(q2 & 15);
+        const int b = b0 + ns, c = ch0 + ch, iy = iy0 + pr, ix = ix0 + pc;
+        const bool ok = (int)n < E && b < B && c < S.C && (unsigned)iy < (unsigned)S.IH &&
+                        (unsigned)ix < (unsigned)S.IW;
+        const float* src = ok ? S.x + (((size_t)b * S.C + c) * S.IH + iy) * S.IW + ix : g_zero_src;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
+    }
+}
 
 template <int NP, int NTW>
 __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
@@ -45,6 +79,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
     const ffc_convp_job& J = args.jobs[ji];
     const int p = NP == 4 ? wave : 0;
     const ffc_convp_phase& P = J.ph[p];
+    const int ebuf = args.ebuf;
 
     const int NS = J.NS, TR = J.TR, TC = J.TC;
     const int bs = pb / (J.nrb * J.ncb);
@@ -76,63 +111,6 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 
     int nchunks = 0;
     for (int s = 0; s < J.nseg; ++s) nchunks += J.seg[s].Cpad / CC;
-
-    float st[PMAX];
-    // stage chunk (segment s, channels ch0..ch0+15) into registers
-    auto load_chunk = [&](int s, int ch0) {
-        const ffc_convp_seg& S = J.seg[s];
-        const int PR = S.PR, PC = S.PC;
-        const int E = NS * CC * PR * PC;
-        const int rpp = 256 / PC;               // rows covered per pass (PC <= 256 checked on host)
-        const int col = tid % PC;
-        const int rg = tid / PC;
-        const bool col_on = rg < rpp;
-        // row index R = rg + e*rpp over (ns, ch, pr) rows; track (pr, chn) incrementally
-        const int dq = rpp / PR, dr = rpp - (rpp / PR) * PR;
-        int pr = rg % PR, chn = rg / PR;
-        const int iy0 = r0 * S.mult_y + S.org_y, ix = c0 * S.mult_x + S.org_x + col;
-        const bool xin = (unsigned)ix < (unsigned)S.IW;
-#pragma unroll
-        for (int e = 0; e < PMAX; ++e) {
-            float v = 0.0f;
-            const int idx = (rg + e * rpp) * PC + col;
-            if (col_on && idx < E) {
-                const int ns = chn >> 4, ch = chn & 15;
-                const int b = b0 + ns, c = ch0 + ch, iy = iy0 + pr;
-                if (xin && b < J.B && c < S.C && (unsigned)iy < (unsigned)S.IH) {
-                    if (!S.pool) {
-                        v = S.x[(((size_t)b * S.C + c) * S.IH + iy) * S.IW + ix];
-                    } else {
-                        const int W2 = 2 * S.IW;
-                        const float* q = S.x + (((size_t)b * S.C + c) * (2 * S.IH) + 2 * iy) * W2 + 2 * ix;
-                        v = (((q[0] + q[1]) + q[W2]) + q[W2 + 1]) * 0.25f;
-                    }
-                    if (S.gate) v *= S.gate[(size_t)b * S.C + c];
-                }
-            }
-            st[e] = v;
-            pr += dr;
-            chn += dq;
-            if (pr >= PR) {
-                pr -= PR;
-                ++chn;
-            }
-        }
-    };
-    auto store_chunk = [&](int s) {
-        const ffc_convp_seg& S = J.seg[s];
-        const int PC = S.PC;
-        const int E = NS * CC * S.PR * PC;
-        const int rpp = 256 / PC;
-        const int col = tid % PC, rg = tid / PC;
-        if (rg < rpp) {
-#pragma unroll
-            for (int e = 0; e < PMAX; ++e) {
-                const int idx = (rg + e * rpp) * PC + col;
-                if (idx < E) patch[idx] = st[e];
-            }
-        }
-    };
     auto chunk_seg = [&](int ci, int& s, int& ch0) {
         s = 0;
         while (ci >= J.seg[s].Cpad / CC) {
@@ -145,51 +123,64 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
     {
         int s, ch0;
         chunk_seg(0, s, ch0);
-        load_chunk(s, ch0);
+        stage_chunk(J.seg[s], NS, J.B, b0, r0, c0, ch0, patch, tid, wave);
     }
     for (int ci = 0; ci < nchunks; ++ci) {
         int s, ch0;
         chunk_seg(ci, s, ch0);
-        __syncthreads();
-        store_chunk(s);
-        __syncthreads();
-        if (ci + 1 < nchunks) {
-            int s2, c2;
-            chunk_seg(ci + 1, s2, c2);
-            load_chunk(s2, c2);
-        }
+        __syncthreads();  // own LDS-DMA for chunk ci drained (vmcnt(0)) + everyone done with chunk ci-1
+        const float* cur = patch + (ci & 1) * ebuf;
         const int T = P.T[s];
-        if (T == 0) continue;
+        const float* __restrict__ Ap = J.A + P.a_off + (size_t)(m0 + cl) * P.Kpad + P.kseg[s] + ch0 * T + 8 * h;
         const ffc_convp_seg& S = J.seg[s];
         const int PRC = S.PR * S.PC;
         int loff[NTW];
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt)
             loff[nt] = pns[nt] * (CC * PRC) + pr_[nt] * S.mult_y * S.PC + pc_[nt] * S.mult_x;
-        const int lt = 31 - __builtin_clz(T);  // T is a power of two dividing 16
+        const int lt = T > 0 ? 31 - __builtin_clz(T) : 0;  // T is a power of two dividing 16
         int boff[8];
 #pragma unroll
         for (int s8 = 0; s8 < 8; ++s8) {
             const int k = 8 * h + s8;
-            boff[s8] = (k >> lt) * PRC + J.taptab[P.tap_base[s] + (k & (T - 1))];
+            boff[s8] = T > 0 ? (k >> lt) * PRC + J.taptab[P.tap_base[s] + (k & (T - 1))] : 0;
         }
         const int gstep = (16 >> lt) * PRC;
-        const float* __restrict__ Ap = J.A + P.a_off + (size_t)(m0 + cl) * P.Kpad + P.kseg[s] + ch0 * T + 8 * h;
-        float4 a0 = *reinterpret_cast<const float4*>(Ap);
-        float4 a1 = *reinterpret_cast<const float4*>(Ap + 4);
-        for (int g = 0; g < T; ++g) {
-            float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            if (g + 1 < T) {
-                a0 = *reinterpret_cast<const float4*>(Ap + 16 * (g + 1));
-                a1 = *reinterpret_cast<const float4*>(Ap + 16 * (g + 1) + 4);
+        // groups of 16 k in batches of 4: A of a batch goes to registers and is waited for BEFORE
+        // the next chunk's LDS-DMA is issued (so that DMA stays in flight under the MFMAs)
+        const int nb = T > 4 ? T : 4;
+        for (int gb = 0; gb < nb; gb += 4) {
+            floatx4 ar0[4], ar1[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+                if (gb + g < T) {
+                    x0 = *reinterpret_cast<const floatx4*>(Ap + 16 * (gb + g));
+                    x1 = *reinterpret_cast<const floatx4*>(Ap + 16 * (gb + g) + 4);
+                }
+                asm volatile("" : "+v"(x0), "+v"(x1));
+                ar0[g] = x0;
+                ar1[g] = x1;
             }
-            const int go = g * gstep;
+            if (gb == 0 && ci + 1 < nchunks) {
+                int s2, c2;
+                chunk_seg(ci + 1, s2, c2);
+                stage_chunk(J.seg[s2], NS, J.B, b0, r0, c0, c2, patch + ((ci + 1) & 1) * ebuf, tid, wave);
+            }
 #pragma unroll
-            for (int s8 = 0; s8 < 8; ++s8) {
+            for (int g = 0; g < 4; ++g) {
+                if (gb + g < T) {
+                    const float av[8] = {ar0[g][0], ar0[g][1], ar0[g][2], ar0[g][3],
+                                         ar1[g][0], ar1[g][1], ar1[g][2], ar1[g][3]};
+                    const int go = (gb + g) * gstep;
 #pragma unroll
-                for (int nt = 0; nt < NTW; ++nt) {
-                    const float bv = patch[loff[nt] + boff[s8] + go];
-                    acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
+                    for (int s8 = 0; s8 < 8; ++s8) {
+#pragma unroll
+                        for (int nt = 0; nt < NTW; ++nt) {
+                            const float bv = cur[loff[nt] + boff[s8] + go];
+                            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
+                        }
+                    }
                 }
             }
         }
@@ -241,20 +232,44 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
             if (cl == 0 && m < J.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
         }
     }
+    auto store = [&](auto actf) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int m = mbase + (r & 3) + 8 * (r >> 2);
-        if (m >= J.M) continue;
+        for (int r = 0; r < 16; ++r) {
+            const int m = mbase + (r & 3) + 8 * (r >> 2);
+            if (m < J.M) {
 #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-            if (pv[nt])
-                J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = ffc::apply_act(acc[nt][r], J.act, J.act_param);
+                for (int nt = 0; nt < NTW; ++nt)
+                    if (pv[nt]) J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = actf(acc[nt][r]);
+            }
+        }
+    };
+    const float ap = J.act_param;
+    switch (J.act) {
+        case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
+        case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
+        case FFC_ACT_TANH: store([](float v) { return tanhf(v); }); break;
+        case FFC_ACT_SIGMOID: store([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
+        case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
+        default: store([](float v) { return v; }); break;
     }
 }
 
 template <int NP, int NTW>
 int launch(const ConvPArgs& a, int ntiles, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((convp_kernel<NP, NTW>), dim3(ntiles), dim3(256), lds, s, a);
+    auto k = convp_kernel<NP, NTW>;
+    if (lds > 64 * 1024) {
+        static bool raised = false;  // per instantiation
+        if (!raised) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) {
+                ffc::set_error(std::string("ffc_convp_forward: hipFuncSetAttribute: ") + hipGetErrorString(e));
+                return FFC_E_LAUNCH;
+            }
+            raised = true;
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(ntiles), dim3(256), lds, s, a);
     return ffc::launch_status("ffc_convp_forward");
 }
 
@@ -275,10 +290,9 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
         for (int s = 0; s < J.nseg; ++s) {
             const ffc_convp_seg& S = J.seg[s];
             FFC_CHECK_ARG(S.x && S.Cpad % CC == 0 && S.Cpad >= S.C, "ffc_convp_forward: segment channels");
-            FFC_CHECK_ARG(S.PC > 0 && S.PC <= 256 && S.PR > 0, "ffc_convp_forward: patch shape");
+            FFC_CHECK_ARG(S.PC > 0 && S.PR > 0, "ffc_convp_forward: patch shape");
+            FFC_CHECK_ARG(!S.pool && !S.gate, "ffc_convp_forward: pooled / gated segments use ffc_conv_forward");
             const size_t E = (size_t)J.NS * CC * S.PR * S.PC;
-            const size_t rows = (size_t)J.NS * CC * S.PR;
-            FFC_CHECK_ARG(rows <= (size_t)(256 / S.PC) * PMAX, "ffc_convp_forward: patch exceeds staging registers");
             if (E > emax) emax = E;
             for (int p = 0; p < J.nphase; ++p) {
                 const int T = J.ph[p].T[s];
@@ -286,9 +300,11 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
             }
         }
     }
-    const size_t lds = emax * sizeof(float);
-    FFC_CHECK_ARG(lds <= 64 * 1024, "ffc_convp_forward: patch too large");
+    const size_t ebuf = (emax + 255) / 256 * 256;
+    const size_t lds = 2 * ebuf * sizeof(float);
+    FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_convp_forward: patch too large");
     ConvPArgs a;
+    a.ebuf = (int)ebuf;
     a.jobs[0] = jobs[0];
     a.jobs[1] = jobs[njobs > 1 ? 1 : 0];
     a.tiles = reinterpret_cast<const int4*>(tiles);
