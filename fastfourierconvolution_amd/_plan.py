@@ -40,6 +40,7 @@ class Seg:
     d: int = 1
     op: int = 0
     pool: bool = False
+    gate: bool = False   # a per-(sample, channel) multiplier is applied on load (SE gate)
 
 
 def conv_out(n, k, s, p, d):
@@ -276,6 +277,8 @@ class PatchPlan:
 def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
     """LDS-patch plan, or None when the job does not fit the patch kernel."""
     segs = tuple(segs)
+    if any(sg.pool or sg.gate for sg in segs):
+        return None                  # LDS-DMA staging copies bytes: no pooling / gating on the way in
     base = plan_job(B, M, segs)      # validates shapes, picks the phase stride
     NP = base.Sy * base.Sx
     if NP not in (1, 4) or len(base.phases) != NP:

@@ -111,7 +111,7 @@ class SpectralTransform(nn.Module):
         key = ("conv1", B, Cin, h2, w2, pool, str(dev))
         ex = self._cache.get(key)
         if ex is None:
-            seg = _plan.Seg("pw", Cin, h2, w2, pool=pool)
+            seg = _plan.Seg("pw", Cin, h2, w2, pool=pool, gate=True)
             ex = rt.ConvExec(B, c, [seg], [rt.conv_weight(self.conv1)], dev)
             lp = rt.LaunchPlan([ex], dev)
             self._cache[key] = ex = (ex, lp)

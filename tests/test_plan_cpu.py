@@ -197,7 +197,6 @@ PATCH_CASES = {
     "gen_ffc4": [_plan.Seg("convT", 6, 32, 32, 4, 2, 1)],
     "odd_sizes": [_plan.Seg("convT", 3, 5, 7, 4, 2, 1)],
     "conv_k4s1p0": [_plan.Seg("conv", 5, 4, 4, 4, 1, 0)],
-    "pw_pool_gate_shape": [_plan.Seg("pw", 7, 4, 6, pool=True)],
 }
 
 
