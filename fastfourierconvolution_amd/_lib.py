@@ -86,6 +86,11 @@ SIGNATURES = [
                                c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_fu_pack_mix", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_fu_lds_bytes", c_size_t, [c_int, c_int, c_int]),
+    ("ffc_st_prologue_lds_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    ("ffc_st_prologue", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
+                                      c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
 ]
 
 _lock = threading.Lock()

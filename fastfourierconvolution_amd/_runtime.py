@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib, _plan
-from ._lib import FFCError, check, ptr
+from ._lib import FFCError, check, ptr  # noqa: F401  (re-exported for the layers)
 
 # --------------------------------------------------------------------------- device / stream
 

@@ -1,0 +1,211 @@
+// Fused SpectralTransform prologue for gfx950: one workgroup per sample.
+//
+// Replaces, for one sample at a time (layers/ffc/spectral_transform.py:79-89):
+//   downsample (AvgPool2d(2) when pool=1; the x2 nearest Upsample commutes with everything
+//   here and is applied later inside the Fourier-unit loads)
+//   SELayer: gate = sigmoid(W2 relu(W1 mean_hw(x)))              (:12-28, hidden may be 0)
+//   conv1 (1x1, no bias) on gate * x  ->  t                      (:52-53, :89)
+//   per-sample BatchNorm partials {n, mean, M2} of t             (bn1, :57, :89)
+// The sample (Cin x h x w) and conv1's weight (transposed) live in LDS; conv1 runs on
+// v_mfma_f32_32x32x2_f32 with the gate folded into the B-fragment read.
+#include "ffc_internal.h"
+
+#include <mutex>
+#include <set>
+#include <string>
+
+namespace {
+
+struct StArgs {
+    const float* x;      // (B, Cin, H, W): H, W are the pre-pool dims when pool=1
+    const float* w1;     // se fc.0 (hid, Cin)
+    const float* w2;     // se fc.2 (Cin, hid)
+    const float* wc;     // conv1 (c, Cin)
+    float* t;            // (B, c, h, w)
+    float* slab;         // [B][c] float4
+    float* gate_out;     // optional (B, Cin) copy of the gate (tests / debugging), may be null
+    int Cin, H, W, pool, hid, c;
+};
+
+constexpr int ST_THREADS = 256;
+
+__global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Cin = a.Cin, c = a.c;
+    const int h = a.pool ? a.H / 2 : a.H, w = a.pool ? a.W / 2 : a.W;
+    const int hw = h * w;
+    const int Mpad = (c + 31) & ~31;
+    float* xs = sm;                      // [Cin][hw]
+    float* wt = xs + Cin * hw;           // [Cin][Mpad]  conv1 weight, transposed, zero padded
+    float* gate = wt + Cin * Mpad;       // [Cin]
+    float* hv = gate + Cin;              // [hid]
+    float* st = hv + ((a.hid + 3) & ~3); // [ntile][c][3]
+
+    // 1. sample -> LDS (2x2 average pool on the way in)
+    const float* xb = a.x + (size_t)b * Cin * a.H * a.W;
+    if (!a.pool) {
+        const int n = Cin * hw;
+        if ((n & 3) == 0) {
+            for (int i = tid; i < n / 4; i += ST_THREADS)
+                reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xb)[i];
+        } else {
+            for (int i = tid; i < n; i += ST_THREADS) xs[i] = xb[i];
+        }
+    } else {
+        for (int i = tid; i < Cin * hw; i += ST_THREADS) {
+            const int ch = i / hw, r = i - ch * hw, yy = r / w, xx = r - yy * w;
+            const float* q = xb + ((size_t)ch * a.H + 2 * yy) * a.W + 2 * xx;
+            xs[i] = (((q[0] + q[1]) + q[a.W]) + q[a.W + 1]) * 0.25f;
+        }
+    }
+    for (int i = tid; i < Cin * Mpad; i += ST_THREADS) {
+        const int k = i / Mpad, o = i - k * Mpad;
+        wt[i] = o < c ? a.wc[(size_t)o * Cin + k] : 0.0f;
+    }
+    __syncthreads();
+
+    // 2. SE gate
+    for (int ch = wave; ch < Cin; ch += ST_THREADS / 64) {
+        float s = 0.0f;
+        for (int i = lane; i < hw; i += 64) s += xs[ch * hw + i];
+        s = ffc::wave_sum(s);
+        if (lane == 0) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
+    }
+    __syncthreads();
+    for (int j = tid; j < a.hid; j += ST_THREADS) {
+        float s = 0.0f;
+        for (int k = 0; k < Cin; ++k) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
+        hv[j] = fmaxf(s, 0.0f);
+    }
+    __syncthreads();
+    float g = 0.0f;
+    if (tid < Cin) {
+        float s = 0.0f;
+        for (int j = 0; j < a.hid; ++j) s = fmaf(a.w2[(size_t)tid * a.hid + j], hv[j], s);
+        g = 1.0f / (1.0f + expf(-s));
+    }
+    for (int k0 = 0; k0 < Cin; k0 += ST_THREADS) {  // Cin may exceed the block
+        const int k = k0 + tid;
+        float gk = g;
+        if (k0 > 0 && k < Cin) {
+            float s = 0.0f;
+            for (int j = 0; j < a.hid; ++j) s = fmaf(a.w2[(size_t)k * a.hid + j], hv[j], s);
+            gk = 1.0f / (1.0f + expf(-s));
+        }
+        __syncthreads();
+        if (k < Cin) {
+            gate[k] = gk;
+            if (a.gate_out) a.gate_out[(size_t)b * Cin + k] = gk;
+        }
+    }
+    __syncthreads();
+
+    // 3. conv1: t[o][p] = sum_k W[o][k] gate[k] x[k][p] on MFMA; lane half h carries k = 2s + h
+    const int h2 = lane >> 5, col = lane & 31;
+    const int MT = Mpad / 32, NT = (hw + 31) / 32;
+    for (int tile = wave; tile < MT * NT; tile += ST_THREADS / 64) {
+        const int mt = tile % MT, nt = tile / MT;
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        const int p = nt * 32 + col;
+        const int pc = p < hw ? p : hw - 1;
+        for (int s = 0; s < Cin / 2; ++s) {
+            const int k = 2 * s + h2;
+            const float av = wt[k * Mpad + mt * 32 + col];
+            const float bv = xs[k * hw + pc] * gate[k];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+        if (Cin & 1) {  // odd Cin: last channel in slot 0, zero in slot 1
+            const int k = Cin - 1;
+            const float av = h2 == 0 ? wt[k * Mpad + mt * 32 + col] : 0.0f;
+            const float bv = h2 == 0 ? xs[k * hw + pc] * gate[k] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+        const bool valid = p < hw;
+        const float cnt = (float)min(32, hw - nt * 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+            const float v = acc[r];
+            if (valid && o < c) a.t[((size_t)b * c + o) * hw + p] = v;
+            const float mean = ffc::half_wave_sum(valid ? v : 0.0f) / cnt;
+            const float d = valid ? v - mean : 0.0f;
+            const float m2 = ffc::half_wave_sum(d * d);
+            if (col == 0 && o < c) {
+                float* e = st + (nt * c + o) * 3;
+                e[0] = cnt;
+                e[1] = mean;
+                e[2] = m2;
+            }
+        }
+    }
+    __syncthreads();
+    for (int o = tid; o < c; o += ST_THREADS) {
+        float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+        for (int nt = 0; nt < NT; ++nt) {
+            const float* e = st + (nt * c + o) * 3;
+            const float tot = nn + e[0];
+            const float delta = e[1] - mean;
+            mean += delta * (e[0] / tot);
+            m2 += e[2] + delta * delta * (nn * e[0] / tot);
+            nn = tot;
+        }
+        reinterpret_cast<float4*>(a.slab)[(size_t)b * c + o] = make_float4(nn, mean, m2, 0.0f);
+    }
+}
+
+size_t st_lds(int Cin, int H, int W, int pool, int hid, int c) {
+    const int h = pool ? H / 2 : H, w = pool ? W / 2 : W;
+    const size_t hw = (size_t)h * w;
+    const size_t Mpad = (size_t)((c + 31) & ~31);
+    const size_t nt = (hw + 31) / 32;
+    return sizeof(float) * (Cin * hw + Cin * Mpad + Cin + ((hid + 3) & ~3) + nt * c * 3);
+}
+
+}  // namespace
+
+extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c) {
+    if (Cin <= 0 || H <= 0 || W <= 0 || c <= 0 || hidden < 0) return 0;
+    if (pool && ((H | W) & 1)) return 0;
+    const size_t b = st_lds(Cin, H, W, pool, hidden, c);
+    return b <= 160 * 1024 ? b : 0;
+}
+
+extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
+                               const float* w2, int hidden, const float* wconv1, int c, float* t, float* slab,
+                               float* gate_out, void* stream) {
+    FFC_CHECK_ARG(x && wconv1 && t && slab && B > 0, "ffc_st_prologue: bad args");
+    FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_st_prologue: null SE weights");
+    const size_t lds = ffc_st_prologue_lds_bytes(Cin, H, W, pool, hidden, c);
+    FFC_CHECK_ARG(lds > 0, "ffc_st_prologue: sample does not fit in LDS (use se_gate + conv)");
+    if (lds > 64 * 1024) {
+        static std::once_flag once;
+        static hipError_t err = hipSuccess;
+        std::call_once(once, [] {
+            err = hipFuncSetAttribute(reinterpret_cast<const void*>(st_prologue_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        });
+        if (err != hipSuccess) {
+            ffc::set_error(std::string("ffc_st_prologue: hipFuncSetAttribute: ") + hipGetErrorString(err));
+            return FFC_E_LAUNCH;
+        }
+    }
+    StArgs a;
+    a.x = x;
+    a.w1 = w1;
+    a.w2 = w2;
+    a.wc = wconv1;
+    a.t = t;
+    a.slab = slab;
+    a.gate_out = gate_out;
+    a.Cin = Cin;
+    a.H = H;
+    a.W = W;
+    a.pool = pool;
+    a.hid = hidden;
+    a.c = c;
+    hipLaunchKernelGGL(st_prologue_kernel, dim3(B), dim3(ST_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_st_prologue");
+}

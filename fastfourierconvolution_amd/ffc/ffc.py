@@ -93,6 +93,10 @@ class _FFCExec:
                 outs[name] = out
                 post.append((out, act, bn, None, 0))
                 continue
+            if self._smallm_ok(segs, w, addend, bn, M):
+                out = self._smallm(segs, w, inp, act, M, B, dev, stream)
+                outs[name] = out
+                continue
             key = (name, B, tuple(segs), str(dev))
             cache = self._ffc_cache()
             ex = cache.get(key)
@@ -137,6 +141,30 @@ class _FFCExec:
                 sh = torch.zeros(C, device=dev, dtype=torch.float32)
             rt.bn_act_apply(out, sc, sh, act[0], act[1])
         return outs["l"], outs["g"]
+
+    @staticmethod
+    def _smallm_ok(segs, w, addend, bn, M):
+        """ConvT k4 s2 p1 into <= 4 channels (the generator's last layer) -> direct VALU kernel"""
+        if addend is not None or bn is not None or M is None or M > 4 or not 1 <= len(segs) <= 2:
+            return False
+        if sum(1 for x in w if x[4] is not None) > 1:
+            return False
+        return all(sg.kind == "convT" and (sg.k, sg.s, sg.p, sg.d, sg.op) == (4, 2, 1, 1, 0) and
+                   sg.IH == segs[0].IH and sg.IW == segs[0].IW for sg in segs)
+
+    def _smallm(self, segs, w, inp, act, M, B, dev, stream):
+        IH, IW = segs[0].IH, segs[0].IW
+        out = torch.empty((B, M, 2 * IH, 2 * IW), device=dev, dtype=torch.float32)
+        x1 = inp[1][0] if len(inp) > 1 else None
+        w1 = w[1][0] if len(w) > 1 else None
+        bias = next((x[4] for x in w if x[4] is not None), None)
+        flops = 2.0 * B * M * sum(sg.C for sg in segs) * 4 * (2 * IH) * (2 * IW)
+        with rt.observe("convt_smallm", flops=flops):
+            rt.check(rt.lib().ffc_convt_k4s2_smallm(
+                inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(), rt.ptr(x1), segs[1].C if x1 is not None else 0,
+                rt.ptr(w1), rt.ptr(bias), B, IH, IW, M, out.data_ptr(), act[0], act[1], stream),
+                "ffc_convt_k4s2_smallm")
+        return out
 
     def _bn_from_tensor(self, bn, out, stream):
         """batch statistics of a pass-through branch (no GEMM epilogue to collect them)"""

@@ -107,24 +107,35 @@ class SpectralTransform(nn.Module):
         c = self.conv1.out_channels
         dev = x.device
         stream = rt.stream_of(x)
-        gate = self.se_block.gate(x, pool)
-        key = ("conv1", B, Cin, h2, w2, pool, str(dev))
-        ex = self._cache.get(key)
-        if ex is None:
-            seg = _plan.Seg("pw", Cin, h2, w2, pool=pool, gate=True)
-            ex = rt.ConvExec(B, c, [seg], [rt.conv_weight(self.conv1)], dev)
-            lp = rt.LaunchPlan([ex], dev)
-            self._cache[key] = ex = (ex, lp)
-        ex, lp = ex
-        ex.ensure_packed([rt.conv_weight(self.conv1)])
         use_batch, _ = rt.bn_mode(self.bn1)
+        L = rt.lib()
+        hid = self.se_block.fc[0].out_features
         t = torch.empty((B, c, h2, w2), device=dev, dtype=torch.float32)
-        slab = None
-        if use_batch:
-            slab = torch.empty((lp.stat_rows(0), c, 4), device=dev, dtype=torch.float32)
-        lp.launch([ex.job([(x, gate)], t, stats=slab)], stream, flops=ex.flops)
-        sc1, sh1 = rt.bn_scale_shift(self.bn1, c, slab, lp.stat_rows(0) if use_batch else 0, float(up * up), dev,
-                                     stream)
+        if L.ffc_st_prologue_lds_bytes(Cin, H, W, int(pool), hid, c) > 0:
+            # one fused launch: [pool] -> SE gate -> conv1 -> per-sample BN1 partials
+            w1 = rt.require(self.se_block.fc[0].weight.detach(), "se.fc.0.weight") if hid > 0 else None
+            w2 = rt.require(self.se_block.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None
+            wc = rt.require(self.conv1.weight.detach(), "conv1.weight")
+            slab = torch.empty((B, c, 4), device=dev, dtype=torch.float32)
+            with rt.observe("st_prologue", flops=2.0 * B * c * Cin * h2 * w2):
+                check(L.ffc_st_prologue(ptr(x), B, Cin, H, W, int(pool), ptr(w1), ptr(w2), hid, ptr(wc), c, ptr(t),
+                                        ptr(slab), None, stream), "ffc_st_prologue")
+            nrows = B
+        else:
+            gate = self.se_block.gate(x, pool)
+            key = ("conv1", B, Cin, h2, w2, pool, str(dev))
+            ex = self._cache.get(key)
+            if ex is None:
+                seg = _plan.Seg("pw", Cin, h2, w2, pool=pool, gate=True)
+                ex = rt.ConvExec(B, c, [seg], [rt.conv_weight(self.conv1)], dev)
+                lp = rt.LaunchPlan([ex], dev)
+                self._cache[key] = ex = (ex, lp)
+            ex, lp = ex
+            ex.ensure_packed([rt.conv_weight(self.conv1)])
+            nrows = lp.stat_rows(0)
+            slab = torch.empty((nrows, c, 4), device=dev, dtype=torch.float32) if use_batch else None
+            lp.launch([ex.job([(x, gate)], t, stats=slab)], stream, flops=ex.flops)
+        sc1, sh1 = rt.bn_scale_shift(self.bn1, c, slab, nrows if use_batch else 0, float(up * up), dev, stream)
         return self.fu._run(t, up=up, in_scale=sc1, in_shift=sh1, in_relu=True, residual=True)
 
     def forward(self, x, y=None):

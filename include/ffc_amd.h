@@ -178,6 +178,22 @@ int ffc_bn_act_apply(const float* x, float* y, int B, int C, int HW, const float
 int ffc_se_gate(const float* x, int B, int C, int H, int W, int pool, const float* w1,
                 const float* w2, int hidden, float* gate, void* stream);
 
+/* Fused SpectralTransform prologue, one workgroup per sample (spectral_transform.py:79-89):
+ * [2x2 avg pool] -> SE gate -> conv1 (1x1, (c, Cin) weight) -> t (B, c, h, w) and per-sample BN1
+ * partials slab [B][c] float4 {n, mean, M2}.  gate_out (B, Cin) optional.  Needs the sample and
+ * conv1's weight in LDS: ffc_st_prologue_lds_bytes() == 0 means "use ffc_se_gate + conv". */
+size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c);
+int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
+                    const float* w2, int hidden, const float* wconv1, int c, float* t, float* slab,
+                    float* gate_out, void* stream);
+
+/* Direct ConvTranspose2d(k=4, s=2, p=1) for M <= 4 output channels (the generator's last
+ * layer, models/ffc_generator.py:28): out = act(conv_t(x0; w0) [+ conv_t(x1; w1)] + bias).
+ * w*: raw ConvTranspose2d weights (C, M, 4, 4); x1/w1 may be NULL. */
+int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                          const float* w1, const float* bias, int B, int IH, int IW, int M,
+                          float* out, int act, float act_param, void* stream);
+
 /* Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56), fused per sample:
  *   s   = in_relu ? relu(t*in_scale + in_shift) : t, nearest-upsampled by `up` (1|2)
  *         (SpectralTransform's bn1/act1 + Upsample, spectral_transform.py:44-45,79,89)

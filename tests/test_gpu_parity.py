@@ -181,3 +181,27 @@ def test_golden_generic_conv_kernel(case):
             assert normwise_err(v.cpu(), torch.from_numpy(data["ref." + k])) <= TOL, k
     finally:
         rt.USE_PATCH = old
+
+
+@pytest.mark.parametrize("M,H,W,bias", [(1, 5, 7, True), (2, 32, 32, False), (4, 3, 40, True), (3, 64, 16, False)])
+def test_smallm_convt_vs_oracle(M, H, W, bias):
+    """direct VALU ConvT k4 s2 p1 path (M <= 4): odd sizes, tiles wider than 32, bias"""
+    import fastfourierconvolution_amd as F
+    from oracle.ffc_oracle import ffc_bn_act
+    cfg = dict(in_channels=40, out_channels=M, kernel_size=4, ratio_gin=0.5, ratio_gout=0.0, stride=2, padding=1,
+               bias=bias, activation_layer="Tanh", upsampling=True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = F.FFC_BN_ACT(40, M, 4, 0.5, 0.0, 2, 1, bias=bias, activation_layer=torch.nn.Tanh, upsampling=True)
+    gen = torch.Generator().manual_seed(M)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn(p.shape, generator=gen) * 0.2)
+    sd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in m.state_dict().items()}
+    xl = torch.randn(3, 20, H, W, generator=gen)
+    xg = torch.randn(3, 20, H, W, generator=gen)
+    m = m.cuda()
+    with torch.no_grad():
+        ol, og = m((xl.cuda(), xg.cuda()))
+        rl, rg = ffc_bn_act((xl.double(), xg.double()), sd, "", cfg, True)
+    assert og == 0 and rg == 0
+    assert normwise_err(ol.cpu(), rl) <= TOL
