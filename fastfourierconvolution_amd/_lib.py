@@ -85,6 +85,7 @@ SIGNATURES = [
     ("ffc_fu_forward", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_fu_pack_mix", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_pack_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_fu_lds_bytes", c_size_t, [c_int, c_int, c_int]),
     ("ffc_st_prologue_lds_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     ("ffc_st_prologue", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,

@@ -32,7 +32,8 @@ struct SmallMArgs {
 };
 
 template <int MM>
-__global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a) {
+__global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a, const float* __restrict__ wseg0,
+                                                           const float* __restrict__ wseg1) {
     extern __shared__ __attribute__((aligned(16))) float patch[];
     const int tid = threadIdx.x, wave = tid >> 6;
     const int TRw = a.TRw, TCw = a.TCw;
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a) {
         const int s = ci < nch0 ? 0 : 1;
         const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
         const int cn = min(CCH, a.C[s] - c0);
-        const float* __restrict__ w = a.w[s];
+        const float* __restrict__ w = s == 0 ? wseg0 : wseg1;
         for (int cc = 0; cc < cn; ++cc) {
             const float* p = cur + (cc * PR + qy + 1) * PC + qx + 1;
             float v[3][3];
@@ -89,7 +90,8 @@ __global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a) {
             for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
                 for (int dx = -1; dx <= 1; ++dx) v[dy + 1][dx + 1] = p[dy * PC + dx];
-            const float* wc = w + (size_t)(c0 + cc) * a.M * 16;
+            // wave-uniform weight address in SGPRs -> scalar (s_load) weight reads
+            const float* wc = w + __builtin_amdgcn_readfirstlane((c0 + cc) * a.M * 16);
 #pragma unroll
             for (int m = 0; m < MM; ++m) {
                 if (m < a.M) {
@@ -166,6 +168,7 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, c
     const size_t lds = 2 * (size_t)((PE + 255) & ~255) * sizeof(float);
     FFC_CHECK_ARG(lds <= 64 * 1024, "ffc_convt_k4s2_smallm: tile too large");
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
-    hipLaunchKernelGGL(convt_smallm_kernel<4>, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(convt_smallm_kernel<4>, dim3(grid), dim3(256), lds, (hipStream_t)stream, a, w0,
+                       x1 ? w1 : w0);
     return ffc::launch_status("ffc_convt_k4s2_smallm");
 }

@@ -296,11 +296,12 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     }
 }
 
-__global__ void fu_pack_mix_kernel(const float* __restrict__ w, int C2, int Mpad, float* __restrict__ wt) {
+// out[k][o] = w[o][k] for o < R (zero for R <= o < Rpad); w is (R, K) row-major
+__global__ void pack_transpose_kernel(const float* __restrict__ w, int R, int K, int Rpad, float* __restrict__ wt) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= C2 * Mpad) return;
-    const int i = idx / Mpad, o = idx - i * Mpad;
-    wt[idx] = (o < C2) ? w[(size_t)o * C2 + i] : 0.0f;
+    if (idx >= K * Rpad) return;
+    const int k = idx / Rpad, o = idx - k * Rpad;
+    wt[idx] = (o < R) ? w[(size_t)o * K + k] : 0.0f;
 }
 
 typedef void (*FuKernel)(FuArgs);
@@ -392,11 +393,15 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
     return ffc::launch_status("ffc_fu_forward");
 }
 
+extern "C" int ffc_pack_transpose(const float* w, int R, int K, float* wT, void* stream) {
+    FFC_CHECK_ARG(w && wT && R > 0 && K > 0, "ffc_pack_transpose: bad args");
+    const int Rpad = (R + 31) / 32 * 32;
+    const int n = K * Rpad;
+    hipLaunchKernelGGL(pack_transpose_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, R, K,
+                       Rpad, wT);
+    return ffc::launch_status("ffc_pack_transpose");
+}
+
 extern "C" int ffc_fu_pack_mix(const float* w, int C2, float* wmixT, void* stream) {
-    FFC_CHECK_ARG(w && wmixT && C2 > 0, "ffc_fu_pack_mix: bad args");
-    const int Mpad = (C2 + 31) / 32 * 32;
-    const int n = C2 * Mpad;
-    hipLaunchKernelGGL(fu_pack_mix_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, C2, Mpad,
-                       wmixT);
-    return ffc::launch_status("ffc_fu_pack_mix");
+    return ffc_pack_transpose(w, C2, C2, wmixT, stream);
 }

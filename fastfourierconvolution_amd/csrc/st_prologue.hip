@@ -6,7 +6,7 @@
 //   SELayer: gate = sigmoid(W2 relu(W1 mean_hw(x)))              (:12-28, hidden may be 0)
 //   conv1 (1x1, no bias) on gate * x  ->  t                      (:52-53, :89)
 //   per-sample BatchNorm partials {n, mean, M2} of t             (bn1, :57, :89)
-// The sample (Cin x h x w) and conv1's weight (transposed) live in LDS; conv1 runs on
+// The sample (Cin x h x w) lives in LDS, conv1's pre-transposed weight streams from L2; conv1 runs on
 // v_mfma_f32_32x32x2_f32 with the gate folded into the B-fragment read.
 #include "ffc_internal.h"
 
@@ -20,7 +20,7 @@ struct StArgs {
     const float* x;      // (B, Cin, H, W): H, W are the pre-pool dims when pool=1
     const float* w1;     // se fc.0 (hid, Cin)
     const float* w2;     // se fc.2 (Cin, hid)
-    const float* wc;     // conv1 (c, Cin)
+    const float* wcT;    // conv1 weight transposed + zero padded: (Cin, Mpad), Mpad = ceil32(c)
     float* t;            // (B, c, h, w)
     float* slab;         // [B][c] float4
     float* gate_out;     // optional (B, Cin) copy of the gate (tests / debugging), may be null
@@ -37,8 +37,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     const int hw = h * w;
     const int Mpad = (c + 31) & ~31;
     float* xs = sm;                      // [Cin][hw]
-    float* wt = xs + Cin * hw;           // [Cin][Mpad]  conv1 weight, transposed, zero padded
-    float* gate = wt + Cin * Mpad;       // [Cin]
+    float* gate = xs + Cin * hw;         // [Cin]
     float* hv = gate + Cin;              // [hid]
     float* st = hv + ((a.hid + 3) & ~3); // [ntile][c][3]
 
@@ -59,10 +58,6 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
             xs[i] = (((q[0] + q[1]) + q[a.W]) + q[a.W + 1]) * 0.25f;
         }
     }
-    for (int i = tid; i < Cin * Mpad; i += ST_THREADS) {
-        const int k = i / Mpad, o = i - k * Mpad;
-        wt[i] = o < c ? a.wc[(size_t)o * Cin + k] : 0.0f;
-    }
     __syncthreads();
 
     // 2. SE gate
@@ -73,10 +68,11 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         if (lane == 0) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
     }
     __syncthreads();
-    for (int j = tid; j < a.hid; j += ST_THREADS) {
+    for (int j = wave; j < a.hid; j += ST_THREADS / 64) {  // fc1: one wave per hidden unit
         float s = 0.0f;
-        for (int k = 0; k < Cin; ++k) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
-        hv[j] = fmaxf(s, 0.0f);
+        for (int k = lane; k < Cin; k += 64) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
+        s = ffc::wave_sum(s);
+        if (lane == 0) hv[j] = fmaxf(s, 0.0f);
     }
     __syncthreads();
     float g = 0.0f;
@@ -113,13 +109,13 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         const int pc = p < hw ? p : hw - 1;
         for (int s = 0; s < Cin / 2; ++s) {
             const int k = 2 * s + h2;
-            const float av = wt[k * Mpad + mt * 32 + col];
+            const float av = a.wcT[(size_t)k * Mpad + mt * 32 + col];
             const float bv = xs[k * hw + pc] * gate[k];
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
         }
         if (Cin & 1) {  // odd Cin: last channel in slot 0, zero in slot 1
             const int k = Cin - 1;
-            const float av = h2 == 0 ? wt[k * Mpad + mt * 32 + col] : 0.0f;
+            const float av = h2 == 0 ? a.wcT[(size_t)k * Mpad + mt * 32 + col] : 0.0f;
             const float bv = h2 == 0 ? xs[k * hw + pc] * gate[k] : 0.0f;
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
         }
@@ -159,9 +155,8 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
 size_t st_lds(int Cin, int H, int W, int pool, int hid, int c) {
     const int h = pool ? H / 2 : H, w = pool ? W / 2 : W;
     const size_t hw = (size_t)h * w;
-    const size_t Mpad = (size_t)((c + 31) & ~31);
     const size_t nt = (hw + 31) / 32;
-    return sizeof(float) * (Cin * hw + Cin * Mpad + Cin + ((hid + 3) & ~3) + nt * c * 3);
+    return sizeof(float) * (Cin * hw + Cin + ((hid + 3) & ~3) + nt * c * 3);
 }
 
 }  // namespace
@@ -174,9 +169,9 @@ extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int
 }
 
 extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
-                               const float* w2, int hidden, const float* wconv1, int c, float* t, float* slab,
+                               const float* w2, int hidden, const float* wconv1T, int c, float* t, float* slab,
                                float* gate_out, void* stream) {
-    FFC_CHECK_ARG(x && wconv1 && t && slab && B > 0, "ffc_st_prologue: bad args");
+    FFC_CHECK_ARG(x && wconv1T && t && slab && B > 0, "ffc_st_prologue: bad args");
     FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_st_prologue: null SE weights");
     const size_t lds = ffc_st_prologue_lds_bytes(Cin, H, W, pool, hidden, c);
     FFC_CHECK_ARG(lds > 0, "ffc_st_prologue: sample does not fit in LDS (use se_gate + conv)");
@@ -196,7 +191,7 @@ extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int
     a.x = x;
     a.w1 = w1;
     a.w2 = w2;
-    a.wc = wconv1;
+    a.wcT = wconv1T;
     a.t = t;
     a.slab = slab;
     a.gate_out = gate_out;

@@ -84,6 +84,17 @@ class SpectralTransform(nn.Module):
         self._cache = {}
 
     # ------------------------------------------------------------------ internals
+    def _conv1_T(self, stream):
+        """conv1 weight transposed + zero padded for ffc_st_prologue (re-packed when it changes)"""
+        w = rt.require(self.conv1.weight.detach(), "conv1.weight")
+        key = (w.data_ptr(), w._version)
+        if self.__dict__.get("_c1key") != key:
+            c, cin = w.shape[0], w.shape[1]
+            self._c1T = torch.empty((cin, -(-c // 32) * 32), device=w.device, dtype=torch.float32)
+            check(rt.lib().ffc_pack_transpose(ptr(w), c, cin, ptr(self._c1T), stream), "ffc_pack_transpose")
+            self.__dict__["_c1key"] = key
+        return self._c1T
+
     def _mode(self):
         if self.stride == 2 and self.upsample:
             return 1, 2  # pool, up
@@ -113,12 +124,12 @@ class SpectralTransform(nn.Module):
         t = torch.empty((B, c, h2, w2), device=dev, dtype=torch.float32)
         if L.ffc_st_prologue_lds_bytes(Cin, H, W, int(pool), hid, c) > 0:
             # one fused launch: [pool] -> SE gate -> conv1 -> per-sample BN1 partials
-            w1 = rt.require(self.se_block.fc[0].weight.detach(), "se.fc.0.weight") if hid > 0 else None
-            w2 = rt.require(self.se_block.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None
-            wc = rt.require(self.conv1.weight.detach(), "conv1.weight")
+            se1 = rt.require(self.se_block.fc[0].weight.detach(), "se.fc.0.weight") if hid > 0 else None
+            se2 = rt.require(self.se_block.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None
+            wc = self._conv1_T(stream)
             slab = torch.empty((B, c, 4), device=dev, dtype=torch.float32)
             with rt.observe("st_prologue", flops=2.0 * B * c * Cin * h2 * w2):
-                check(L.ffc_st_prologue(ptr(x), B, Cin, H, W, int(pool), ptr(w1), ptr(w2), hid, ptr(wc), c, ptr(t),
+                check(L.ffc_st_prologue(ptr(x), B, Cin, H, W, int(pool), ptr(se1), ptr(se2), hid, ptr(wc), c, ptr(t),
                                         ptr(slab), None, stream), "ffc_st_prologue")
             nrows = B
         else:

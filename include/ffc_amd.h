@@ -179,13 +179,16 @@ int ffc_se_gate(const float* x, int B, int C, int H, int W, int pool, const floa
                 const float* w2, int hidden, float* gate, void* stream);
 
 /* Fused SpectralTransform prologue, one workgroup per sample (spectral_transform.py:79-89):
- * [2x2 avg pool] -> SE gate -> conv1 (1x1, (c, Cin) weight) -> t (B, c, h, w) and per-sample BN1
- * partials slab [B][c] float4 {n, mean, M2}.  gate_out (B, Cin) optional.  Needs the sample and
- * conv1's weight in LDS: ffc_st_prologue_lds_bytes() == 0 means "use ffc_se_gate + conv". */
+ * [2x2 avg pool] -> SE gate -> conv1 (1x1) -> t (B, c, h, w) and per-sample BN1 partials
+ * slab [B][c] float4 {n, mean, M2}.  wconv1T: conv1 weight transposed by ffc_pack_transpose
+ * ((Cin, ceil32(c))).  gate_out (B, Cin) optional.  The sample must fit in LDS:
+ * ffc_st_prologue_lds_bytes() == 0 means "use ffc_se_gate + conv". */
 size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c);
 int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
-                    const float* w2, int hidden, const float* wconv1, int c, float* t, float* slab,
+                    const float* w2, int hidden, const float* wconv1T, int c, float* t, float* slab,
                     float* gate_out, void* stream);
+/* wT[k][o] = w[o][k] for a row-major (R, K) matrix, o zero-padded to ceil32(R) */
+int ffc_pack_transpose(const float* w, int R, int K, float* wT, void* stream);
 
 /* Direct ConvTranspose2d(k=4, s=2, p=1) for M <= 4 output channels (the generator's last
  * layer, models/ffc_generator.py:28): out = act(conv_t(x0; w0) [+ conv_t(x1; w1)] + bias).
