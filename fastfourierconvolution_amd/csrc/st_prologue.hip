@@ -25,6 +25,7 @@ struct StArgs {
     float* slab;         // [B][c] float4
     float* gate_out;     // optional (B, Cin) copy of the gate (tests / debugging), may be null
     int Cin, H, W, pool, hid, c;
+    int wt_lds;          // conv1 weight staged in LDS
 };
 
 constexpr int ST_THREADS = 256;
@@ -37,9 +38,11 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     const int hw = h * w;
     const int Mpad = (c + 31) & ~31;
     float* xs = sm;                      // [Cin][hw]
-    float* gate = xs + Cin * hw;         // [Cin]
-    float* hv = gate + Cin;              // [hid]
+    float* gate = xs + ((Cin * hw + 3) & ~3);  // [Cin]
+    float* hv = gate + ((Cin + 3) & ~3); // [hid]
     float* st = hv + ((a.hid + 3) & ~3); // [ntile][c][3]
+    float* red = st + (((hw + 31) / 32) * c * 3 + 3) / 4 * 4;   // [4 waves][16][64] split-K partials
+    float* wt = red + 4 * 16 * 64;       // [Cin][Mpad] conv1 weight (when it fits)
 
     // 1. sample -> LDS (2x2 average pool on the way in)
     const float* xb = a.x + (size_t)b * Cin * a.H * a.W;
@@ -57,6 +60,11 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
             const float* q = xb + ((size_t)ch * a.H + 2 * yy) * a.W + 2 * xx;
             xs[i] = (((q[0] + q[1]) + q[a.W]) + q[a.W + 1]) * 0.25f;
         }
+    }
+    if (a.wt_lds) {  // pre-transposed (Cin, Mpad) weight: plain coalesced copy
+        const int n4 = Cin * Mpad / 4;
+        for (int i = tid; i < n4; i += ST_THREADS)
+            reinterpret_cast<float4*>(wt)[i] = reinterpret_cast<const float4*>(a.wcT)[i];
     }
     __syncthreads();
 
@@ -97,28 +105,37 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     }
     __syncthreads();
 
-    // 3. conv1: t[o][p] = sum_k W[o][k] gate[k] x[k][p] on MFMA; lane half h carries k = 2s + h
+    // 3. conv1: t[o][p] = sum_k W[o][k] gate[k] x[k][p] on MFMA; lane half h carries k = 2s + h.
+    //    With fewer than 4 output tiles the K range is split over the idle waves (LDS reduction).
     const int h2 = lane >> 5, col = lane & 31;
     const int MT = Mpad / 32, NT = (hw + 31) / 32;
-    for (int tile = wave; tile < MT * NT; tile += ST_THREADS / 64) {
-        const int mt = tile % MT, nt = tile / MT;
+    const int tiles = MT * NT;
+    const int nsplit = tiles >= 4 ? 1 : 4 / tiles;
+    const int KS = Cin / 2;
+    const float* wa = a.wt_lds ? wt : a.wcT;
+    auto mfma_range = [&](int mt, int nt, int s0, int s1, bool odd_tail) {
         floatx16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
         const int p = nt * 32 + col;
         const int pc = p < hw ? p : hw - 1;
-        for (int s = 0; s < Cin / 2; ++s) {
+        const float* ap = wa + mt * 32 + col;
+        const float* xp = xs + pc;
+#pragma unroll 4
+        for (int s = s0; s < s1; ++s) {
             const int k = 2 * s + h2;
-            const float av = a.wcT[(size_t)k * Mpad + mt * 32 + col];
-            const float bv = xs[k * hw + pc] * gate[k];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[(size_t)k * Mpad], xp[k * hw] * gate[k], acc, 0, 0, 0);
         }
-        if (Cin & 1) {  // odd Cin: last channel in slot 0, zero in slot 1
+        if (odd_tail && (Cin & 1)) {  // odd Cin: last channel in slot 0, zero in slot 1
             const int k = Cin - 1;
-            const float av = h2 == 0 ? a.wcT[(size_t)k * Mpad + mt * 32 + col] : 0.0f;
-            const float bv = h2 == 0 ? xs[k * hw + pc] * gate[k] : 0.0f;
+            const float av = h2 == 0 ? ap[(size_t)k * Mpad] : 0.0f;
+            const float bv = h2 == 0 ? xp[k * hw] * gate[k] : 0.0f;
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
         }
+        return acc;
+    };
+    auto finish = [&](int mt, int nt, const floatx16& acc) {
+        const int p = nt * 32 + col;
         const bool valid = p < hw;
         const float cnt = (float)min(32, hw - nt * 32);
 #pragma unroll
@@ -136,6 +153,29 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
                 e[2] = m2;
             }
         }
+    };
+    if (nsplit == 1) {
+        for (int tile = wave; tile < tiles; tile += ST_THREADS / 64) {
+            const int mt = tile % MT, nt = tile / MT;
+            finish(mt, nt, mfma_range(mt, nt, 0, KS, true));
+        }
+    } else {
+        const int tile = wave / nsplit, part = wave % nsplit;
+        const int mt = tile % MT, nt = tile / MT;
+        const int per = (KS + nsplit - 1) / nsplit;
+        floatx16 acc;
+        if (tile < tiles) acc = mfma_range(mt, nt, min(KS, part * per), min(KS, (part + 1) * per), part == 0);
+        if (tile < tiles && part > 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
+        }
+        __syncthreads();
+        if (tile < tiles && part == 0) {
+            for (int q = 1; q < nsplit; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] += red[((wave + q) * 16 + r) * 64 + lane];
+            finish(mt, nt, acc);
+        }
     }
     __syncthreads();
     for (int o = tid; o < c; o += ST_THREADS) {
@@ -152,11 +192,13 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     }
 }
 
-size_t st_lds(int Cin, int H, int W, int pool, int hid, int c) {
+size_t st_lds(int Cin, int H, int W, int pool, int hid, int c, bool with_w) {
     const int h = pool ? H / 2 : H, w = pool ? W / 2 : W;
     const size_t hw = (size_t)h * w;
     const size_t nt = (hw + 31) / 32;
-    return sizeof(float) * (Cin * hw + Cin + ((hid + 3) & ~3) + nt * c * 3);
+    const size_t Mpad = (size_t)((c + 31) & ~31);
+    return sizeof(float) * (((Cin * hw + 3) & ~(size_t)3) + ((Cin + 3) & ~3) + ((hid + 3) & ~3) + (nt * c * 3 + 3) / 4 * 4 + 4 * 16 * 64 +
+                            (with_w ? Cin * Mpad : 0));
 }
 
 }  // namespace
@@ -164,7 +206,9 @@ size_t st_lds(int Cin, int H, int W, int pool, int hid, int c) {
 extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c) {
     if (Cin <= 0 || H <= 0 || W <= 0 || c <= 0 || hidden < 0) return 0;
     if (pool && ((H | W) & 1)) return 0;
-    const size_t b = st_lds(Cin, H, W, pool, hidden, c);
+    const size_t bw = st_lds(Cin, H, W, pool, hidden, c, true);
+    if (bw <= 160 * 1024) return bw;
+    const size_t b = st_lds(Cin, H, W, pool, hidden, c, false);
     return b <= 160 * 1024 ? b : 0;
 }
 
@@ -201,6 +245,7 @@ extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int
     a.pool = pool;
     a.hid = hidden;
     a.c = c;
+    a.wt_lds = st_lds(Cin, H, W, pool, hidden, c, true) <= 160 * 1024;
     hipLaunchKernelGGL(st_prologue_kernel, dim3(B), dim3(ST_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_st_prologue");
 }
