@@ -43,7 +43,7 @@ class ConvJob(ctypes.Structure):
 class ConvPSeg(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("gate", c_void_p), ("C", c_int), ("Cpad", c_int), ("IH", c_int), ("IW", c_int),
                 ("mult_y", c_int), ("mult_x", c_int), ("org_y", c_int), ("org_x", c_int), ("PR", c_int),
-                ("PC", c_int), ("pool", c_int), ("pad_", c_int)]
+                ("PC", c_int), ("pool", c_int), ("direct", c_int)]
 
 
 class ConvPPhase(ctypes.Structure):
@@ -102,9 +102,11 @@ class FFCError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH):
-    """Load libffc_amd.so (no GPU needed).  Raises if it is missing."""
+def load(path: str | None = None):
+    """Load libffc_amd.so (no GPU needed).  Raises if it is missing.  FFC_LIB_PATH overrides the
+    in-tree library (A/B benchmarking of kernel variants)."""
     global _lib
+    path = path or os.environ.get("FFC_LIB_PATH") or LIB_PATH
     with _lock:
         if _lib is not None:
             return _lib

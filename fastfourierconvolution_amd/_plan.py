@@ -304,7 +304,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
             ty = _taps(sg, base.Sy, ph.py, sg.IH, ph.PH)
             tx = _taps(sg, base.Sx, ph.px, sg.IW, ph.PW)
             T = len(ty) * len(tx)
-            if T and 16 % T:
+            if T and 4 % T:
                 return None
             row.append((ty, tx))
         taps.append(row)
@@ -318,7 +318,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         oy0, ox0 = min(oys), min(oxs)
         PR = (TR - 1) * my_ + (max(oys) - oy0) + 1
         PC = (TC - 1) * mx_ + (max(oxs) - ox0) + 1
-        if PC > 256 or NS * PATCH_CC * PR > (256 // PC) * PATCH_PMAX or NS * PATCH_CC * PR * PC > 16384:
+        if NS * PATCH_CC * PR * PC > 16384:
             return None
         org.append((oy0, ox0))
         prc.append((PR, PC))

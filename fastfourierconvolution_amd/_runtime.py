@@ -271,6 +271,7 @@ class ConvExec:
             s.org_y, s.org_x = pl.org[i]
             s.PR, s.PC = pl.prc[i]
             s.pool = int(sg.pool)
+            s.direct = 0
         for i, ph in enumerate(pl.phases):
             p = job.ph[i]
             p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]

@@ -56,7 +56,7 @@ __device__ __forceinline__ void stage_chunk(const ffc_convp_seg& S, int NS, int 
         const int b = b0 + ns, c = ch0 + ch, iy = iy0 + pr, ix = ix0 + pc;
         const bool ok = (int)n < E && b < B && c < S.C && (unsigned)iy < (unsigned)S.IH &&
                         (unsigned)ix < (unsigned)S.IW;
-        const float* src = ok ? S.x + (((size_t)b * S.C + c) * S.IH + iy) * S.IW + ix : g_zero_src;
+        const float* src = ok ? S.x + (unsigned)(((b * S.C + c) * S.IH + iy) * S.IW + ix) : g_zero_src;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
     }
 }
@@ -119,67 +119,75 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         }
         ch0 = ci * CC;
     };
-
-    {
+    // A (16-k groups, T <= 4 per chunk) of chunk ci into registers (not waited for here)
+    auto load_A = [&](int ci, floatx4 (&a0)[4], floatx4 (&a1)[4]) {
         int s, ch0;
-        chunk_seg(0, s, ch0);
-        stage_chunk(J.seg[s], NS, J.B, b0, r0, c0, ch0, patch, tid, wave);
-    }
+        chunk_seg(ci, s, ch0);
+        const int T = P.T[s];
+        const float* __restrict__ Ap = J.A + P.a_off + (size_t)(m0 + cl) * P.Kpad + P.kseg[s] + ch0 * T + 8 * h;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (g < T) {
+                a0[g] = *reinterpret_cast<const floatx4*>(Ap + 16 * g);
+                a1[g] = *reinterpret_cast<const floatx4*>(Ap + 16 * g + 4);
+            } else {
+                a0[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+                a1[g] = a0[g];
+            }
+        }
+    };
+    auto stage = [&](int ci) {
+        int s, ch0;
+        chunk_seg(ci, s, ch0);
+        stage_chunk(J.seg[s], NS, J.B, b0, r0, c0, ch0, patch + (ci & 1) * ebuf, tid, wave);
+    };
+    floatx4 a0[4], a1[4], n0[4], n1[4];
+    stage(0);
+    load_A(0, n0, n1);
     for (int ci = 0; ci < nchunks; ++ci) {
         int s, ch0;
         chunk_seg(ci, s, ch0);
-        __syncthreads();  // own LDS-DMA for chunk ci drained (vmcnt(0)) + everyone done with chunk ci-1
-        const float* cur = patch + (ci & 1) * ebuf;
+        __syncthreads();  // patch + A of chunk ci landed (vmcnt(0)); everyone is done with chunk ci-1
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            a0[g] = n0[g];
+            a1[g] = n1[g];
+            asm volatile("" : "+v"(a0[g]), "+v"(a1[g]));
+        }
+        if (ci + 1 < nchunks) {  // next chunk's A and patch stay in flight under this chunk's MFMAs
+            load_A(ci + 1, n0, n1);
+            stage(ci + 1);
+        }
         const int T = P.T[s];
-        const float* __restrict__ Ap = J.A + P.a_off + (size_t)(m0 + cl) * P.Kpad + P.kseg[s] + ch0 * T + 8 * h;
+        if (T == 0) continue;
         const ffc_convp_seg& S = J.seg[s];
+        const int lt = 31 - __builtin_clz(T);  // T is a power of two dividing 4
+        const float* cur = patch + (ci & 1) * ebuf;
         const int PRC = S.PR * S.PC;
         int loff[NTW];
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt)
             loff[nt] = pns[nt] * (CC * PRC) + pr_[nt] * S.mult_y * S.PC + pc_[nt] * S.mult_x;
-        const int lt = T > 0 ? 31 - __builtin_clz(T) : 0;  // T is a power of two dividing 16
         int boff[8];
 #pragma unroll
         for (int s8 = 0; s8 < 8; ++s8) {
             const int k = 8 * h + s8;
-            boff[s8] = T > 0 ? (k >> lt) * PRC + J.taptab[P.tap_base[s] + (k & (T - 1))] : 0;
+            boff[s8] = (k >> lt) * PRC + J.taptab[P.tap_base[s] + (k & (T - 1))];
         }
         const int gstep = (16 >> lt) * PRC;
-        // groups of 16 k in batches of 4: A of a batch goes to registers and is waited for BEFORE
-        // the next chunk's LDS-DMA is issued (so that DMA stays in flight under the MFMAs)
-        const int nb = T > 4 ? T : 4;
-        for (int gb = 0; gb < nb; gb += 4) {
-            floatx4 ar0[4], ar1[4];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
-                if (gb + g < T) {
-                    x0 = *reinterpret_cast<const floatx4*>(Ap + 16 * (gb + g));
-                    x1 = *reinterpret_cast<const floatx4*>(Ap + 16 * (gb + g) + 4);
-                }
-                asm volatile("" : "+v"(x0), "+v"(x1));
-                ar0[g] = x0;
-                ar1[g] = x1;
-            }
-            if (gb == 0 && ci + 1 < nchunks) {
-                int s2, c2;
-                chunk_seg(ci + 1, s2, c2);
-                stage_chunk(J.seg[s2], NS, J.B, b0, r0, c0, c2, patch + ((ci + 1) & 1) * ebuf, tid, wave);
-            }
+        for (int g = 0; g < 4; ++g) {
+            if (g < T) {
+                const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3], a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
+                int go = g * gstep;
+                asm volatile("" : "+s"(go));  // keep the per-group LDS addresses from being hoisted (VGPRs)
+                const float* cg = cur + go;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                if (gb + g < T) {
-                    const float av[8] = {ar0[g][0], ar0[g][1], ar0[g][2], ar0[g][3],
-                                         ar1[g][0], ar1[g][1], ar1[g][2], ar1[g][3]};
-                    const int go = (gb + g) * gstep;
+                for (int s8 = 0; s8 < 8; ++s8) {
 #pragma unroll
-                    for (int s8 = 0; s8 < 8; ++s8) {
-#pragma unroll
-                        for (int nt = 0; nt < NTW; ++nt) {
-                            const float bv = cur[loff[nt] + boff[s8] + go];
-                            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
-                        }
+                    for (int nt = 0; nt < NTW; ++nt) {
+                        const float bv = cg[loff[nt] + boff[s8]];
+                        acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
                     }
                 }
             }
@@ -296,11 +304,11 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
             if (E > emax) emax = E;
             for (int p = 0; p < J.nphase; ++p) {
                 const int T = J.ph[p].T[s];
-                FFC_CHECK_ARG(T >= 0 && T <= 16 && (T == 0 || (16 % T) == 0), "ffc_convp_forward: taps must divide 16");
+                FFC_CHECK_ARG(T >= 0 && T <= 4 && (T == 0 || (4 % T) == 0), "ffc_convp_forward: taps must divide 4");
             }
         }
     }
-    const size_t ebuf = (emax + 255) / 256 * 256;
+    const size_t ebuf = (emax + 255) / 256 * 256 + 256;
     const size_t lds = 2 * ebuf * sizeof(float);
     FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_convp_forward: patch too large");
     ConvPArgs a;

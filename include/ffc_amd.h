@@ -101,8 +101,8 @@ int ffc_conv_stat_rows_per_tile(int tile_cfg);
  * the block needs (NS x 16 x PR x PC, zero outside the input) is staged once in LDS; every
  * (phase, tap) B fragment is then read from that patch, so an input element is fetched from
  * HBM/L2 once per block instead of once per (phase, tap).  Requires the taps per phase of each
- * segment to divide 16 (ConvT k4 s2: 4; 1x1: 1; conv k4: 16).  A is packed with every
- * segment's channels padded to a multiple of 16 (k = (seg, ch, tap)). */
+ * segment to divide 4 (ConvT k4 s2: 4; 1x1: 1).  A is packed with every segment's channels
+ * padded to a multiple of 16 (k = (seg, ch, tap)). */
 #define FFC_PATCH_CC 16
 typedef struct ffc_convp_seg {
     const float* x;      /* (B, C, IH, IW), or (B, C, 2IH, 2IW) when pool=1 */
@@ -111,7 +111,8 @@ typedef struct ffc_convp_seg {
     int mult_y, mult_x;  /* input coord = m*mult + off */
     int org_y, org_x;    /* patch origin relative to r0*mult_y / c0*mult_x (the minimum tap offset) */
     int PR, PC;          /* patch rows / cols per channel */
-    int pool, pad_;
+    int pool;
+    int direct;          /* 1x1 segment read straight from global memory (no LDS patch) */
 } ffc_convp_seg;
 
 typedef struct ffc_convp_phase {
