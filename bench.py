@@ -90,10 +90,10 @@ def main():
     cpu_state = {k: v.clone() for k, v in G.state_dict().items()}
     G = G.to(dev).train(args.bn_mode == "train")
     if world > 1:
-        for t in G.state_dict().values():
-            dist.broadcast(t, 0)
+        from fastfourierconvolution_amd import distributed as D
+        D.broadcast_module(G)           # weights + BN buffers from rank 0, once
         if args.bn_mode == "train":
-            rt.set_sync_bn_group(dist.group.WORLD)
+            D.enable_sync_bn()          # the only data-path exchange: BN moments all-reduce
     gen = torch.Generator(device="cpu").manual_seed(100 + rank)
     z_cpu = torch.randn((args.batch, args.nz, 1, 1), generator=gen)
     z = z_cpu.to(dev)

@@ -93,7 +93,7 @@ _SYNC = {"group": None}
 
 def set_sync_bn_group(group):
     """Route train-mode BN moments through torch.distributed.all_reduce (RCCL) over ``group``
-    (None disables).  Set by fastfourierconvolution_amd.distributed.shard_batch users."""
+    (None disables).  See fastfourierconvolution_amd.distributed.enable_sync_bn."""
     _SYNC["group"] = group
 
 
@@ -137,9 +137,9 @@ def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: flo
                                                int(update), momentum, float(bn.eps), float(count_mult), ptr(scale),
                                                ptr(shift), stream), "ffc_bn_reduce_finalize")
         else:
-            import torch.distributed as dist
+            from .distributed import merge_moments
             check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(moments), stream), "ffc_bn_reduce")
-            dist.all_reduce(moments, group=grp)
+            merge_moments(moments, group=grp)
             check(L.ffc_bn_finalize(ptr(moments), C, gamma, beta, rm, rv, nbt, 1, int(update), momentum,
                                     float(bn.eps), float(count_mult), ptr(scale), ptr(shift), stream),
                   "ffc_bn_finalize")
@@ -271,7 +271,7 @@ class ConvExec:
             s.org_y, s.org_x = pl.org[i]
             s.PR, s.PC = pl.prc[i]
             s.pool = int(sg.pool)
-            s.direct = 0
+            s.reserved_ = 0
         for i, ph in enumerate(pl.phases):
             p = job.ph[i]
             p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]

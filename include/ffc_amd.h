@@ -112,13 +112,13 @@ typedef struct ffc_convp_seg {
     int org_y, org_x;    /* patch origin relative to r0*mult_y / c0*mult_x (the minimum tap offset) */
     int PR, PC;          /* patch rows / cols per channel */
     int pool;
-    int direct;          /* 1x1 segment read straight from global memory (no LDS patch) */
+    int reserved_;       /* must be 0 */
 } ffc_convp_seg;
 
 typedef struct ffc_convp_phase {
     int py, px, PH, PW;
     int Kpad;            /* sum over segments of Cpad * T[s] */
-    int T[FFC_MAX_SEG];  /* taps of each segment in this phase (each divides 16, or 0) */
+    int T[FFC_MAX_SEG];  /* taps of each segment in this phase (1, 2 or 4, or 0) */
     int kseg[FFC_MAX_SEG];   /* k offset of each segment inside the phase's packed rows */
     int tap_base[FFC_MAX_SEG];  /* offset of the segment's patch-relative tap offsets in taptab */
     long long a_off;     /* float offset of the phase's packed weights [Mpad][Kpad] */

@@ -205,3 +205,51 @@ def test_smallm_convt_vs_oracle(M, H, W, bias):
         rl, rg = ffc_bn_act((xl.double(), xg.double()), sd, "", cfg, True)
     assert og == 0 and rg == 0
     assert normwise_err(ol.cpu(), rl) <= TOL
+
+
+def _w_sharded_gpu(rank, port, out_dir):
+    """one rank of a 2-way sample shard on cuda:0 (gloo carries the BN moments; RCCL needs one
+    GPU per rank, which the 1-GPU test box does not have)"""
+    import os
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import fastfourierconvolution_amd.distributed as D
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    g, _ = _gen_state(100, 3, 64, seed=21 + rank)   # rank 1 starts from different weights ...
+    g = g.cuda().train()
+    D.broadcast_module(g)                            # ... and receives rank 0's
+    D.enable_sync_bn()
+    z = torch.randn((10, 100, 1, 1), generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        out = g(D.shard_batch(z).cuda())
+    torch.save({"out": out.cpu(), "sd": {k: v.cpu() for k, v in g.state_dict().items()}},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    D.disable_sync_bn()
+    dist.destroy_process_group()
+
+
+def test_sharded_syncbn_gpu(tmp_path):
+    """N>1 data path through the HIP kernels: a ragged 2-way shard (5+5 of B=10) with SyncBN
+    equals the single-process global-batch forward, running statistics included."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_w_sharded_gpu, args=(port, str(tmp_path)), nprocs=2, join=True)
+    g, _ = _gen_state(100, 3, 64, seed=21)
+    g = g.cuda().train()
+    z = torch.randn((10, 100, 1, 1), generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        ref = g(z.cuda()).cpu()
+    rs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(2)]
+    got = torch.cat([r["out"] for r in rs], dim=0)
+    assert normwise_err(got, ref) <= TOL
+    gsd = g.state_dict()
+    for r in rs:
+        for k, v in gsd.items():
+            if "running" in k:
+                np.testing.assert_allclose(r["sd"][k].numpy(), v.cpu().numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
+            elif k.endswith("num_batches_tracked"):
+                assert int(r["sd"][k]) == int(v), k

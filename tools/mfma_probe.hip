@@ -94,6 +94,8 @@ int main() {
     constexpr int IT = 256;
     const double f32 = 4.0 * 8 * IT * 2.0 * 32 * 32 * 2;   // per wave: NT*8*IT MFMAs x 4096 flop; x4 waves
     for (int blocks : {256, 512, 1024, 2048}) {
+        run("32x32x2 regs NT=1", probe32<0, 1, IT>, blocks, 4 * 8.0 * IT * 1 * 4096);
+        run("32x32x2 regs NT=2", probe32<0, 2, IT>, blocks, 4 * 8.0 * IT * 2 * 4096);
         run("32x32x2 regs NT=4", probe32<0, 4, IT>, blocks, 4 * 8.0 * IT * 4 * 4096);
         run("32x32x2 lds  NT=4", probe32<1, 4, IT>, blocks, 4 * 8.0 * IT * 4 * 4096);
         run("32x32x2 lds  NT=2", probe32<1, 2, IT>, blocks, 4 * 8.0 * IT * 2 * 4096);
