@@ -43,7 +43,7 @@ class ConvJob(ctypes.Structure):
 class ConvPSeg(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("gate", c_void_p), ("C", c_int), ("Cpad", c_int), ("IH", c_int), ("IW", c_int),
                 ("mult_y", c_int), ("mult_x", c_int), ("org_y", c_int), ("org_x", c_int), ("PR", c_int),
-                ("PC", c_int), ("pool", c_int), ("reserved_", c_int)]
+                ("PC", c_int), ("pool", c_int), ("vec4", c_int)]
 
 
 class ConvPPhase(ctypes.Structure):

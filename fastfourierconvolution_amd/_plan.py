@@ -254,6 +254,8 @@ class PatchPlan:
     cpad: list
     org: list            # per segment (org_y, org_x)
     prc: list            # per segment (PR, PC)
+    vec4: list           # per segment: staged in 16-byte groups (IW % 4 == 0)
+    rowlen: list         # per segment: LDS patch row length in floats (PC, or whole 4-float groups)
     phases: list         # dicts: py, px, PH, PW, T[s], kseg[s], tap_base[s], Kpad, a_off, kt_off, K
     ktab: np.ndarray     # packing table (same format as JobPlan.ktab)
     taptab: np.ndarray   # int32 patch-relative tap offsets
@@ -272,6 +274,17 @@ class PatchPlan:
     @property
     def npb(self):
         return -(-self.B // self.NS) * self.nrb * self.ncb
+
+
+PATCH_MAX_UNITS = 8 * 256   # staging units per chunk (convp_kernels.hip NEMAX x 256 threads)
+
+
+def patch_units_per_row(PC: int, vec4: bool, aligned: bool = False) -> int:
+    """staging units per patch row: 4-float groups covering PC columns from the row start rounded
+    down to a multiple of 4 (by up to 3 columns unless every block's start is aligned), or floats"""
+    if not vec4:
+        return PC
+    return -(-PC // 4) if aligned else (PC + 6) // 4
 
 
 def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
@@ -308,7 +321,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
                 return None
             row.append((ty, tx))
         taps.append(row)
-    org, prc = [], []
+    org, prc, vec4, rowlen = [], [], [], []
     for si, sg in enumerate(segs):
         oys = [o for row in taps for (k, o) in row[si][0]]
         oxs = [o for row in taps for (k, o) in row[si][1]]
@@ -318,8 +331,12 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         oy0, ox0 = min(oys), min(oxs)
         PR = (TR - 1) * my_ + (max(oys) - oy0) + 1
         PC = (TC - 1) * mx_ + (max(oxs) - ox0) + 1
-        if NS * PATCH_CC * PR * PC > 16384:
+        v4 = sg.IW % 4 == 0
+        al = ox0 % 4 == 0 and (TC * mx_) % 4 == 0
+        if NS * PATCH_CC * PR * patch_units_per_row(PC, v4, al) > PATCH_MAX_UNITS:
             return None
+        vec4.append(v4)
+        rowlen.append(4 * patch_units_per_row(PC, True, al) if v4 else PC)
         org.append((oy0, ox0))
         prc.append((PR, PC))
     phases, ktab, taptab = [], [], []
@@ -338,7 +355,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
             PR, PC = prc[si]
             for (ky, oy) in ty:
                 for (kx, ox) in tx:
-                    taptab.append((oy - org[si][0]) * PC + (ox - org[si][1]))
+                    taptab.append(((oy - org[si][0]) << 16) | (ox - org[si][1]))
             for ch in range(cpad[si]):
                 for (ky, oy) in ty:
                     for (kx, ox) in tx:
@@ -352,7 +369,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         d["a_off"] = a_total
         a_total += Mpad * k
         phases.append(d)
-    return PatchPlan(B, M, base.OH, base.OW, base.Sy, base.Sx, segs, base.mults, cpad, org, prc, phases,
+    return PatchPlan(B, M, base.OH, base.OW, base.Sy, base.Sx, segs, base.mults, cpad, org, prc, vec4, rowlen, phases,
                      np.asarray(ktab, dtype=np.int32).reshape(-1, 4), np.asarray(taptab or [0], dtype=np.int32),
                      a_total, cfg, NS, TR, TC, nrb, ncb)
 
@@ -361,7 +378,7 @@ def pick_patch_cfg(B, M, segs):
     """4-phase jobs: NTW=4 unless that leaves fewer than ~2 workgroups per CU."""
     p = plan_patch_job(B, M, segs)
     if p is None:
-        return None
+        return plan_patch_job(B, M, segs, 1)   # a smaller pixel block may still fit the staging limits
     if p.cfg == 0:
         blocks = p.npb * (-(-M // 32))
         if blocks < 512:

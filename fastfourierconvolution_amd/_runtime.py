@@ -225,7 +225,8 @@ class ConvExec:
             self.taptab = None
         self.device = device
         self.ktab = torch.from_numpy(self.plan.ktab.copy()).to(device)
-        self.A = torch.empty(max(1, self.plan.a_size), device=device, dtype=torch.float32)
+        # + tail padding: the patch kernel loads all 4 tap groups of a chunk, used or not
+        self.A = torch.zeros(max(1, self.plan.a_size) + 256, device=device, dtype=torch.float32)
         self.has_bias = any(w[4] is not None for w in weights)
         self.bias = torch.empty(M, device=device, dtype=torch.float32) if self.has_bias else None
         self._packed = None
@@ -269,9 +270,9 @@ class ConvExec:
             s.C, s.Cpad, s.IH, s.IW = sg.C, pl.cpad[i], sg.IH, sg.IW
             s.mult_y, s.mult_x = pl.mults[i]
             s.org_y, s.org_x = pl.org[i]
-            s.PR, s.PC = pl.prc[i]
+            s.PR, s.PC = pl.prc[i][0], pl.rowlen[i]
             s.pool = int(sg.pool)
-            s.reserved_ = 0
+            s.vec4 = int(pl.vec4[i])
         for i, ph in enumerate(pl.phases):
             p = job.ph[i]
             p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]
@@ -301,6 +302,8 @@ class ConvExec:
     def job(self, inputs, out, act=0, act_param=0.0, addend=None, stats=None):
         job = self.base_job()
         for i, (x, gate) in enumerate(inputs):
+            if self.kind == "patch" and self.plan.vec4[i] and x.data_ptr() % 16:
+                raise FFCError("patch conv: input segment is not 16-byte aligned")
             job.seg[i].x = x.data_ptr()
             job.seg[i].gate = ptr(gate)
         job.out = out.data_ptr()

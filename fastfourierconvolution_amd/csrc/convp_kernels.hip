@@ -31,35 +31,40 @@ struct ConvPArgs {
 
 __device__ float g_zero_src[64];   // source of the zero fill for out-of-bounds patch elements
 
+#ifdef FFC_TRACE
+// Diagnostic build only (tools/trace_convp.py): per workgroup {realtime start, end, HW_ID | XCC_ID << 32,
+// wave-0 cycles in barrier / staging issue / MFMA section, total cycles, chunks}.
+__device__ unsigned long long g_ffc_trace[8 * 4096];
+#define FFC_STAMP(t)                                                                        \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    } while (0)
+#endif
+
 typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 __device__ __forceinline__ unsigned magic_div(unsigned d) { return 0xFFFFFFFFu / d + 1u; }
 
-// Stage one 16-channel chunk of segment S into LDS `dst` with LDS-DMA (global_load_lds_dword):
-// element n of the patch image [ns][ch][pr][pc] comes from lane n % 64 of wave-instruction n / 64;
-// out-of-range elements read a zero word.  No VGPR staging, no branches.
-__device__ __forceinline__ void stage_chunk(const ffc_convp_seg& S, int NS, int B, int b0, int r0, int c0,
-                                            int ch0, float* dst, int tid, int wave) {
-    const int PR = S.PR, PC = S.PC;
-    const int E = NS * CC * PR * PC;
-    const unsigned mPC = magic_div((unsigned)PC), mPR = magic_div((unsigned)PR);
-    const int iy0 = r0 * S.mult_y + S.org_y, ix0 = c0 * S.mult_x + S.org_x;
-    const int nE = (E + 255) >> 8;
-    for (int e = 0; e < nE; ++e) {
-        const unsigned n = (unsigned)(e * 256 + tid);
-        const unsigned q1 = __umulhi(n, mPC);
-        const int pc = (int)(n - q1 * PC);
-        const unsigned q2 = __umulhi(q1, mPR);
-        const int pr = (int)(q1 - q2 * PR);
-        const int ns = (int)(q2 >> 4), ch = (int)(q2 & 15);
-        const int b = b0 + ns, c = ch0 + ch, iy = iy0 + pr, ix = ix0 + pc;
-        const bool ok = (int)n < E && b < B && c < S.C && (unsigned)iy < (unsigned)S.IH &&
-                        (unsigned)ix < (unsigned)S.IW;
-        const float* src = ok ? S.x + (unsigned)(((b * S.C + c) * S.IH + iy) * S.IW + ix) : g_zero_src;
-        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
-    }
-}
+constexpr int NEMAX = 8;   // staging units (4-float groups, or floats) per thread per chunk
+
+// Per-segment staging state: the chunk-invariant part of every unit this thread moves.
+// Unit n of the patch image [ns][ch][pr][col] (col in 4-float groups when vec4) maps to
+// x + off[e] + ch0 * IH*IW; off < 0 marks a unit outside the input / batch (zero fill).
+struct Stager {
+    const float* x;
+    int C, Cpad, IHW, T, kseg, vec4, nunits;
+    int off[NEMAX];
+    unsigned chn;   // 4-bit channel-in-chunk of each of the thread's units
+};
+
+// A row pointer + patch geometry for the segment whose chunks are being multiplied.
+struct Computer {
+    int T, lt, PRC, gstep, Cpad;
+    int sb[8];      // per k-step s8: (s8 >> lt) * PRC + tap offset (s8 & (T-1))
+};
 
 template <int NP, int NTW>
 __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
@@ -87,6 +92,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
     const int rb = prem / J.ncb, cb = prem - rb * J.ncb;
     const int b0 = bs * NS, r0 = rb * TR, c0 = cb * TC;
     const int TRC = TR * TC;
+    const int nseg = J.nseg;
 
     // this lane's pixels (one per N-tile)
     int pns[NTW], pr_[NTW], pc_[NTW];
@@ -109,88 +115,189 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[nt][r] = 0.0f;
 
-    int nchunks = 0;
-    for (int s = 0; s < J.nseg; ++s) nchunks += J.seg[s].Cpad / CC;
-    auto chunk_seg = [&](int ci, int& s, int& ch0) {
-        s = 0;
-        while (ci >= J.seg[s].Cpad / CC) {
-            ci -= J.seg[s].Cpad / CC;
-            ++s;
-        }
-        ch0 = ci * CC;
-    };
-    // A (16-k groups, T <= 4 per chunk) of chunk ci into registers (not waited for here)
-    auto load_A = [&](int ci, floatx4 (&a0)[4], floatx4 (&a1)[4]) {
-        int s, ch0;
-        chunk_seg(ci, s, ch0);
-        const int T = P.T[s];
-        const float* __restrict__ Ap = J.A + P.a_off + (size_t)(m0 + cl) * P.Kpad + P.kseg[s] + ch0 * T + 8 * h;
+    // ---- staging: segment geometry (once per segment, not per chunk)
+    const float* zsrc = g_zero_src;
+    asm volatile("" : "+s"(zsrc));   // keep the zero-fill source in SGPRs (no per-unit GOT reload)
+    Stager st;
+    auto stage_setup = [&](int s) {
+        const ffc_convp_seg& S = J.seg[s];
+        st.x = S.x;
+        st.C = S.C;
+        st.Cpad = S.Cpad;
+        st.IHW = S.IH * S.IW;
+        st.T = P.T[s];
+        st.kseg = P.kseg[s];
+        st.vec4 = S.vec4;
+        const int PR = S.PR;
+        const int iy0 = r0 * S.mult_y + S.org_y;
+        const int ix0 = c0 * S.mult_x + S.org_x;
+        const int xa = S.vec4 ? (ix0 & ~3) : ix0;
+        const int PCu = S.vec4 ? S.PC / 4 : S.PC;   // units per patch row (4-float groups when vec4)
+        const int step = S.vec4 ? 4 : 1;
+        st.nunits = NS * CC * PR * PCu;
+        const unsigned mPC = magic_div((unsigned)PCu), mPR = magic_div((unsigned)PR);
+        st.chn = 0;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (g < T) {
-                a0[g] = *reinterpret_cast<const floatx4*>(Ap + 16 * g);
-                a1[g] = *reinterpret_cast<const floatx4*>(Ap + 16 * g + 4);
-            } else {
-                a0[g] = floatx4{0.f, 0.f, 0.f, 0.f};
-                a1[g] = a0[g];
+        for (int e = 0; e < NEMAX; ++e) {
+            const unsigned n = (unsigned)(e * 256 + tid);
+            const unsigned q1 = __umulhi(n, mPC);
+            const int g = (int)(n - q1 * PCu);
+            const unsigned q2 = __umulhi(q1, mPR);
+            const int pr = (int)(q1 - q2 * PR);
+            const int ns = (int)(q2 >> 4), ch = (int)(q2 & 15);
+            const int b = b0 + ns, iy = iy0 + pr, ix = xa + g * step;
+            const bool ok = (int)n < st.nunits && b < J.B && (unsigned)iy < (unsigned)S.IH &&
+                            (unsigned)ix < (unsigned)S.IW;
+            st.off[e] = ok ? ((b * S.C + ch) * S.IH + iy) * S.IW + ix : -1;
+            st.chn |= (unsigned)ch << (4 * e);
+        }
+    };
+    // LDS-DMA of one chunk: unit n -> lane n % 64 of wave-instruction n / 64 (no VGPR staging)
+    auto stage_issue = [&](int ch0, float* dst) {
+        const int cmax = st.C - ch0;
+        const float* xb = st.x + ch0 * st.IHW;
+        const int nw = (st.nunits + 255) >> 8;
+        if (st.vec4) {
+#pragma unroll
+            for (int e = 0; e < NEMAX; ++e) {
+                if (e < nw) {
+                    const bool ok = st.off[e] >= 0 && (int)((st.chn >> (4 * e)) & 15) < cmax;
+                    const float* src = ok ? xb + st.off[e] : zsrc;
+                    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (e * 256 + wave * 64) * 4), 16, 0, 0);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < NEMAX; ++e) {
+                if (e < nw) {
+                    const bool ok = st.off[e] >= 0 && (int)((st.chn >> (4 * e)) & 15) < cmax;
+                    const float* src = ok ? xb + st.off[e] : zsrc;
+                    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
+                }
             }
         }
     };
-    auto stage = [&](int ci) {
-        int s, ch0;
-        chunk_seg(ci, s, ch0);
-        stage_chunk(J.seg[s], NS, J.B, b0, r0, c0, ch0, patch + (ci & 1) * ebuf, tid, wave);
+    // A of one chunk (4 groups of 16 k; groups >= T are loaded but unused: the packed
+    // buffer carries tail padding) into registers, not waited for here
+    auto load_A = [&](int ch0, floatx4 (&n0)[4], floatx4 (&n1)[4]) {
+        const float* __restrict__ Ap =
+            J.A + P.a_off + (size_t)(m0 + cl) * P.Kpad + st.kseg + ch0 * st.T + 8 * h;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            n0[g] = *reinterpret_cast<const floatx4*>(Ap + 16 * g);
+            n1[g] = *reinterpret_cast<const floatx4*>(Ap + 16 * g + 4);
+        }
     };
+
+    // ---- compute: per-segment LDS read offsets
+    Computer cp;
+    int lb[NTW];   // per N-tile byte offset of the lane's pixel inside a chunk buffer (+ lane-half channel)
+    auto compute_setup = [&](int s) {
+        const ffc_convp_seg& S = J.seg[s];
+        const int T = P.T[s];
+        cp.T = T;
+        cp.Cpad = S.Cpad;
+        if (T == 0) return;
+        cp.lt = T == 4 ? 2 : (T == 2 ? 1 : 0);
+        const int PCa = S.PC;
+        const int ix0 = c0 * S.mult_x + S.org_x;
+        const int xoff = S.vec4 ? ix0 - (ix0 & ~3) : 0;
+        cp.PRC = S.PR * PCa;
+        cp.gstep = (16 >> cp.lt) * cp.PRC;
+        int tap[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int tt = J.taptab[P.tap_base[s] + (t & (T - 1))];
+            tap[t] = (tt >> 16) * PCa + (tt & 0xFFFF);
+        }
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) cp.sb[s8] = (s8 >> cp.lt) * cp.PRC + tap[s8 & 3 & (T - 1)];
+        const int hoff = ((8 * h) >> cp.lt) * cp.PRC;
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+            lb[nt] = 4 * (pns[nt] * (CC * cp.PRC) + pr_[nt] * S.mult_y * PCa + pc_[nt] * S.mult_x + xoff + hoff);
+    };
+
+    int nchunks = 0;
+    for (int s = 0; s < nseg; ++s) nchunks += J.seg[s].Cpad / CC;
+
+#ifdef FFC_TRACE
+    unsigned long long tr_rt0 = __builtin_amdgcn_s_memrealtime(), tr_c0, tr_a, tr_b, tr_bar = 0, tr_stg = 0, tr_mf = 0;
+    FFC_STAMP(tr_c0);
+#endif
+    // stager runs one chunk ahead of the computer
+    int ss = 0, sch = 0;   // segment / channel offset of the next chunk to stage
+    int cs = 0, cch = 0;   // ... of the chunk being multiplied
+    stage_setup(0);
+    compute_setup(0);
     floatx4 a0[4], a1[4], n0[4], n1[4];
-    stage(0);
+    stage_issue(0, patch);
     load_A(0, n0, n1);
+    sch = CC;
+    if (sch >= st.Cpad && nseg > 1) {
+        ss = 1;
+        sch = 0;
+        stage_setup(1);
+    }
     for (int ci = 0; ci < nchunks; ++ci) {
-        int s, ch0;
-        chunk_seg(ci, s, ch0);
+#ifdef FFC_TRACE
+        FFC_STAMP(tr_a);
+#endif
         __syncthreads();  // patch + A of chunk ci landed (vmcnt(0)); everyone is done with chunk ci-1
+#ifdef FFC_TRACE
+        FFC_STAMP(tr_b);
+        tr_bar += tr_b - tr_a;
+#endif
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             a0[g] = n0[g];
             a1[g] = n1[g];
-            asm volatile("" : "+v"(a0[g]), "+v"(a1[g]));
         }
         if (ci + 1 < nchunks) {  // next chunk's A and patch stay in flight under this chunk's MFMAs
-            load_A(ci + 1, n0, n1);
-            stage(ci + 1);
+            load_A(sch, n0, n1);
+            stage_issue(sch, patch + ((ci + 1) & 1) * ebuf);
+            sch += CC;
+            if (sch >= st.Cpad && ss + 1 < nseg) {
+                ++ss;
+                sch = 0;
+                stage_setup(ss);
+            }
         }
-        const int T = P.T[s];
-        if (T == 0) continue;
-        const ffc_convp_seg& S = J.seg[s];
-        const int lt = 31 - __builtin_clz(T);  // T is a power of two dividing 4
-        const float* cur = patch + (ci & 1) * ebuf;
-        const int PRC = S.PR * S.PC;
-        int loff[NTW];
+#ifdef FFC_TRACE
+        FFC_STAMP(tr_a);
+        tr_stg += tr_a - tr_b;
+#endif
+        const int T = cp.T;
+        if (T > 0) {
+            const int base = ((ci & 1) * ebuf) * 4;   // byte offset of this chunk's buffer
 #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-            loff[nt] = pns[nt] * (CC * PRC) + pr_[nt] * S.mult_y * S.PC + pc_[nt] * S.mult_x;
-        int boff[8];
+            for (int g = 0; g < 4; ++g) {
+                if (g < T) {
+                    const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
+                                         a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
+                    const int gb = base + 4 * g * cp.gstep;
 #pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8) {
-            const int k = 8 * h + s8;
-            boff[s8] = (k >> lt) * PRC + J.taptab[P.tap_base[s] + (k & (T - 1))];
-        }
-        const int gstep = (16 >> lt) * PRC;
+                    for (int s8 = 0; s8 < 8; ++s8) {
+                        const int sb = gb + 4 * cp.sb[s8];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (g < T) {
-                const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3], a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
-                int go = g * gstep;
-                asm volatile("" : "+s"(go));  // keep the per-group LDS addresses from being hoisted (VGPRs)
-                const float* cg = cur + go;
-#pragma unroll
-                for (int s8 = 0; s8 < 8; ++s8) {
-#pragma unroll
-                    for (int nt = 0; nt < NTW; ++nt) {
-                        const float bv = cg[loff[nt] + boff[s8]];
-                        acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
+                        for (int nt = 0; nt < NTW; ++nt) {
+                            const float bv = *reinterpret_cast<const float*>(
+                                reinterpret_cast<const char*>(patch) + (lb[nt] + sb));
+                            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
+                        }
                     }
                 }
             }
+        }
+#ifdef FFC_TRACE
+        FFC_STAMP(tr_b);
+        tr_mf += tr_b - tr_a;
+#endif
+        cch += CC;
+        if (cch >= cp.Cpad && cs + 1 < nseg) {
+            ++cs;
+            cch = 0;
+            compute_setup(cs);
         }
     }
 
@@ -260,6 +367,23 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
         default: store([](float v) { return v; }); break;
     }
+#ifdef FFC_TRACE
+    __syncthreads();
+    unsigned long long tr_c1;
+    FFC_STAMP(tr_c1);
+    if (tid == 0) {
+        unsigned long long* t = g_ffc_trace + 8 * blockIdx.x;
+        t[0] = tr_rt0;
+        t[1] = __builtin_amdgcn_s_memrealtime();
+        t[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+               ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+        t[3] = tr_bar;
+        t[4] = tr_stg;
+        t[5] = tr_mf;
+        t[6] = tr_c1 - tr_c0;
+        t[7] = (unsigned long long)nchunks;
+    }
+#endif
 }
 
 template <int NP, int NTW>
@@ -283,6 +407,12 @@ int launch(const ConvPArgs& a, int ntiles, size_t lds, hipStream_t s) {
 
 }  // namespace
 
+#ifdef FFC_TRACE
+extern "C" int ffc_debug_trace_read(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_ffc_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                                  void* stream) {
     FFC_CHECK_ARG(jobs && tiles && njobs >= 1 && njobs <= 2 && ntiles > 0, "ffc_convp_forward: bad args");
@@ -300,7 +430,12 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
             FFC_CHECK_ARG(S.x && S.Cpad % CC == 0 && S.Cpad >= S.C, "ffc_convp_forward: segment channels");
             FFC_CHECK_ARG(S.PC > 0 && S.PR > 0, "ffc_convp_forward: patch shape");
             FFC_CHECK_ARG(!S.pool && !S.gate, "ffc_convp_forward: pooled / gated segments use ffc_conv_forward");
-            const size_t E = (size_t)J.NS * CC * S.PR * S.PC;
+            FFC_CHECK_ARG(!S.vec4 || (S.IW % 4 == 0 && S.PC % 4 == 0), "ffc_convp_forward: vec4 staging needs IW, PC % 4 == 0");
+            FFC_CHECK_ARG(!S.vec4 || (reinterpret_cast<uintptr_t>(S.x) & 15) == 0,
+                          "ffc_convp_forward: vec4 staging needs a 16-byte aligned input");
+            const size_t units = (size_t)J.NS * CC * S.PR * (S.vec4 ? S.PC / 4 : S.PC);
+            FFC_CHECK_ARG(units <= (size_t)NEMAX * 256, "ffc_convp_forward: patch too large for the staging registers");
+            const size_t E = (units + 255) / 256 * 256 * (S.vec4 ? 4 : 1);
             if (E > emax) emax = E;
             for (int p = 0; p < J.nphase; ++p) {
                 const int T = J.ph[p].T[s];
@@ -308,7 +443,7 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
             }
         }
     }
-    const size_t ebuf = (emax + 255) / 256 * 256 + 256;
+    const size_t ebuf = emax + 64;   // + 64 floats: consecutive buffers start on different banks
     const size_t lds = 2 * ebuf * sizeof(float);
     FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_convp_forward: patch too large");
     ConvPArgs a;

@@ -102,7 +102,10 @@ int ffc_conv_stat_rows_per_tile(int tile_cfg);
  * (phase, tap) B fragment is then read from that patch, so an input element is fetched from
  * HBM/L2 once per block instead of once per (phase, tap).  Requires the taps per phase of each
  * segment to divide 4 (ConvT k4 s2: 4; 1x1: 1).  A is packed with every segment's channels
- * padded to a multiple of 16 (k = (seg, ch, tap)). */
+ * padded to a multiple of 16 (k = (seg, ch, tap)); the packed buffer needs >= 64 floats of tail padding
+ * (groups of taps a phase does not use are loaded, not multiplied).  taptab entries are
+ * (dy << 16) | dx, the tap's offset from the patch origin.  Per-thread staging holds at most 2048
+ * units (16-byte groups when vec4, else floats) of NS x 16 x PR x PC. */
 #define FFC_PATCH_CC 16
 typedef struct ffc_convp_seg {
     const float* x;      /* (B, C, IH, IW), or (B, C, 2IH, 2IW) when pool=1 */
@@ -110,9 +113,10 @@ typedef struct ffc_convp_seg {
     int C, Cpad, IH, IW;
     int mult_y, mult_x;  /* input coord = m*mult + off */
     int org_y, org_x;    /* patch origin relative to r0*mult_y / c0*mult_x (the minimum tap offset) */
-    int PR, PC;          /* patch rows / cols per channel */
+    int PR, PC;          /* patch rows / LDS row length in floats (vec4: whole 16-byte groups from the
+                          * row start rounded down to a multiple of 4) */
     int pool;
-    int reserved_;       /* must be 0 */
+    int vec4;            /* 1: stage the patch in 16-byte groups (IW % 4 == 0, x 16-byte aligned) */
 } ffc_convp_seg;
 
 typedef struct ffc_convp_phase {

@@ -176,10 +176,13 @@ def emulate_patch(plan, xs, ws, layouts):
                     continue
                 assert sx == (s | (ch << 4))
                 tt = plan.taptab[ph["tap_base"][s] + t]
-                dy, dx = divmod(int(tt), PC)
+                dy, dx = int(tt) >> 16, int(tt) & 0xFFFF
                 assert (dy, dx) == (oy - plan.org[s][0], ox - plan.org[s][1])
-                # every in-block pixel stays inside the patch
-                assert (plan.TR - 1) * mul_y + dy < PR and (plan.TC - 1) * mul_x + dx < PC
+                # every in-block pixel stays inside the patch, also shifted by the 16-byte row alignment
+                PCa = plan.rowlen[s]
+                al = plan.org[s][1] % 4 == 0 and (plan.TC * mul_x) % 4 == 0
+                xs_max = 3 if plan.vec4[s] and not al else 0
+                assert (plan.TR - 1) * mul_y + dy < PR and (plan.TC - 1) * mul_x + dx + xs_max < PCa
                 ky, kx = kyx & 0xFFFF, kyx >> 16
                 A[:, k] = ws[s][:, ch, ky, kx] if layouts[s] == 0 else ws[s][ch, :, ky, kx]
                 iy = my * mul_y + plan.org[s][0] + dy
