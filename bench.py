@@ -58,6 +58,29 @@ def parse():
     return p.parse_args()
 
 
+# kernel-name prefixes behind each observed launch label (for the PMC traffic lookup)
+LABEL_KERNELS = {"conv_gemm": ("convp_kernel", "conv_gemm_kernel"), "fu_pass0": ("fu_kernel",),
+                 "fu_pass1": ("fu_kernel",), "st_prologue": ("st_prologue_kernel",),
+                 "convt_smallm": ("convt_smallm_kernel",)}
+
+
+def pmc_traffic(label):
+    """HBM bytes per launch of the kernels behind `label`, from the newest committed
+    profiles/<round>/pmc_traffic.json (tools/pmc_traffic.sh: FETCH_SIZE / WRITE_SIZE passes,
+    corrected per MI355X_MICROARCH.md), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not files or label not in LABEL_KERNELS:
+        return None
+    kern = json.load(open(files[-1]))["kernels"]
+    sel = [v for k, v in kern.items() if k.startswith(LABEL_KERNELS[label])]
+    n = sum(v["launches"] for v in sel)
+    if n == 0:
+        return None
+    return {"bytes_per_launch": round(sum(v["bytes_per_launch"] * v["launches"] for v in sel) / n),
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 def weights_init(m):
     """fgan64_complete.py:22-31"""
     import torch.nn as nn
@@ -163,7 +186,10 @@ def main():
         achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4)}
-    roof["traffic"] = None
+    tr = pmc_traffic(dom)
+    roof["traffic"] = tr["bytes_per_launch"] if tr else None
+    if tr:
+        roof["traffic_source"] = tr["source"]
     fu = {k: summ[k] for k in ("fu_pass0", "fu_pass1") if k in summ}
     fft_roof = None
     if fu:

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import os
+
 import numpy as np
 
 BK = 16
@@ -388,14 +390,37 @@ def pick_patch_cfg(B, M, segs):
     return p
 
 
-def build_patch_tiles(plans):
-    """int32 [ntiles, 4] {job, m0, pixel block, 0}: blocks sharing a pixel block adjacent, XCD-remapped."""
-    ordered = []
+def patch_tile_cost(pl) -> int:
+    """k-steps a workgroup of this job runs (the phases of a block run concurrently, so the
+    slowest phase counts)"""
+    return max(ph["Kpad"] for ph in pl.phases)
+
+
+def build_patch_tiles(plans, nxcd: int = 8):
+    """int32 [ntiles, 4] {job, m0, pixel block, 0}, XCD-remapped.
+
+    The pixel blocks are cut into nxcd contiguous ranges, one per XCD (blockIdx % 8), so the
+    workgroups that share a block's input patch share an L2.  Within an XCD's run the heaviest
+    job's tiles come first: a CU's first and second resident workgroups are then one heavy and
+    one light tile (dispatch deals an XCD's blocks round-robin over its CUs), and in launches of
+    more rounds the light tiles fill in behind the heavy ones (longest-processing-time first)."""
     npb = max(pl.npb for pl in plans)
-    for pb in range(npb):
-        for j, pl in enumerate(plans):
-            if pb < pl.npb:
+    order = sorted(range(len(plans)), key=lambda j: -patch_tile_cost(plans[j]))
+    ordered = []
+    if os.environ.get("FFC_TILE_ORDER") == "interleaved":   # previous order, for A/B measurements
+        for pb in range(npb):
+            for j, pl in enumerate(plans):
+                if pb < pl.npb:
+                    for m0 in range(0, pl.M, 32):
+                        ordered.append((j, m0, pb, 0))
+        remap = xcd_remap(len(ordered), nxcd)
+        return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)
+    for x in range(nxcd):
+        lo, hi = npb * x // nxcd, npb * (x + 1) // nxcd
+        for j in order:
+            pl = plans[j]
+            for pb in range(lo, min(hi, pl.npb)):
                 for m0 in range(0, pl.M, 32):
                     ordered.append((j, m0, pb, 0))
-    remap = xcd_remap(len(ordered))
+    remap = xcd_remap(len(ordered), nxcd)
     return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)

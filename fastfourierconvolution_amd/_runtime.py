@@ -205,6 +205,8 @@ def algorithmic_flops(plan) -> float:
 
 
 USE_PATCH = True   # LDS-patch kernel where it applies (tests flip this to cover the generic kernel)
+USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
+USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 
 
 class ConvExec:
@@ -329,6 +331,9 @@ class LaunchPlan:
         else:
             self.cfg = _plan.pick_tile_cfg([e.plan.M for e in execs])
             tiles, nslots = _plan.build_tiles([e.plan for e in execs], self.cfg)
+            while tiles.shape[0] < 256 and self.cfg == 0:   # too few tiles to fill 256 CUs: halve BM
+                self.cfg = 1
+                tiles, nslots = _plan.build_tiles([e.plan for e in execs], self.cfg)
             rpt = _plan.TILE_CFGS[self.cfg][2]
             self._rows = [n * rpt for n in nslots]
         self.ntiles = tiles.shape[0]

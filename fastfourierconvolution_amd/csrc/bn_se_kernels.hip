@@ -49,6 +49,7 @@ struct FinalizeArgs {
     float* running_var;
     int64_t* nbt;
     int use_batch_stats, update_running;
+    int bump_here;   // momentum given: nobody reads num_batches_tracked, so one thread bumps it in-kernel
     float momentum, eps, count_mult;
     float* scale;
     float* shift;
@@ -90,6 +91,7 @@ __global__ void bn_reduce_kernel(const float4* __restrict__ slab, int nrows, int
 __global__ void bn_finalize_kernel(const double* __restrict__ moments, int C, FinalizeArgs a) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c < C) finalize_channel(moments + 3 * c, c, a);
+    if (a.bump_here && c == 0) *a.nbt += 1;
 }
 
 // nbt is bumped after every block has read it (stream order: separate tiny kernel)
@@ -103,6 +105,7 @@ __global__ void bn_reduce_finalize_kernel(const float4* __restrict__ slab, int n
     reduce_channel(slab, nrows, C, c, moments + 3 * c);
     __syncthreads();
     if (threadIdx.x == 0) finalize_channel(moments + 3 * c, c, a);
+    if (a.bump_here && c == 0 && threadIdx.x == 0) *a.nbt += 1;
 }
 
 __global__ void bn_act_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW, long long total4,
@@ -187,6 +190,7 @@ static FinalizeArgs make_finalize(const float* gamma, const float* beta, float* 
     a.nbt = nbt;
     a.use_batch_stats = use_batch_stats;
     a.update_running = update_running;
+    a.bump_here = update_running && use_batch_stats && momentum >= 0.0f;
     a.momentum = momentum;
     a.eps = eps;
     a.count_mult = count_mult;
@@ -207,7 +211,8 @@ extern "C" int ffc_bn_finalize(const double* moments, int C, const float* gamma,
     FinalizeArgs a = make_finalize(gamma, beta, running_mean, running_var, num_batches_tracked, use_batch_stats,
                                    update_running, momentum, eps, count_mult, scale, shift);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, moments, C, a);
-    if (update_running && use_batch_stats)
+    // momentum=None (cumulative average) reads num_batches_tracked in every block: bump after them
+    if (update_running && use_batch_stats && !a.bump_here)
         hipLaunchKernelGGL(bn_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, num_batches_tracked);
     return ffc::launch_status("ffc_bn_finalize");
 }
@@ -224,7 +229,7 @@ extern "C" int ffc_bn_reduce_finalize(const float* slab, int nrows, int C, doubl
                                    momentum, eps, count_mult, scale, shift);
     hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(C), dim3(RED_THREADS), 0, (hipStream_t)stream,
                        reinterpret_cast<const float4*>(slab), nrows, C, moments, a);
-    if (update_running)
+    if (update_running && !a.bump_here)
         hipLaunchKernelGGL(bn_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, num_batches_tracked);
     return ffc::launch_status("ffc_bn_reduce_finalize");
 }

@@ -46,7 +46,6 @@ __device__ unsigned long long g_ffc_trace[8 * 4096];
 typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-__device__ __forceinline__ unsigned magic_div(unsigned d) { return 0xFFFFFFFFu / d + 1u; }
 
 constexpr int NEMAX = 8;   // staging units (4-float groups, or floats) per thread per chunk
 
@@ -135,14 +134,13 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         const int PCu = S.vec4 ? S.PC / 4 : S.PC;   // units per patch row (4-float groups when vec4)
         const int step = S.vec4 ? 4 : 1;
         st.nunits = NS * CC * PR * PCu;
-        const unsigned mPC = magic_div((unsigned)PCu), mPR = magic_div((unsigned)PR);
         st.chn = 0;
 #pragma unroll
         for (int e = 0; e < NEMAX; ++e) {
-            const unsigned n = (unsigned)(e * 256 + tid);
-            const unsigned q1 = __umulhi(n, mPC);
+            const unsigned n = (unsigned)(e * 256 + tid);   // once per segment: plain division
+            const unsigned q1 = n / (unsigned)PCu;
             const int g = (int)(n - q1 * PCu);
-            const unsigned q2 = __umulhi(q1, mPR);
+            const unsigned q2 = q1 / (unsigned)PR;
             const int pr = (int)(q1 - q2 * PR);
             const int ns = (int)(q2 >> 4), ch = (int)(q2 & 15);
             const int b = b0 + ns, iy = iy0 + pr, ix = xa + g * step;
@@ -286,6 +284,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
                             acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
                         }
                     }
+
                 }
             }
         }

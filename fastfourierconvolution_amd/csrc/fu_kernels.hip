@@ -104,10 +104,26 @@ struct FuArgs {
     const float* bn_shift;
     float* out;
     int C, Mpad, in_relu, residual, has_in_affine;
+    int wm_lds;   // mix weight staged in LDS (when it fits beside the Z/Y planes)
     float norm;
 };
 
 constexpr int FU_THREADS = 512;
+
+#ifdef FFC_TRACE
+// Diagnostic build only: per workgroup {realtime start, end, s_memtime at phase boundaries 0..5}.
+__device__ unsigned long long g_fu_trace[8 * 4096];
+#define FU_STAMP(i)                                                                         \
+    do {                                                                                    \
+        unsigned long long t_;                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        if (threadIdx.x == 0) g_fu_trace[8 * blockIdx.x + 2 + (i)] = t_;                   \
+    } while (0)
+#else
+#define FU_STAMP(i) do { } while (0)
+#endif
 
 // s row (channel ch, output row y) = transform(t) nearest-upsampled by UP
 template <int W, int UP>
@@ -144,6 +160,23 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     float* Zim = Zre + C * NB;
     float* Yre = Zim + C * NB;
     float* Yim = Yre + C * NB;
+    float* Wm = Yim + C * NB;   // mix weight (2C, Mpad), staged by LDS-DMA under the FFT phases
+    if (a.wm_lds) {
+        typedef __attribute__((address_space(1))) void* gptr_t;
+        typedef __attribute__((address_space(3))) void* lptr_t;
+        const int n4 = (C2 * a.Mpad) >> 2;   // Mpad is a multiple of 32
+        for (int i0 = 0; i0 < n4; i0 += FU_THREADS) {
+            if (i0 + (tid & ~63) < n4) {   // whole wave-instructions; the region is padded to 64 groups
+                const int i = min(i0 + tid, n4 - 1);
+                __builtin_amdgcn_global_load_lds((gptr_t)(a.wmixT + 4 * (size_t)i),
+                                                 (lptr_t)(Wm + 4 * (i0 + (tid & ~63))), 16, 0, 0);
+            }
+        }
+    }
+#ifdef FFC_TRACE
+    if (tid == 0) g_fu_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+    FU_STAMP(0);
 
     // 1. row R2C (real W-point FFT per (channel,row)), input transform fused
     for (int r = tid; r < C * H; r += FU_THREADS) {
@@ -161,6 +194,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             zi[k] = im[k];
         }
     }
+    FU_STAMP(1);
     __syncthreads();
 
     // 2. column C2C over H, ortho scale 1/sqrt(HW)
@@ -182,6 +216,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         }
     }
     __syncthreads();
+    FU_STAMP(2);
 
     // 3. spectral mix on MFMA: Y[o][n] = sum_i Wmix[o][i] Z[i][n], Z[2c+h] = (h ? Im : Re)(channel c)
     //    k-step s feeds k-slot h = lane>>5 with channel s, component h.
@@ -192,12 +227,19 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         floatx16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-        const float* wp = a.wmixT + (size_t)h * a.Mpad + mt * 32 + col;
         const float* zp = (h ? Zim : Zre) + nt * 32 + col;
-        const size_t wstep = (size_t)2 * a.Mpad;
+        const int wstep = 2 * a.Mpad;
+        if (a.wm_lds) {
+            const float* wp = Wm + h * a.Mpad + mt * 32 + col;
 #pragma unroll 8
-        for (int s = 0; s < C; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[s * wstep], zp[s * NB], acc, 0, 0, 0);
+            for (int s = 0; s < C; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[s * wstep], zp[s * NB], acc, 0, 0, 0);
+        } else {
+            const float* __restrict__ wp = a.wmixT + h * a.Mpad + mt * 32 + col;
+#pragma unroll 8
+            for (int s = 0; s < C; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wp[(size_t)s * wstep], zp[s * NB], acc, 0, 0, 0);
+        }
         const int n = nt * 32 + col;
         const bool nvalid = n < NB;
         if constexpr (PASS == 0) {
@@ -228,8 +270,10 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         }
     }
     __syncthreads();
+    FU_STAMP(3);
 
     if constexpr (PASS == 0) {
+        FU_STAMP(4);
         // merge the per-tile partials of each channel (Chan et al.) -> one slab row per sample
         for (int o = tid; o < C2; o += FU_THREADS) {
             float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
@@ -244,6 +288,11 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             }
             reinterpret_cast<float4*>(a.slab)[(size_t)b * C2 + o] = make_float4(nn, mean, m2, 0.0f);
         }
+#ifdef FFC_TRACE
+        __syncthreads();
+        FU_STAMP(5);
+        if (tid == 0) g_fu_trace[8 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
         return;
     } else {
         // 4. inverse column C2C over H, ortho scale
@@ -265,6 +314,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             }
         }
         __syncthreads();
+        FU_STAMP(4);
 
         // 5. per-row C2R over W (imaginary part of bins 0 and W/2 ignored) + residual
         for (int r = tid; r < C * H; r += FU_THREADS) {
@@ -293,6 +343,11 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             }
             store_row<W>(a.out + ((size_t)(b * C + ch) * H + y) * W, re);
         }
+#ifdef FFC_TRACE
+        __syncthreads();
+        FU_STAMP(5);
+        if (tid == 0) g_fu_trace[8 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
 }
 
@@ -335,12 +390,26 @@ FuKernel pick_kernel(int H, int W, int up, int pass) {
 
 bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
 
+// floats of the LDS mix-weight region: (2C, ceil32(2C)) in whole 64-lane x 16-B DMA groups
+size_t fu_wm_floats(int C) {
+    const size_t Mpad = (size_t)(2 * C + 31) / 32 * 32;
+    return ((size_t)(2 * C) * Mpad + 255) / 256 * 256;
+}
+
 }  // namespace
+
+#ifdef FFC_TRACE
+extern "C" int ffc_debug_fu_trace_read(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fu_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" size_t ffc_fu_lds_bytes(int C, int H, int W) {
     if (C <= 0 || !pow2_in(H, 4, 32) || !pow2_in(W, 4, 32)) return 0;
-    const size_t bytes = (size_t)16 * C * H * (W / 2 + 1);
-    return bytes <= 160 * 1024 ? bytes : 0;
+    const size_t planes = (size_t)16 * C * H * (W / 2 + 1);
+    const size_t with_w = planes + 4 * fu_wm_floats(C);
+    if (with_w <= 160 * 1024) return with_w;
+    return planes <= 160 * 1024 ? planes : 0;
 }
 
 extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
@@ -374,6 +443,7 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
     a.Mpad = (2 * C + 31) / 32 * 32;
     a.residual = residual;
     a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
+    a.wm_lds = lds > (size_t)16 * C * H * (W / 2 + 1);
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;

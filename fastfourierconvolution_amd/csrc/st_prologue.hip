@@ -30,6 +30,21 @@ struct StArgs {
 
 constexpr int ST_THREADS = 256;
 
+#ifdef FFC_TRACE
+// Diagnostic build only: per workgroup {realtime start, end, s_memtime at phase boundaries 0..5}.
+__device__ unsigned long long g_st_trace[8 * 4096];
+#define ST_STAMP(i)                                                                         \
+    do {                                                                                    \
+        unsigned long long t_;                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        if (threadIdx.x == 0) g_st_trace[8 * blockIdx.x + 2 + (i)] = t_;                   \
+    } while (0)
+#else
+#define ST_STAMP(i) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -44,6 +59,10 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     float* red = st + (((hw + 31) / 32) * c * 3 + 3) / 4 * 4;   // [4 waves][16][64] split-K partials
     float* wt = red + 4 * 16 * 64;       // [Cin][Mpad] conv1 weight (when it fits)
 
+#ifdef FFC_TRACE
+    if (tid == 0) g_st_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+    ST_STAMP(0);
     // 1. sample -> LDS (2x2 average pool on the way in)
     const float* xb = a.x + (size_t)b * Cin * a.H * a.W;
     if (!a.pool) {
@@ -67,6 +86,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
             reinterpret_cast<float4*>(wt)[i] = reinterpret_cast<const float4*>(a.wcT)[i];
     }
     __syncthreads();
+    ST_STAMP(1);
 
     // 2. SE gate
     for (int ch = wave; ch < Cin; ch += ST_THREADS / 64) {
@@ -104,6 +124,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         }
     }
     __syncthreads();
+    ST_STAMP(2);
 
     // 3. conv1: t[o][p] = sum_k W[o][k] gate[k] x[k][p] on MFMA; lane half h carries k = 2s + h.
     //    With fewer than 4 output tiles the K range is split over the idle waves (LDS reduction).
@@ -178,6 +199,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         }
     }
     __syncthreads();
+    ST_STAMP(3);
     for (int o = tid; o < c; o += ST_THREADS) {
         float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
         for (int nt = 0; nt < NT; ++nt) {
@@ -190,6 +212,11 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         }
         reinterpret_cast<float4*>(a.slab)[(size_t)b * c + o] = make_float4(nn, mean, m2, 0.0f);
     }
+#ifdef FFC_TRACE
+    __syncthreads();
+    ST_STAMP(4);
+    if (tid == 0) g_st_trace[8 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 size_t st_lds(int Cin, int H, int W, int pool, int hid, int c, bool with_w) {
@@ -202,6 +229,12 @@ size_t st_lds(int Cin, int H, int W, int pool, int hid, int c, bool with_w) {
 }
 
 }  // namespace
+
+#ifdef FFC_TRACE
+extern "C" int ffc_debug_st_trace_read(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_st_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c) {
     if (Cin <= 0 || H <= 0 || W <= 0 || c <= 0 || hidden < 0) return 0;

@@ -97,6 +97,12 @@ class _FFCExec:
                 out = self._smallm(segs, w, inp, act, M, B, dev, stream)
                 outs[name] = out
                 continue
+            out_shape = None
+            if addend is None and bn is None:
+                rw = self._outer_rewrite(segs, w, M)
+                if rw is not None:
+                    segs, w, M, chw = rw
+                    out_shape = (B,) + chw
             key = (name, B, tuple(segs), str(dev))
             cache = self._ffc_cache()
             ex = cache.get(key)
@@ -104,7 +110,7 @@ class _FFCExec:
                 ex = cache[key] = rt.ConvExec(B, M, segs, w, dev)
             ex.ensure_packed(w)
             pl = ex.plan
-            out = torch.empty((B, pl.M, pl.OH, pl.OW), device=dev, dtype=torch.float32)
+            out = torch.empty(out_shape or (B, pl.M, pl.OH, pl.OW), device=dev, dtype=torch.float32)
             if addend is not None and tuple(addend.shape) != tuple(out.shape):
                 raise RuntimeError(f"shape mismatch adding pass-through {tuple(addend.shape)} to {tuple(out.shape)}")
             outs[name] = out
@@ -142,10 +148,38 @@ class _FFCExec:
             rt.bn_act_apply(out, sc, sh, act[0], act[1])
         return outs["l"], outs["g"]
 
+    def _outer_rewrite(self, segs, w, M):
+        """ConvTranspose2d(k, s=1, p=0) on a 1x1 input (the generator's first layer, ffc0:
+        ffc_transpose.py:79-86 on z of shape (B, nz, 1, 1)) is an outer product: out[b, m, y, x] =
+        sum_c z[b, c] W[c, m, y, x].  As ONE GEMM with M' = M*k*k "channels" at 1x1 (the output
+        (B, M, k, k) has the memory layout of (B, M*k*k, 1, 1)) it fills the GPU with tiles instead
+        of 16 tiny per-phase GEMMs.  -> (segments, weights, M', output shape) or None."""
+        if M is None or not segs or not rt.USE_OUTER:
+            return None
+        k = segs[0].k
+        for sg in segs:
+            if (sg.kind, sg.IH, sg.IW, sg.s, sg.p, sg.d, sg.op, sg.k) != ("convT", 1, 1, 1, 0, 1, 0, k):
+                return None
+        cache = self._ffc_cache()
+        segs2, w2 = [], []
+        for sg, (wt, lay, kh, kw, bias) in zip(segs, w):
+            key = ("outer", wt.data_ptr(), wt._version, None if bias is None else (bias.data_ptr(), bias._version))
+            hit = cache.get(key)
+            if hit is None:
+                for old in [kk for kk in cache if kk[0] == "outer" and kk[1] == wt.data_ptr()]:
+                    del cache[old]
+                wr = wt.permute(1, 2, 3, 0).reshape(M * k * k, sg.C, 1, 1).contiguous()   # (C,M,k,k) -> (M k k, C)
+                br = bias.repeat_interleave(k * k).contiguous() if bias is not None else None
+                hit = cache[key] = (wr, br)
+            segs2.append(_plan.Seg("pw", sg.C, 1, 1))
+            w2.append((hit[0], 0, 1, 1, hit[1]))
+        return segs2, w2, M * k * k, (M, k, k)
+
     @staticmethod
     def _smallm_ok(segs, w, addend, bn, M):
         """ConvT k4 s2 p1 into <= 4 channels (the generator's last layer) -> direct VALU kernel"""
-        if addend is not None or bn is not None or M is None or M > 4 or not 1 <= len(segs) <= 2:
+        if not rt.USE_SMALLM or addend is not None or bn is not None or M is None or M > 4 or \
+                not 1 <= len(segs) <= 2:
             return False
         if sum(1 for x in w if x[4] is not None) > 1:
             return False

@@ -253,3 +253,57 @@ def test_sharded_syncbn_gpu(tmp_path):
                 np.testing.assert_allclose(r["sd"][k].numpy(), v.cpu().numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
             elif k.endswith("num_batches_tracked"):
                 assert int(r["sd"][k]) == int(v), k
+
+
+def test_bn_momentum_none_cumulative():
+    """nn.BatchNorm2d(momentum=None): cumulative running average (factor 1/(num_batches_tracked+1)),
+    the one case where num_batches_tracked is read by the statistics kernel."""
+    import functools
+    import oracle.ffc_oracle as O
+    g, sd = _gen_state(100, 3, 16, seed=13)
+    g = g.cuda().train()
+    for m in g.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = None
+    osd = {k: v.double() if v.is_floating_point() else v.clone() for k, v in sd.items()}
+    orig = O.batch_norm
+    try:
+        for step in range(2):
+            z = torch.randn((9, 100, 1, 1), generator=torch.Generator().manual_seed(40 + step))
+            with torch.no_grad():
+                out = g(z.cuda()).cpu()
+            O.batch_norm = functools.partial(orig, momentum=1.0 / (step + 1))
+            with torch.no_grad():
+                ref = O.ffc_generator(z.double(), osd, 100, 3, 16, True)
+            assert normwise_err(out, ref) <= TOL
+    finally:
+        O.batch_norm = orig
+    gsd = g.state_dict()
+    for k, v in osd.items():
+        if k.endswith("running_mean") or k.endswith("running_var"):
+            np.testing.assert_allclose(gsd[k].cpu().double().numpy(), v.numpy(), rtol=2e-4, atol=1e-5, err_msg=k)
+        elif k.endswith("num_batches_tracked"):
+            assert int(gsd[k]) == int(v) == (0 if ".lfu." in k else 2), k
+
+
+@pytest.mark.parametrize("B,C,M,H", [(4, 100, 4096, 1), (8, 16, 32, 1), (4, 16, 32, 2), (4, 16, 32, 3),
+                                     (4, 16, 32, 8), (2, 20, 40, 6), (256, 100, 4096, 1)])
+@pytest.mark.parametrize("patch", [True, False])
+def test_pointwise_conv_kernels(B, C, M, H, patch):
+    """1x1 segments through both conv kernels (LDS-patch incl. its unaligned float staging, and
+    the generic GEMM) vs the PyTorch fp32 reference; 1x1 spatial is the outer-product ConvT path."""
+    from fastfourierconvolution_amd import _plan, _runtime as rt
+    gen = torch.Generator().manual_seed(B * 131 + H)
+    x = torch.randn(B, C, H, H, generator=gen).cuda()
+    w = torch.randn(M, C, 1, 1, generator=gen).cuda()
+    ref = torch.nn.functional.conv2d(x, w)
+    old = rt.USE_PATCH
+    rt.USE_PATCH = patch
+    try:
+        ex = rt.ConvExec(B, M, [_plan.Seg("pw", C, H, H)], [(w, 0, 1, 1, None)], x.device)
+        lp = rt.LaunchPlan([ex], x.device)
+        out = torch.empty(B, M, H, H, device=x.device)
+        lp.launch([ex.job([(x, None)], out)], torch.cuda.current_stream().cuda_stream)
+    finally:
+        rt.USE_PATCH = old
+    assert normwise_err(out.cpu(), ref.cpu()) <= TOL

@@ -1,19 +1,25 @@
 #!/bin/bash
-# A/B the in-tree library against libffc_amd_<variant>.so variants, interleaved, in one session.
+# A/B the in-tree library against variants, interleaved, in one GPU session.
+# usage: tools/ab_bench.sh <variant>...   variant = cur | <name> (libffc_amd_<name>.so)
+#        optionally suffixed +VAR=value (environment for that run), e.g. cur+FFC_TILE_ORDER=interleaved
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for round in 1 2; do
   for v in "$@"; do
-    if [ "$v" = cur ]; then lib=""; else lib="fastfourierconvolution_amd/libffc_amd_$v.so"; fi
-    FFC_LIB_PATH=$lib timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/ab_$v.log 2>&1
+    name=${v%%+*}; envs=""
+    if [ "$name" != "$v" ]; then envs=${v#*+}; fi
+    if [ "$name" = cur ]; then lib=""; else lib="fastfourierconvolution_amd/libffc_amd_$name.so"; fi
+    tag=$(echo "$v" | tr '+=/' '___')
+    env FFC_LIB_PATH=$lib $envs timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline \
+      > gpurun_out/ab_$tag.log 2>&1
     rc=$?
-    if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; tail -5 gpurun_out/ab_$v.log; exit $rc; fi
-    python - "$v" <<'PY'
+    if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; tail -5 gpurun_out/ab_$tag.log; exit $rc; fi
+    python - "$tag" <<'PY'
 import json, sys
 l = [x for x in open(f"gpurun_out/ab_{sys.argv[1]}.log") if x.startswith("{")][-1]
 d = json.loads(l)
-print(f"{sys.argv[1]:8s} {d['value']:10.0f} img/s {d['ms_per_step']:.4f} ms  " +
+print(f"{sys.argv[1]:36s} {d['value']:10.0f} img/s {d['ms_per_step']:.4f} ms  " +
       " ".join(f"{k}={v['ms_per_step']*1e3:.0f}" for k, v in d["kernels"].items()))
 PY
   done
