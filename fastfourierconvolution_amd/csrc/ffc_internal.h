@@ -40,6 +40,51 @@ __device__ __forceinline__ float half_wave_sum(float v) {
     return v;
 }
 
+// DPP lane moves (no LDS round trip).  CTRL: 0x111..0x11F row_shr:1..15, 0xB1 quad_perm [1,0,3,2]
+// (= lane ^ 1).  Lanes whose source is outside the row read 0 (bound_ctrl).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over each 16-lane DPP row; the result is valid in lane 15 of the row (inclusive scan).
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0x111>(v);
+    v += dpp_f<0x112>(v);
+    v += dpp_f<0x114>(v);
+    v += dpp_f<0x118>(v);
+    return v;
+}
+
+// Chan partials of every row of a v_mfma_f32_32x32x2f32 accumulator tile over its first nv
+// (1..32) columns, without cross-lane shuffle chains: the tile goes through this wave's LDS
+// scratch (32 x 33 floats, conflict-free both ways) and lane pair (2o, 2o+1) reduces row o
+// (16 columns each).  Accumulator layout: lane l, register r -> row (r&3) + 8(r>>2) + 4(l>>5),
+// column l&31.  Row o = lane >> 1's {mean, M2} are valid in the even lane of the pair.
+constexpr int TILE_SCRATCH = 32 * 33;
+__device__ __forceinline__ void tile_row_stats(const floatx16& acc, int nv, float* scratch, float& mean, float& m2) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) scratch[((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + col] = acc[r];
+    // same-wave LDS write -> read: the LDS serves a wave's instructions in order
+    const int o = lane >> 1, c0 = (lane & 1) * 16;
+    float v[16];
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        v[j] = scratch[o * 33 + c0 + j];
+        if (c0 + j < nv) s += v[j];
+    }
+    mean = (s + dpp_f<0xB1>(s)) / (float)nv;
+    float q = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const float d = v[j] - mean;
+        if (c0 + j < nv) q = fmaf(d, d, q);
+    }
+    m2 = q + dpp_f<0xB1>(q);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -105,10 +105,20 @@ struct FuArgs {
     float* out;
     int C, Mpad, in_relu, residual, has_in_affine;
     int wm_lds;   // mix weight staged in LDS (when it fits beside the Z/Y planes)
+    int scr_off;  // float offset of the pass-0 stats scratch in LDS
     float norm;
 };
 
 constexpr int FU_THREADS = 512;
+
+// floats of the LDS mix-weight region: (2C, ceil32(2C)) in whole 64-lane x 16-B DMA groups
+__host__ __device__ inline size_t fu_wm_floats(int C) {
+    const size_t Mpad = (size_t)(2 * C + 31) / 32 * 32;
+    return ((size_t)(2 * C) * Mpad + 255) / 256 * 256;
+}
+// Pass-0 per-wave stats scratch (FuArgs::scr_off): the Y-imaginary plane (unused in pass 0)
+// when it is large enough, else a region after the planes (and the mix weight, when staged).
+constexpr int FU_SCRATCH = (FU_THREADS / 64) * 32 * 33;
 
 #ifdef FFC_TRACE
 // Diagnostic build only: per workgroup {realtime start, end, s_memtime at phase boundaries 0..5}.
@@ -243,20 +253,15 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         const int n = nt * 32 + col;
         const bool nvalid = n < NB;
         if constexpr (PASS == 0) {
-            const float cnt = (float)min(32, NB - nt * 32);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float v = nvalid ? acc[r] : 0.0f;
-                const float mean = ffc::half_wave_sum(v) / cnt;
-                const float d = nvalid ? acc[r] - mean : 0.0f;
-                const float m2 = ffc::half_wave_sum(d * d);
-                if (col == 0 && o < C2) {
-                    float* st = Yre + (nt * C2 + o) * 3;
-                    st[0] = cnt;
-                    st[1] = mean;
-                    st[2] = m2;
-                }
+            const int nv = min(32, NB - nt * 32);
+            float mean, m2;
+            ffc::tile_row_stats(acc, nv, smem + a.scr_off + wave * ffc::TILE_SCRATCH, mean, m2);
+            const int o = mt * 32 + (lane >> 1);
+            if ((lane & 1) == 0 && o < C2) {
+                float* st = Yre + (nt * C2 + o) * 3;
+                st[0] = (float)nv;
+                st[1] = mean;
+                st[2] = m2;
             }
         } else {
 #pragma unroll
@@ -390,11 +395,25 @@ FuKernel pick_kernel(int H, int W, int up, int pass) {
 
 bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
 
-// floats of the LDS mix-weight region: (2C, ceil32(2C)) in whole 64-lane x 16-B DMA groups
-size_t fu_wm_floats(int C) {
-    const size_t Mpad = (size_t)(2 * C + 31) / 32 * 32;
-    return ((size_t)(2 * C) * Mpad + 255) / 256 * 256;
+// LDS plan: Z/Y planes, then the mix weight when it fits, then the stats scratch unless it fits in
+// the Y-imaginary plane.  bytes = 0: unsupported.
+struct FuLayout {
+    size_t bytes;
+    int wm_lds, scr_off;
+};
+FuLayout fu_layout(int C, int H, int W) {
+    const size_t plane = (size_t)C * H * (W / 2 + 1);
+    const bool in_y = plane >= (size_t)FU_SCRATCH;
+    for (int wm = 1; wm >= 0; --wm) {
+        const size_t wfl = wm ? fu_wm_floats(C) : 0;
+        const size_t floats = 4 * plane + wfl + (in_y ? 0 : FU_SCRATCH);
+        if (4 * floats <= 160 * 1024)
+            return {4 * floats, wm, (int)(in_y ? 3 * plane : 4 * plane + wfl)};
+    }
+    return {0, 0, 0};
 }
+
+
 
 }  // namespace
 
@@ -406,10 +425,7 @@ extern "C" int ffc_debug_fu_trace_read(void* dst, size_t bytes) {
 
 extern "C" size_t ffc_fu_lds_bytes(int C, int H, int W) {
     if (C <= 0 || !pow2_in(H, 4, 32) || !pow2_in(W, 4, 32)) return 0;
-    const size_t planes = (size_t)16 * C * H * (W / 2 + 1);
-    const size_t with_w = planes + 4 * fu_wm_floats(C);
-    if (with_w <= 160 * 1024) return with_w;
-    return planes <= 160 * 1024 ? planes : 0;
+    return fu_layout(C, H, W).bytes;
 }
 
 extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
@@ -443,7 +459,9 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
     a.Mpad = (2 * C + 31) / 32 * 32;
     a.residual = residual;
     a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
-    a.wm_lds = lds > (size_t)16 * C * H * (W / 2 + 1);
+    const FuLayout lay = fu_layout(C, H, W);
+    a.wm_lds = lay.wm_lds;
+    a.scr_off = lay.scr_off;
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;

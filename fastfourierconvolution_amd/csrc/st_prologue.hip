@@ -57,7 +57,8 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     float* hv = gate + ((Cin + 3) & ~3); // [hid]
     float* st = hv + ((a.hid + 3) & ~3); // [ntile][c][3]
     float* red = st + (((hw + 31) / 32) * c * 3 + 3) / 4 * 4;   // [4 waves][16][64] split-K partials
-    float* wt = red + 4 * 16 * 64;       // [Cin][Mpad] conv1 weight (when it fits)
+    float* scr = red + 4 * 16 * 64;      // [4 waves][32 x 33] tile-stats scratch
+    float* wt = scr + 4 * ffc::TILE_SCRATCH;   // [Cin][Mpad] conv1 weight (when it fits)
 
 #ifdef FFC_TRACE
     if (tid == 0) g_st_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -88,19 +89,21 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     __syncthreads();
     ST_STAMP(1);
 
-    // 2. SE gate
-    for (int ch = wave; ch < Cin; ch += ST_THREADS / 64) {
+    // 2. SE gate.  Reductions run over 16-lane DPP rows (no shuffle chains): row q of the
+    //    block (16 lanes, consecutive pixels / inputs: conflict-free LDS) owns one channel / unit.
+    const int row = tid >> 4, rl = tid & 15;
+    for (int ch = row; ch < Cin; ch += ST_THREADS / 16) {
         float s = 0.0f;
-        for (int i = lane; i < hw; i += 64) s += xs[ch * hw + i];
-        s = ffc::wave_sum(s);
-        if (lane == 0) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
+        for (int i = rl; i < hw; i += 16) s += xs[ch * hw + i];
+        s = ffc::row16_sum(s);
+        if (rl == 15) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
     }
     __syncthreads();
-    for (int j = wave; j < a.hid; j += ST_THREADS / 64) {  // fc1: one wave per hidden unit
+    for (int j = row; j < a.hid; j += ST_THREADS / 16) {  // fc1: one 16-lane row per hidden unit
         float s = 0.0f;
-        for (int k = lane; k < Cin; k += 64) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
-        s = ffc::wave_sum(s);
-        if (lane == 0) hv[j] = fmaxf(s, 0.0f);
+        for (int k = rl; k < Cin; k += 16) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
+        s = ffc::row16_sum(s);
+        if (rl == 15) hv[j] = fmaxf(s, 0.0f);
     }
     __syncthreads();
     float g = 0.0f;
@@ -158,21 +161,20 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     auto finish = [&](int mt, int nt, const floatx16& acc) {
         const int p = nt * 32 + col;
         const bool valid = p < hw;
-        const float cnt = (float)min(32, hw - nt * 32);
+        const int nv = min(32, hw - nt * 32);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-            const float v = acc[r];
-            if (valid && o < c) a.t[((size_t)b * c + o) * hw + p] = v;
-            const float mean = ffc::half_wave_sum(valid ? v : 0.0f) / cnt;
-            const float d = valid ? v - mean : 0.0f;
-            const float m2 = ffc::half_wave_sum(d * d);
-            if (col == 0 && o < c) {
-                float* e = st + (nt * c + o) * 3;
-                e[0] = cnt;
-                e[1] = mean;
-                e[2] = m2;
-            }
+            if (valid && o < c) a.t[((size_t)b * c + o) * hw + p] = acc[r];
+        }
+        float mean, m2;
+        ffc::tile_row_stats(acc, nv, scr + wave * ffc::TILE_SCRATCH, mean, m2);
+        const int o = mt * 32 + (lane >> 1);
+        if ((lane & 1) == 0 && o < c) {
+            float* e = st + (nt * c + o) * 3;
+            e[0] = (float)nv;
+            e[1] = mean;
+            e[2] = m2;
         }
     };
     if (nsplit == 1) {
@@ -224,8 +226,8 @@ size_t st_lds(int Cin, int H, int W, int pool, int hid, int c, bool with_w) {
     const size_t hw = (size_t)h * w;
     const size_t nt = (hw + 31) / 32;
     const size_t Mpad = (size_t)((c + 31) & ~31);
-    return sizeof(float) * (((Cin * hw + 3) & ~(size_t)3) + ((Cin + 3) & ~3) + ((hid + 3) & ~3) + (nt * c * 3 + 3) / 4 * 4 + 4 * 16 * 64 +
-                            (with_w ? Cin * Mpad : 0));
+    return sizeof(float) * (((Cin * hw + 3) & ~(size_t)3) + ((Cin + 3) & ~3) + ((hid + 3) & ~3) + (nt * c * 3 + 3) / 4 * 4 +
+                            4 * 16 * 64 + 4 * ffc::TILE_SCRATCH + (with_w ? Cin * Mpad : 0));
 }
 
 }  // namespace
