@@ -85,6 +85,22 @@ __device__ __forceinline__ void tile_row_stats(const floatx16& acc, int nv, floa
     m2 = q + dpp_f<0xB1>(q);
 }
 
+// LDS-DMA copy of n4 16-byte groups from 16-byte aligned global memory into LDS by whole 64-lane
+// wave instructions (global_load_lds_dwordx4; lane i of an instruction lands at dst + 16 i bytes):
+// dst needs room for n4 rounded up to 64 groups.  Completion: the issuing waves' vmcnt (the next
+// __syncthreads waits for it).
+__device__ __forceinline__ void dma_copy16(const float* src, float* dst, int n4, int tid, int nthreads) {
+    typedef __attribute__((address_space(1))) void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    for (int i0 = 0; i0 < n4; i0 += nthreads) {
+        const int wbase = i0 + (tid & ~63);
+        if (wbase < n4) {
+            const int i = min(i0 + tid, n4 - 1);   // tail lanes repeat the last group inside the padding
+            __builtin_amdgcn_global_load_lds((gptr_t)(src + 4 * (size_t)i), (lptr_t)(dst + 4 * wbase), 16, 0, 0);
+        }
+    }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -106,6 +106,7 @@ struct FuArgs {
     int C, Mpad, in_relu, residual, has_in_affine;
     int wm_lds;   // mix weight staged in LDS (when it fits beside the Z/Y planes)
     int scr_off;  // float offset of the pass-0 stats scratch in LDS
+    int bn_off;   // float offset of the pass-1 BN scale/shift (4C floats)
     float norm;
 };
 
@@ -187,6 +188,13 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     if (tid == 0) g_fu_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
     FU_STAMP(0);
+    float* bnss = smem + a.bn_off;    // pass 1: BN scale [2C] | shift [2C]
+    if constexpr (PASS == 1) {
+        for (int i = tid; i < C2; i += FU_THREADS) {
+            bnss[i] = a.bn_scale[i];
+            bnss[C2 + i] = a.bn_shift[i];
+        }
+    }
 
     // 1. row R2C (real W-point FFT per (channel,row)), input transform fused
     for (int r = tid; r < C * H; r += FU_THREADS) {
@@ -268,7 +276,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             for (int r = 0; r < 16; ++r) {
                 const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (nvalid && o < C2) {
-                    const float v = fmaxf(fmaf(acc[r], a.bn_scale[o], a.bn_shift[o]), 0.0f);
+                    const float v = fmaxf(fmaf(acc[r], bnss[o], bnss[C2 + o]), 0.0f);
                     ((o & 1) ? Yim : Yre)[(o >> 1) * NB + n] = v;
                 }
             }
@@ -399,18 +407,19 @@ bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1))
 // the Y-imaginary plane.  bytes = 0: unsupported.
 struct FuLayout {
     size_t bytes;
-    int wm_lds, scr_off;
+    int wm_lds, scr_off, bn_off;
 };
 FuLayout fu_layout(int C, int H, int W) {
     const size_t plane = (size_t)C * H * (W / 2 + 1);
     const bool in_y = plane >= (size_t)FU_SCRATCH;
     for (int wm = 1; wm >= 0; --wm) {
         const size_t wfl = wm ? fu_wm_floats(C) : 0;
-        const size_t floats = 4 * plane + wfl + (in_y ? 0 : FU_SCRATCH);
+        const size_t scr = in_y ? 0 : FU_SCRATCH;
+        const size_t floats = 4 * plane + wfl + scr + 4 * (size_t)C;
         if (4 * floats <= 160 * 1024)
-            return {4 * floats, wm, (int)(in_y ? 3 * plane : 4 * plane + wfl)};
+            return {4 * floats, wm, (int)(in_y ? 3 * plane : 4 * plane + wfl), (int)(4 * plane + wfl + scr)};
     }
-    return {0, 0, 0};
+    return {0, 0, 0, 0};
 }
 
 
@@ -462,6 +471,7 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
     const FuLayout lay = fu_layout(C, H, W);
     a.wm_lds = lay.wm_lds;
     a.scr_off = lay.scr_off;
+    a.bn_off = lay.bn_off;
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;

@@ -25,7 +25,9 @@ struct StArgs {
     float* slab;         // [B][c] float4
     float* gate_out;     // optional (B, Cin) copy of the gate (tests / debugging), may be null
     int Cin, H, W, pool, hid, c;
-    int wt_lds;          // conv1 weight staged in LDS
+    int x_dma;           // sample copied by LDS-DMA (no pooling, 16-byte aligned rows)
+    // LDS layout (float offsets; -1: not staged, read from global)
+    int gate_off, hv_off, st_off, red_off, scr_off, wt_off, w1_off, w2_off;
 };
 
 constexpr int ST_THREADS = 256;
@@ -53,24 +55,30 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     const int hw = h * w;
     const int Mpad = (c + 31) & ~31;
     float* xs = sm;                      // [Cin][hw]
-    float* gate = xs + ((Cin * hw + 3) & ~3);  // [Cin]
-    float* hv = gate + ((Cin + 3) & ~3); // [hid]
-    float* st = hv + ((a.hid + 3) & ~3); // [ntile][c][3]
-    float* red = st + (((hw + 31) / 32) * c * 3 + 3) / 4 * 4;   // [4 waves][16][64] split-K partials
-    float* scr = red + 4 * 16 * 64;      // [4 waves][32 x 33] tile-stats scratch
-    float* wt = scr + 4 * ffc::TILE_SCRATCH;   // [Cin][Mpad] conv1 weight (when it fits)
+    float* gate = sm + a.gate_off;       // [Cin]
+    float* hv = sm + a.hv_off;           // [hid]
+    float* st = sm + a.st_off;           // [ntile][c][3]
+    float* red = sm + a.red_off;         // [4 waves][16][64] split-K partials
+    float* scr = sm + a.scr_off;         // [4 waves][32 x 33] tile-stats scratch
+    float* wt = sm + a.wt_off;           // [Cin][Mpad] conv1 weight (when staged)
+    const int hid = a.hid;
 
 #ifdef FFC_TRACE
     if (tid == 0) g_st_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
     ST_STAMP(0);
-    // 1. sample -> LDS (2x2 average pool on the way in)
+    // 1. sample, conv1 weight and SE weights -> LDS, all in flight at once (LDS-DMA; the 2x2
+    //    average pool, when present, on the way in through registers)
     const float* xb = a.x + (size_t)b * Cin * a.H * a.W;
+    if (a.wt_off >= 0) ffc::dma_copy16(a.wcT, wt, Cin * Mpad / 4, tid, ST_THREADS);
+    if (a.w1_off >= 0) {
+        ffc::dma_copy16(a.w1, sm + a.w1_off, hid * Cin / 4, tid, ST_THREADS);
+        ffc::dma_copy16(a.w2, sm + a.w2_off, Cin * hid / 4, tid, ST_THREADS);
+    }
     if (!a.pool) {
         const int n = Cin * hw;
-        if ((n & 3) == 0) {
-            for (int i = tid; i < n / 4; i += ST_THREADS)
-                reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xb)[i];
+        if (a.x_dma) {
+            ffc::dma_copy16(xb, xs, n / 4, tid, ST_THREADS);
         } else {
             for (int i = tid; i < n; i += ST_THREADS) xs[i] = xb[i];
         }
@@ -81,17 +89,13 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
             xs[i] = (((q[0] + q[1]) + q[a.W]) + q[a.W + 1]) * 0.25f;
         }
     }
-    if (a.wt_lds) {  // pre-transposed (Cin, Mpad) weight: plain coalesced copy
-        const int n4 = Cin * Mpad / 4;
-        for (int i = tid; i < n4; i += ST_THREADS)
-            reinterpret_cast<float4*>(wt)[i] = reinterpret_cast<const float4*>(a.wcT)[i];
-    }
     __syncthreads();
     ST_STAMP(1);
 
     // 2. SE gate.  Reductions run over 16-lane DPP rows (no shuffle chains): row q of the
     //    block (16 lanes, consecutive pixels / inputs: conflict-free LDS) owns one channel / unit.
     const int row = tid >> 4, rl = tid & 15;
+#pragma unroll 4
     for (int ch = row; ch < Cin; ch += ST_THREADS / 16) {
         float s = 0.0f;
         for (int i = rl; i < hw; i += 16) s += xs[ch * hw + i];
@@ -99,29 +103,31 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         if (rl == 15) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
     }
     __syncthreads();
-    for (int j = row; j < a.hid; j += ST_THREADS / 16) {  // fc1: one 16-lane row per hidden unit
+    for (int j = row; j < hid; j += ST_THREADS / 16) {  // fc1: one 16-lane row per hidden unit
         float s = 0.0f;
-        for (int k = rl; k < Cin; k += 16) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
+        if (a.w1_off >= 0) {
+            const float* w1 = sm + a.w1_off + j * Cin;
+            for (int k = rl; k < Cin; k += 16) s = fmaf(w1[k], gate[k], s);
+        } else {
+            for (int k = rl; k < Cin; k += 16) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
+        }
         s = ffc::row16_sum(s);
         if (rl == 15) hv[j] = fmaxf(s, 0.0f);
     }
     __syncthreads();
-    float g = 0.0f;
-    if (tid < Cin) {
+    // fc2 + sigmoid: one 16-lane row per input channel k (lanes over the hidden units)
+#pragma unroll 4
+    for (int k = row; k < Cin; k += ST_THREADS / 16) {
         float s = 0.0f;
-        for (int j = 0; j < a.hid; ++j) s = fmaf(a.w2[(size_t)tid * a.hid + j], hv[j], s);
-        g = 1.0f / (1.0f + expf(-s));
-    }
-    for (int k0 = 0; k0 < Cin; k0 += ST_THREADS) {  // Cin may exceed the block
-        const int k = k0 + tid;
-        float gk = g;
-        if (k0 > 0 && k < Cin) {
-            float s = 0.0f;
-            for (int j = 0; j < a.hid; ++j) s = fmaf(a.w2[(size_t)k * a.hid + j], hv[j], s);
-            gk = 1.0f / (1.0f + expf(-s));
+        if (a.w2_off >= 0) {
+            const float* w2 = sm + a.w2_off + k * hid;
+            for (int j = rl; j < hid; j += 16) s = fmaf(w2[j], hv[j], s);
+        } else {
+            for (int j = rl; j < hid; j += 16) s = fmaf(a.w2[(size_t)k * hid + j], hv[j], s);
         }
-        __syncthreads();
-        if (k < Cin) {
+        s = ffc::row16_sum(s);
+        if (rl == 15) {
+            const float gk = 1.0f / (1.0f + expf(-s));   // hidden = 0: sigmoid(0) = 0.5
             gate[k] = gk;
             if (a.gate_out) a.gate_out[(size_t)b * Cin + k] = gk;
         }
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     const int tiles = MT * NT;
     const int nsplit = tiles >= 4 ? 1 : 4 / tiles;
     const int KS = Cin / 2;
-    const float* wa = a.wt_lds ? wt : a.wcT;
+    const float* wa = a.wt_off >= 0 ? wt : a.wcT;
     auto mfma_range = [&](int mt, int nt, int s0, int s1, bool odd_tail) {
         floatx16 acc;
 #pragma unroll
@@ -221,13 +227,56 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
 #endif
 }
 
-size_t st_lds(int Cin, int H, int W, int pool, int hid, int c, bool with_w) {
+// LDS plan (floats): sample, gate, hidden, tile stats, split-K partials, stats scratch, then the
+// conv1 weight and the SE weights when they fit (DMA regions padded to whole 64 x 16-B groups).
+struct StLayout {
+    size_t bytes;
+    int gate_off, hv_off, st_off, red_off, scr_off, wt_off, w1_off, w2_off;
+};
+size_t pad256(size_t n) { return (n + 255) / 256 * 256; }
+StLayout st_layout(int Cin, int H, int W, int pool, int hid, int c) {
     const int h = pool ? H / 2 : H, w = pool ? W / 2 : W;
     const size_t hw = (size_t)h * w;
     const size_t nt = (hw + 31) / 32;
     const size_t Mpad = (size_t)((c + 31) & ~31);
-    return sizeof(float) * (((Cin * hw + 3) & ~(size_t)3) + ((Cin + 3) & ~3) + ((hid + 3) & ~3) + (nt * c * 3 + 3) / 4 * 4 +
-                            4 * 16 * 64 + 4 * ffc::TILE_SCRATCH + (with_w ? Cin * Mpad : 0));
+    StLayout L{};
+    size_t o = pad256((size_t)Cin * hw);
+    L.gate_off = (int)o;
+    o += (Cin + 3) & ~3;
+    L.hv_off = (int)o;
+    o += (hid + 3) & ~3;
+    L.st_off = (int)o;
+    o += (nt * c * 3 + 3) / 4 * 4;
+    L.red_off = (int)o;
+    o += 4 * 16 * 64;
+    L.scr_off = (int)o;
+    o += 4 * ffc::TILE_SCRATCH;
+    const size_t base = o;
+    const bool w12_ok = hid > 0 && ((size_t)hid * Cin) % 4 == 0;
+    for (int opt = 0; opt < 3; ++opt) {   // 0: conv1 + SE weights staged, 1: conv1 only, 2: neither
+        size_t q = base;
+        int wt = -1, w1 = -1, w2 = -1;
+        if (opt < 2) {
+            wt = (int)q;
+            q += pad256((size_t)Cin * Mpad);
+        }
+        if (opt == 0) {
+            if (!w12_ok) continue;
+            w1 = (int)q;
+            q += pad256((size_t)hid * Cin);
+            w2 = (int)q;
+            q += pad256((size_t)hid * Cin);
+        }
+        if (4 * q <= 160 * 1024) {
+            L.bytes = 4 * q;
+            L.wt_off = wt;
+            L.w1_off = w1;
+            L.w2_off = w2;
+            return L;
+        }
+    }
+    L.bytes = 0;
+    return L;
 }
 
 }  // namespace
@@ -241,10 +290,7 @@ extern "C" int ffc_debug_st_trace_read(void* dst, size_t bytes) {
 extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c) {
     if (Cin <= 0 || H <= 0 || W <= 0 || c <= 0 || hidden < 0) return 0;
     if (pool && ((H | W) & 1)) return 0;
-    const size_t bw = st_lds(Cin, H, W, pool, hidden, c, true);
-    if (bw <= 160 * 1024) return bw;
-    const size_t b = st_lds(Cin, H, W, pool, hidden, c, false);
-    return b <= 160 * 1024 ? b : 0;
+    return st_layout(Cin, H, W, pool, hidden, c).bytes;
 }
 
 extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
@@ -280,7 +326,20 @@ extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int
     a.pool = pool;
     a.hid = hidden;
     a.c = c;
-    a.wt_lds = st_lds(Cin, H, W, pool, hidden, c, true) <= 160 * 1024;
+    const StLayout L = st_layout(Cin, H, W, pool, hidden, c);
+    a.gate_off = L.gate_off;
+    a.hv_off = L.hv_off;
+    a.st_off = L.st_off;
+    a.red_off = L.red_off;
+    a.scr_off = L.scr_off;
+    a.wt_off = L.wt_off;
+    a.w1_off = L.w1_off;
+    a.w2_off = L.w2_off;
+    a.x_dma = !pool && ((size_t)Cin * H * W) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (L.w1_off >= 0 && ((reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2)) & 15)) {
+        a.w1_off = a.w2_off = -1;   // unaligned SE weights: read from global
+    }
+    if (L.wt_off >= 0 && (reinterpret_cast<uintptr_t>(wconv1T) & 15)) a.wt_off = -1;
     hipLaunchKernelGGL(st_prologue_kernel, dim3(B), dim3(ST_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_st_prologue");
 }

@@ -45,7 +45,7 @@ def test_argument_validation_without_gpu():
     """invalid shapes are rejected before any launch, with a readable error"""
     lib = _lib.load()
     # Z/Y planes (Re, Im) + the mix weight (2C x ceil32(2C), whole 256-float DMA groups)
-    assert lib.ffc_fu_lds_bytes(16, 32, 32) == 16 * 16 * 32 * 17 + 4 * 32 * 32
+    assert lib.ffc_fu_lds_bytes(16, 32, 32) == 16 * 16 * 32 * 17 + 4 * 32 * 32 + 4 * 4 * 16   # + BN scale/shift
     assert lib.ffc_fu_lds_bytes(16, 64, 64) == 0          # large planes: next round
     assert lib.ffc_fu_lds_bytes(16, 12, 12) == 0          # not a power of two
     rc = lib.ffc_fu_forward(None, 1, 4, 12, 12, 1, None, None, 0, None, 0, None, None, None, 0, None, None)
