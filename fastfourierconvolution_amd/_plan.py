@@ -378,6 +378,11 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
 
 def pick_patch_cfg(B, M, segs):
     """4-phase jobs: NTW=4 unless that leaves fewer than ~2 workgroups per CU."""
+    force = os.environ.get("FFC_PATCH_CFG4")   # A/B measurements: force the 4-phase configuration
+    if force is not None:
+        q = plan_patch_job(B, M, segs, int(force))
+        if q is not None:
+            return q
     p = plan_patch_job(B, M, segs)
     if p is None:
         return plan_patch_job(B, M, segs, 1)   # a smaller pixel block may still fit the staging limits
