@@ -7,11 +7,12 @@
 // produces their 4x4 output pixels (2my+py, 2mx+px) for all M channels from the 4x4 input
 // neighbourhood it reads once per channel:
 //     py = 0: (ky=1, dy=0), (ky=3, dy=-1)      py = 1: (ky=0, dy=+1), (ky=2, dy=0)
-// A workgroup covers a 32x32 input tile (+1 halo).  8-channel chunks of the tile and of the
-// weights are staged in LDS by LDS-DMA (global_load_lds_dword, zero fill outside the image),
-// double buffered; the weights of a channel are read as wave-uniform (broadcast) ds_read_b128
-// and reused by the thread's 4 pixels, so the loop is FMA-bound: per channel 16 patch reads +
-// 4M broadcast reads feed 64M FMAs.
+// A workgroup covers a 32x32 input tile (+1 halo) with two halves of 256 threads that split the
+// channel chunks (even / odd 8-channel chunks; two waves per SIMD) and add their partial sums
+// in a fixed order at the end.  Each half's chunk of the tile and of the weights is staged in
+// LDS by LDS-DMA (global_load_lds_dword, zero fill outside the image), double buffered; the
+// weights of a channel are read as wave-uniform (broadcast) ds_read_b128 and reused by the
+// thread's 4 pixels: per channel 16 patch reads + 4M broadcast reads feed 64M FMAs.
 #include "ffc_internal.h"
 
 namespace {
@@ -21,7 +22,8 @@ constexpr int TT = 32;       // input tile (TT x TT), 16 x 16 threads x 2 x 2 pi
 constexpr int PP = TT + 2;   // patch side with halo
 constexpr int PE = CCH * PP * PP;
 constexpr int WE = CCH * 4 * 16;          // chunk weights (M <= 4)
-constexpr int EBUF = ((PE + WE) + 255) & ~255;
+constexpr int EBUF = ((PE + WE) + 255) & ~255;   // 4 buffers (2 halves x 2 stages) = 160 KiB
+constexpr int SM_THREADS = 512;
 
 __device__ float g_zero_sm[64];
 typedef __attribute__((address_space(1))) void* gptr_t;
@@ -41,9 +43,9 @@ struct SmallMArgs {
 };
 
 template <int MM>
-__global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a) {
+__global__ __launch_bounds__(SM_THREADS) void convt_smallm_kernel(SmallMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int tid = threadIdx.x, wave = tid >> 6;
+    const int half = threadIdx.x >> 8, tid = threadIdx.x & 255, wave = tid >> 6;
     int bid = blockIdx.x;
     const int tx = bid % a.ntx;
     bid /= a.ntx;
@@ -87,11 +89,14 @@ __global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[m][i][j] = 0.0f;
 
-    stage(0, lds);
-    for (int ci = 0; ci < nchunks; ++ci) {
+    const int nsteps = (nchunks + 1) / 2;   // half h takes chunks 2k + h
+    if (half < nchunks) stage(half, lds + half * EBUF);
+    for (int k = 0; k < nsteps; ++k) {
         __syncthreads();
-        if (ci + 1 < nchunks) stage(ci + 1, lds + ((ci + 1) & 1) * EBUF);
-        const float* cur = lds + (ci & 1) * EBUF;
+        const int ci = 2 * k + half;
+        if (ci + 2 < nchunks) stage(ci + 2, lds + (((k + 1) & 1) * 2 + half) * EBUF);
+        if (ci >= nchunks) continue;
+        const float* cur = lds + ((k & 1) * 2 + half) * EBUF;
         const int s = ci < nch0 ? 0 : 1;
         const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
         const int cn = min(CCH, a.C[s] - c0);
@@ -139,6 +144,25 @@ __global__ __launch_bounds__(256) void convt_smallm_kernel(SmallMArgs a) {
             }
         }
     }
+    // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
+    __syncthreads();
+    float* part = lds;   // 256 threads x MM x 16 (the stage buffers are free now)
+    if (half == 1) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * 256 + tid] = acc[m][i][j];
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[m][i][j] += part[((m * 4 + i) * 4 + j) * 256 + tid];
     const int OH = 2 * a.IH, OW = 2 * a.IW;
     const int oy0 = 2 * (y0 + qy), ox0 = 2 * (x0 + qx);
     const bool xin = x0 + qx + 1 < a.IW;   // both input columns in range
@@ -201,7 +225,7 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, c
     a.ntx = (IW + TT - 1) / TT;
     a.act = act;
     a.act_param = act_param;
-    const size_t lds = 2 * (size_t)EBUF * sizeof(float);
+    const size_t lds = 4 * (size_t)EBUF * sizeof(float);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     auto k = convt_smallm_kernel<4>;
     static bool raised = false;
@@ -213,6 +237,6 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, c
         }
         raised = true;
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_convt_k4s2_smallm");
 }
