@@ -207,6 +207,25 @@ def algorithmic_flops(plan) -> float:
 USE_PATCH = True   # LDS-patch kernel where it applies (tests flip this to cover the generic kernel)
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
+# Run SpectralTransform's kernels on a side stream beside the local-branch GEMM of the same FFC
+# layer ("gemm-first" / "spectral-first": which is issued first).  Off by default: measured on
+# MI355X (B=256 generator) 10-18 % slower than one launch pairing the local and global GEMMs,
+# because the FU / ST kernels' LDS footprint cannot co-reside with the GEMM workgroups and the
+# separate GEMM launches lose the heavy/light tile pairing.
+OVERLAP_SPECTRAL = __import__("os").environ.get("FFC_OVERLAP", "off")
+if OVERLAP_SPECTRAL in ("0", "off", "false"):
+    OVERLAP_SPECTRAL = False
+
+_SIDE = {}
+
+
+def side_stream(device):
+    """one side stream per device (created once, outside any graph capture of later steps)"""
+    key = str(device)
+    s = _SIDE.get(key)
+    if s is None:
+        s = _SIDE[key] = torch.cuda.Stream(device=device)
+    return s
 
 
 class ConvExec:

@@ -59,6 +59,33 @@ class _FFCExec:
             M = self.convl2l.out_channels if isinstance(self.convl2l, (nn.Conv2d, nn.ConvTranspose2d)) else (
                 self.convg2l.out_channels if isinstance(self.convg2l, (nn.Conv2d, nn.ConvTranspose2d)) else None)
             branches.append(("l", segs, w, inp, add, act_l, bn_l, M))
+        spectral = (self.ratio_gout != 0 and isinstance(self.convg2g, SpectralTransform) and y is None and
+                    isinstance(x_g, torch.Tensor))
+        if rt.OVERLAP_SPECTRAL and spectral and branches and branches[0][1]:
+            # The local branch does not depend on the spectral chain: its GEMM runs on the main stream
+            # while SpectralTransform's latency-bound kernels run on a side stream (fork / join by
+            # events, hipGraph-capturable); then the global-branch GEMM consumes v.
+            main = torch.cuda.current_stream(dev)
+            side = rt.side_stream(dev)
+            side.wait_stream(main)
+            if rt.OVERLAP_SPECTRAL == "spectral-first":
+                with torch.cuda.stream(side):
+                    v = self.convg2g.spectral(x_g)
+                out_l, _ = self._launch_branches(branches, B, dev, stream)
+            else:
+                out_l, _ = self._launch_branches(branches, B, dev, stream)
+                with torch.cuda.stream(side):
+                    v = self.convg2g.spectral(x_g)
+            main.wait_stream(side)
+            v.record_stream(main)
+            segs, w, inp, add = self._branch([(self.convl2g, x_l)])
+            segs.append(_plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]))
+            w.append(rt.conv_weight(self.convg2g.conv2))
+            inp.append((v, None))
+            M = self.convl2g.out_channels if isinstance(self.convl2g, (nn.Conv2d, nn.ConvTranspose2d)) else \
+                self.convg2g.conv2.out_channels
+            _, out_g = self._launch_branches([("g", segs, w, inp, add, act_g, bn_g, M)], B, dev, stream)
+            return out_l, out_g
         if self.ratio_gout != 0:
             segs, w, inp, add = self._branch([(self.convl2g, x_l)])
             if not isinstance(self.convg2g, nn.Identity):
@@ -78,7 +105,11 @@ class _FFCExec:
             M = self.convl2g.out_channels if isinstance(self.convl2g, (nn.Conv2d, nn.ConvTranspose2d)) else (
                 self.convg2g.conv2.out_channels if isinstance(self.convg2g, SpectralTransform) else None)
             branches.append(("g", segs, w, inp, add, act_g, bn_g, M))
+        return self._launch_branches(branches, B, dev, stream)
 
+    def _launch_branches(self, branches, B, dev, stream):
+        """plan / pack / launch the GEMM(s) of the given branches (one launch per kernel kind),
+        then BN statistics and BN+activation passes.  -> (out_l, out_g)"""
         outs = {"l": 0, "g": 0}
         execs, jobs, post = [], [], []
         for name, segs, w, inp, add, act, bn, M in branches:
