@@ -48,13 +48,13 @@ class ConvPSeg(ctypes.Structure):
 
 class ConvPPhase(ctypes.Structure):
     _fields_ = [("py", c_int), ("px", c_int), ("PH", c_int), ("PW", c_int), ("Kpad", c_int),
-                ("T", c_int * MAX_SEG), ("kseg", c_int * MAX_SEG), ("tap_base", c_int * MAX_SEG),
+                ("T", c_int * MAX_SEG), ("kseg", c_int * MAX_SEG), ("tap", (c_int * 4) * MAX_SEG),
                 ("a_off", c_longlong)]
 
 
 class ConvPJob(ctypes.Structure):
     _fields_ = [("seg", ConvPSeg * MAX_SEG), ("ph", ConvPPhase * 4),
-                ("A", c_void_p), ("taptab", c_void_p), ("out", c_void_p), ("bias", c_void_p),
+                ("A", c_void_p), ("out", c_void_p), ("bias", c_void_p),
                 ("addend", c_void_p), ("stats", c_void_p),
                 ("nseg", c_int), ("nphase", c_int), ("B", c_int), ("M", c_int), ("Mpad", c_int),
                 ("OH", c_int), ("OW", c_int), ("Sy", c_int), ("Sx", c_int),

@@ -239,11 +239,9 @@ class ConvExec:
         if pp is not None:
             self.kind, self.plan = "patch", pp
             self.launch_key = ("patch", pp.cfg)
-            self.taptab = torch.from_numpy(pp.taptab.copy()).to(device)
         else:
             self.kind, self.plan = "gemm", _plan.plan_job(B, M, segs)
             self.launch_key = ("gemm",)
-            self.taptab = None
         self.device = device
         self.ktab = torch.from_numpy(self.plan.ktab.copy()).to(device)
         # + tail padding: the patch kernel loads all 4 tap groups of a chunk, used or not
@@ -298,9 +296,10 @@ class ConvExec:
             p = job.ph[i]
             p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]
             for si in range(len(pl.segs)):
-                p.T[si], p.kseg[si], p.tap_base[si] = ph["T"][si], ph["kseg"][si], ph["tap_base"][si]
+                p.T[si], p.kseg[si] = ph["T"][si], ph["kseg"][si]
+                for t in range(ph["T"][si]):
+                    p.tap[si][t] = int(pl.taptab[ph["tap_base"][si] + t])
         job.A = self.A.data_ptr()
-        job.taptab = self.taptab.data_ptr()
         job.bias = self.bias.data_ptr() if self.bias is not None else None
         return job
 

@@ -135,12 +135,15 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         const int step = S.vec4 ? 4 : 1;
         st.nunits = NS * CC * PR * PCu;
         st.chn = 0;
+        // n / d as umulhi(n, ceil(2^32 / d)): exact for n < 2^16 (n < 2048 units here); d = 1 special
+        const unsigned mPC = PCu > 1 ? 0xFFFFFFFFu / (unsigned)PCu + 1u : 0u;
+        const unsigned mPR = PR > 1 ? 0xFFFFFFFFu / (unsigned)PR + 1u : 0u;
 #pragma unroll
         for (int e = 0; e < NEMAX; ++e) {
-            const unsigned n = (unsigned)(e * 256 + tid);   // once per segment: plain division
-            const unsigned q1 = n / (unsigned)PCu;
+            const unsigned n = (unsigned)(e * 256 + tid);
+            const unsigned q1 = PCu > 1 ? __umulhi(n, mPC) : n;
             const int g = (int)(n - q1 * PCu);
-            const unsigned q2 = q1 / (unsigned)PR;
+            const unsigned q2 = PR > 1 ? __umulhi(q1, mPR) : q1;
             const int pr = (int)(q1 - q2 * PR);
             const int ns = (int)(q2 >> 4), ch = (int)(q2 & 15);
             const int b = b0 + ns, iy = iy0 + pr, ix = xa + g * step;
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         int tap[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const int tt = J.taptab[P.tap_base[s] + (t & (T - 1))];
+            const int tt = P.tap[s][t & (T - 1)];
             tap[t] = (tt >> 16) * PCa + (tt & 0xFFFF);
         }
 #pragma unroll
@@ -237,6 +240,10 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         sch = 0;
         stage_setup(1);
     }
+#ifdef FFC_TRACE
+    unsigned long long tr_ls, tr_le;
+    FFC_STAMP(tr_ls);
+#endif
     for (int ci = 0; ci < nchunks; ++ci) {
 #ifdef FFC_TRACE
         FFC_STAMP(tr_a);
@@ -299,6 +306,9 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
             compute_setup(cs);
         }
     }
+#ifdef FFC_TRACE
+    FFC_STAMP(tr_le);
+#endif
 
     // ---------------- epilogue: bias/addend, BN partials, activation, store
     const size_t plane = (size_t)J.OH * J.OW;
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         t[4] = tr_stg;
         t[5] = tr_mf;
         t[6] = tr_c1 - tr_c0;
-        t[7] = (unsigned long long)nchunks;
+        t[7] = (tr_ls - tr_c0) | ((tr_c1 - tr_le) << 32);   // prologue | epilogue cycles
     }
 #endif
 }
@@ -419,7 +429,7 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
     const int np = (cfg <= 1) ? 4 : 1;
     for (int j = 0; j < njobs; ++j) {
         const ffc_convp_job& J = jobs[j];
-        FFC_CHECK_ARG(J.A && J.taptab && J.out && J.B > 0 && J.M > 0, "ffc_convp_forward: incomplete job");
+        FFC_CHECK_ARG(J.A && J.out && J.B > 0 && J.M > 0, "ffc_convp_forward: incomplete job");
         FFC_CHECK_ARG(J.nphase == np, "ffc_convp_forward: phase count does not match cfg");
         FFC_CHECK_ARG(J.nseg >= 1 && J.nseg <= FFC_MAX_SEG, "ffc_convp_forward: nseg out of range");
         FFC_CHECK_ARG(J.Mpad % 128 == 0 && J.Mpad >= J.M, "ffc_convp_forward: Mpad");

@@ -103,8 +103,8 @@ int ffc_conv_stat_rows_per_tile(int tile_cfg);
  * HBM/L2 once per block instead of once per (phase, tap).  Requires the taps per phase of each
  * segment to divide 4 (ConvT k4 s2: 4; 1x1: 1).  A is packed with every segment's channels
  * padded to a multiple of 16 (k = (seg, ch, tap)); the packed buffer needs >= 64 floats of tail padding
- * (groups of taps a phase does not use are loaded, not multiplied).  taptab entries are
- * (dy << 16) | dx, the tap's offset from the patch origin.  Per-thread staging holds at most 2048
+ * (groups of taps a phase does not use are loaded, not multiplied).  Tap offsets travel in the
+ * phase descriptor (kernel arguments, no table in memory).  Per-thread staging holds at most 2048
  * units (16-byte groups when vec4, else floats) of NS x 16 x PR x PC. */
 #define FFC_PATCH_CC 16
 typedef struct ffc_convp_seg {
@@ -124,7 +124,7 @@ typedef struct ffc_convp_phase {
     int Kpad;            /* sum over segments of Cpad * T[s] */
     int T[FFC_MAX_SEG];  /* taps of each segment in this phase (1, 2 or 4, or 0) */
     int kseg[FFC_MAX_SEG];   /* k offset of each segment inside the phase's packed rows */
-    int tap_base[FFC_MAX_SEG];  /* offset of the segment's patch-relative tap offsets in taptab */
+    int tap[FFC_MAX_SEG][4];    /* each segment's taps: (dy << 16) | dx from the patch origin */
     long long a_off;     /* float offset of the phase's packed weights [Mpad][Kpad] */
 } ffc_convp_phase;
 
@@ -132,7 +132,6 @@ typedef struct ffc_convp_job {
     ffc_convp_seg seg[FFC_MAX_SEG];
     ffc_convp_phase ph[4];
     const float* A;
-    const int* taptab;   /* patch-relative tap offsets (dy*PC + dx) */
     float* out;
     const float* bias;
     const float* addend;

@@ -88,8 +88,13 @@ def main():
             if sel.any():
                 d = dur[sel]
                 f = buf[sel][:, 3:6].astype(np.float64).sum(0) / buf[sel][:, 6].astype(np.float64).sum()
+                pe = buf[sel][:, 7]
+                tot = buf[sel][:, 6].astype(np.float64).sum()
+                pro = (pe & np.uint64(0xFFFFFFFF)).astype(np.float64).sum() / tot
+                epi = (pe >> np.uint64(32)).astype(np.float64).sum() / tot
                 print(f"   job {j}: {sel.sum()} WGs  dur us mean {d.mean():.1f} min {d.min():.1f} max {d.max():.1f}  "
-                      f"chunks {int(buf[sel][0, 7])}  wave0 share: barrier {f[0]:.2f} stage {f[1]:.2f} mfma {f[2]:.2f}")
+                      f"wave0 share: prologue {pro:.2f} barrier {f[0]:.2f} stage {f[1]:.2f} mfma {f[2]:.2f} "
+                      f"epilogue {epi:.2f}")
 
 
 if __name__ == "__main__":
