@@ -43,10 +43,13 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def parse():
     p = argparse.ArgumentParser()
+    p.add_argument("--workload", choices=["gen64", "fgan128"], default="gen64",
+                   help="gen64: FFCGenerator 64x64 (BASELINE metric, configs[1]/[2]); "
+                        "fgan128: fgan128 FGenerator 128x128x3 (configs[3], per-GPU shard)")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=256, help="samples per GPU")
+    p.add_argument("--batch", type=int, default=None, help="samples per GPU (gen64: 256, fgan128: 64)")
     p.add_argument("--nz", type=int, default=100)
     p.add_argument("--nc", type=int, default=3)
     p.add_argument("--ngf", type=int, default=64)
@@ -81,6 +84,41 @@ def pmc_traffic(label):
             "source": os.path.relpath(files[-1], ROOT)}
 
 
+def fgan_cpu_baseline(args, G, cpu_state, z_cpu, step):
+    """fgan128: the oracle's fp32 torch-CPU FGenerator (train mode draws its noise on the CPU) on a
+    bounded sample of the batch; parity in eval mode (noise-free) on the same sample."""
+    from oracle.ffc_oracle import fgan128_generator, normwise_err
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    nb = min(args.batch, 8)
+    training = args.bn_mode == "train"
+    zs = z_cpu[:nb]
+
+    def noises():
+        return [(torch.randn(nb, 1, 2 ** (n + 1), 2 ** (n + 1)), torch.randn(nb, 1, 2 ** (n + 1), 2 ** (n + 1)))
+                for n in (2, 3, 4, 5, 6)] if training else None
+    with torch.no_grad():
+        sd = {k: v.clone() for k, v in cpu_state.items()}
+        iters, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds or iters == 0:
+            fgan128_generator(zs, sd, training, noises(), fft="torch")
+            iters += 1
+        el = time.perf_counter() - t0
+        # parity: eval mode on the GPU model's running stats
+        G.eval()
+        sd = {k: v.detach().cpu().clone() for k, v in G.state_dict().items()}
+        ref = fgan128_generator(zs.double(), {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()},
+                                False)
+        got = G.forward_float(zs.to(next(G.parameters()).device)).cpu()
+        G.train(training)
+    cpu = {"value": round(nb * iters / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
+           "sample": f"oracle fp32 torch-CPU fgan128 FGenerator fwd, B={nb} (bounded sample), {iters} iterations "
+                     f"in {el:.1f}s, {args.bn_mode}-mode BN"}
+    parity = {"normwise_err_vs_cpu_ref": normwise_err(got, ref), "mode": "eval (fp64 oracle, same weights/stats)",
+              "tolerance": 1e-4}
+    return cpu, parity
+
+
 def weights_init(m):
     """fgan64_complete.py:22-31"""
     import torch.nn as nn
@@ -94,6 +132,9 @@ def weights_init(m):
 
 def main():
     args = parse()
+    if args.batch is None:
+        args.batch = 256 if args.workload == "gen64" else 64
+    fgan = args.workload == "fgan128"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -108,7 +149,7 @@ def main():
 
     torch.manual_seed(1234)
     with contextlib.redirect_stdout(io.StringIO()):
-        G = F.FFCGenerator(args.nz, args.nc, args.ngf)
+        G = F.FGenerator(128) if fgan else F.FFCGenerator(args.nz, args.nc, args.ngf)
     G.apply(weights_init)
     cpu_state = {k: v.clone() for k, v in G.state_dict().items()}
     G = G.to(dev).train(args.bn_mode == "train")
@@ -118,12 +159,12 @@ def main():
         if args.bn_mode == "train":
             D.enable_sync_bn()          # the only data-path exchange: BN moments all-reduce
     gen = torch.Generator(device="cpu").manual_seed(100 + rank)
-    z_cpu = torch.randn((args.batch, args.nz, 1, 1), generator=gen)
+    z_cpu = torch.randn((args.batch, 128) if fgan else (args.batch, args.nz, 1, 1), generator=gen)
     z = z_cpu.to(dev)
 
     def step():
         with torch.no_grad():
-            return G(z)
+            return G.forward_float(z) if fgan else G(z)
 
     for _ in range(max(1, args.warmup)):
         out = step()
@@ -140,7 +181,7 @@ def main():
             torch.cuda.current_stream().wait_stream(s)
             graph = torch.cuda.CUDAGraph()
             with torch.no_grad(), torch.cuda.graph(graph):
-                gout = G(z)
+                step()
             run = graph.replay
             run()
             torch.cuda.synchronize()
@@ -190,19 +231,21 @@ def main():
     roof["traffic"] = tr["bytes_per_launch"] if tr else None
     if tr:
         roof["traffic_source"] = tr["source"]
-    fu = {k: summ[k] for k in ("fu_pass0", "fu_pass1") if k in summ}
+    fu = {k: summ[k] for k in ("fu_pass0", "fu_pass1", "fu2d_r2c", "fu2d_c2r") if k in summ}
     fft_roof = None
     if fu:
         b = sum(v["bytes"] for v in fu.values())
         ms = sum(v["ms"] for v in fu.values())
-        fft_roof = {"kernel": "fu_pass0+fu_pass1", "bound": "hbm", "achieved": round(b / (ms * 1e-3) / 1e9, 1),
+        fft_roof = {"kernel": "+".join(fu), "bound": "hbm", "achieved": round(b / (ms * 1e-3) / 1e9, 1),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                     "algorithmic_bytes_per_step": b / max(1, args.profile_steps)}
 
     # ---- CPU baseline + parity (rank 0, N=1 only)
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and fgan:
+        cpu, parity = fgan_cpu_baseline(args, G, cpu_state, z_cpu, step)
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.ffc_oracle import ffc_generator, normwise_err
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         torch.set_num_threads(threads)
@@ -232,7 +275,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
-            "config": {"workload": f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) forward 64x64x{args.nc}",
+            "config": {"workload": ("fgan128 FGenerator(z=128, ngf=128) forward 128x128x3 (float output)" if fgan else
+                                    f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) forward 64x64x{args.nc}"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch, "bn_mode": args.bn_mode,
                        "hipgraph": use_graph, "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and
                                                                           args.bn_mode == "train" else "")},

@@ -4,13 +4,14 @@
 
 exports FourierUnitSN, SELayer, SpectralTransform, FFC, FFCTranspose, FFC_BN_ACT, Resizer,
 Print, debug_print, NoiseInjection (the names layers/__init__.py:2-18 exports for this path)
-plus the restated callers FFCModel / FFCGenerator / FFCDiscriminator.  All compute runs in
+plus the restated callers FFCModel / FFCGenerator / FFCDiscriminator / FGenerator (fgan128).  All compute runs in
 the gfx950 HIP library libffc_amd.so (include/ffc_amd.h); there is no CPU fallback.
 """
 from .config import Config
 from .ffc import FFC, FFC_BN_ACT, FFCTranspose, FourierUnitSN, SELayer, SpectralTransform
 from .layers_misc import NoiseInjection, Print, Resizer, debug_print
-from .models import FFCDiscriminator, FFCGenerator, FFCModel
+from .models import FFCDiscriminator, FFCGenerator, FFCModel, FGenerator
 
 __all__ = ["FourierUnitSN", "SELayer", "SpectralTransform", "FFC", "FFCTranspose", "FFC_BN_ACT", "Resizer",
-           "Print", "debug_print", "NoiseInjection", "FFCModel", "FFCGenerator", "FFCDiscriminator", "Config"]
+           "Print", "debug_print", "NoiseInjection", "FFCModel", "FFCGenerator", "FFCDiscriminator", "FGenerator",
+           "Config"]

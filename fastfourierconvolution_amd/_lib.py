@@ -90,6 +90,15 @@ SIGNATURES = [
     ("ffc_st_prologue_lds_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     ("ffc_st_prologue", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                 c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("ffc_fu2d_supported", c_int, [c_int, c_int, c_int, c_int]),
+    ("ffc_fu2d_slab_rows", c_int, [c_int, c_int, c_int, c_int]),
+    ("ffc_fu2d_r2c", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_fu2d_mix", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p]),
+    ("ffc_fu2d_c2r", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                             c_int, c_void_p, c_void_p]),
+    ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),
     ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                       c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
 ]

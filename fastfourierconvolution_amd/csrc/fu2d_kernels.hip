@@ -1,0 +1,652 @@
+// Large-plane Fourier unit for gfx950 (FU planes that do not fit one workgroup's LDS per sample:
+// the fgan128 generator's 64x64 and 128x128 FUs, fgan128_complete.py:474-485).
+//
+// Replaces FourierUnitSN.forward (layers/ffc/fourier_unity.py:32-56) with three HBM stages:
+//
+//   r2c  one workgroup per (sample, channel) plane of t (h x w = H/up x W/up):
+//        s0 = relu(t*in_scale + in_shift) (bn1 + act1, spectral_transform.py:89), 2-D real FFT
+//        in LDS -> T (B, C, h, w/2+1) complex, unnormalised.
+//   mix  per (sample, bin range): rebuild X = rfftn(s, ortho) from T, where s is s0
+//        nearest-upsampled by `up` (spectral_transform.py:44-45), using the identity
+//            X[kh][kw] = T[kh mod h][kw mod w] (1 + e^{-2 pi i kh/H}) (1 + e^{-2 pi i kw/W}) / sqrt(HW)
+//        (T folded through Hermitian symmetry for kw mod w > w/2), then the 1x1 spectral mix
+//        Y = Wmix Z on v_mfma_f32_32x32x2_f32 (Z = the interleaved Re/Im channels, :40-45).
+//        pass 0: BatchNorm partials {n, mean, M2} per output channel -> one slab row per workgroup
+//        pass 1: relu(Y*bn_scale + bn_shift) (:46-49) -> Y (B, C, H, W/2+1) complex
+//   c2r  one workgroup per output plane: irfftn(Y, s=(H, W), ortho) (:51-56) -- inverse column
+//        FFT, then the row C2R that ignores Im of bins 0 and W/2 (torch's C2R semantics) -- plus
+//        the SpectralTransform residual s (spectral_transform.py:108) -> out (B, C, H, W).
+//
+// Line FFTs of length N = N1*N2 are split over the N1 lanes of one wave: each lane runs an
+// N2-point FFT in registers, multiplies the twiddles W_N^{j k2}, and the lanes exchange through
+// the line's own LDS slots (same wave: LDS operations complete in issue order, no barrier) for
+// the N1-point FFTs.  The upsample identity lets r2c transform the 4x smaller t plane, and the
+// mix reads the 4x smaller T, so HBM carries: r2c t + T, mix T (+ Y), c2r Y + t + out.
+#include "ffc_internal.h"
+
+#include <cmath>
+#include <mutex>
+#include <set>
+
+#include "fft_common.h"
+
+namespace {
+
+constexpr int FU2_THREADS = 256;
+
+template <int N>
+struct Split {
+    static constexpr int N1 = N >= 64 ? 8 : (N >= 16 ? 4 : 2);
+    static constexpr int N2 = N / N1;
+    static constexpr int Q = N2 / N1;
+    static_assert(N1 * N2 == N && N2 % N1 == 0 && N <= 128, "line FFT split");
+};
+
+// twiddle W_N^e (e in [0, N)), forward exp(-2 pi i e/N) or inverse exp(+..)
+template <int N, bool INV>
+__device__ __forceinline__ void twiddle(int e, float& c, float& s) {
+    c = c_twc[e * (128 / N)];
+    s = INV ? c_tws[e * (128 / N)] : -c_tws[e * (128 / N)];
+}
+
+// Stage A on this lane's samples x[jj + N1*m] (m = 0..N2-1, in re/im): N2-point FFT in registers,
+// then the twiddles W_N^{jj*k2}.  Result index k2 holds Y[jj][k2].
+template <int N, bool INV>
+__device__ __forceinline__ void stage_a(float (&re)[Split<N>::N2], float (&im)[Split<N>::N2], int jj) {
+    constexpr int N2 = Split<N>::N2;
+    fft_reg<N2, INV>(re, im);
+#pragma unroll
+    for (int k2 = 1; k2 < N2; ++k2) {
+        float c, s;
+        twiddle<N, INV>(jj * k2, c, s);
+        const float xr = re[k2] * c - im[k2] * s;
+        im[k2] = re[k2] * s + im[k2] * c;
+        re[k2] = xr;
+    }
+}
+
+// Stage B through an LDS line of N float2 (element n at line[n*stride]): writes stage-A results,
+// reads back the N1-point columns k2 in {jj, jj+N1, ..} and transforms them.  On return
+// (ore, oim)[q][k1] = X[(jj + N1*q) + N2*k1].  Every lane of the group must call it (one wave).
+template <int N, bool INV>
+__device__ __forceinline__ void stage_b(float2* line, int stride, const float (&re)[Split<N>::N2],
+                                        const float (&im)[Split<N>::N2], int jj,
+                                        float (&ore)[Split<N>::Q][Split<N>::N1],
+                                        float (&oim)[Split<N>::Q][Split<N>::N1]) {
+    constexpr int N1 = Split<N>::N1, N2 = Split<N>::N2, Q = Split<N>::Q;
+#pragma unroll
+    for (int k2 = 0; k2 < N2; ++k2) line[(jj + N1 * k2) * stride] = make_float2(re[k2], im[k2]);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int k2 = jj + N1 * q;
+#pragma unroll
+        for (int n1 = 0; n1 < N1; ++n1) {
+            const float2 v = line[(n1 + N1 * k2) * stride];
+            ore[q][n1] = v.x;
+            oim[q][n1] = v.y;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) fft_reg<N1, INV>(ore[q], oim[q]);
+}
+
+// In-place length-N complex FFT of line[n*stride] by the N1 lanes jj of one wave.
+template <int N, bool INV>
+__device__ __forceinline__ void line_fft(float2* line, int stride, int jj) {
+    constexpr int N1 = Split<N>::N1, N2 = Split<N>::N2, Q = Split<N>::Q;
+    float re[N2], im[N2];
+#pragma unroll
+    for (int m = 0; m < N2; ++m) {
+        const float2 v = line[(jj + N1 * m) * stride];
+        re[m] = v.x;
+        im[m] = v.y;
+    }
+    stage_a<N, INV>(re, im, jj);
+    float ore[Q][N1], oim[Q][N1];
+    stage_b<N, INV>(line, stride, re, im, jj, ore, oim);
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int k1 = 0; k1 < N1; ++k1)
+            line[((jj + N1 * q) + N2 * k1) * stride] = make_float2(ore[q][k1], oim[q][k1]);
+}
+
+// Column pass over an (rows x ZS) float2 plane: length-`rows` FFTs of columns 0..ncols-1.
+template <int ROWS, bool INV>
+__device__ __forceinline__ void column_pass(float2* Z, int ZS, int ncols, int tid) {
+    constexpr int N1 = Split<ROWS>::N1;
+    constexpr int LPR = FU2_THREADS / N1;   // lines per round
+    const int jj = tid % N1;
+    for (int c0 = 0; c0 < ncols; c0 += LPR) {
+        const int col = c0 + tid / N1;
+        if (col < ncols) line_fft<ROWS, INV>(Z + col, ZS, jj);
+    }
+}
+
+__device__ __forceinline__ float in_tf(float v, float sc, float sh, int relu) {
+    v = fmaf(v, sc, sh);
+    return relu ? fmaxf(v, 0.0f) : v;
+}
+
+struct R2cArgs {
+    const float* t;
+    const float* in_scale;
+    const float* in_shift;
+    float* T;
+    int C, in_relu;
+};
+
+// ---------------------------------------------------------------- stage 1: R2C of the t planes
+// LDS: real plane R (h rows, stride w+4: conflict-free row-pair reads), complex plane Z (h x WPt).
+template <int h, int w>
+__global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
+    constexpr int WPt = w / 2 + 1;
+    constexpr int RS = w + 4;
+    constexpr int N1 = Split<w>::N1, N2 = Split<w>::N2, Q = Split<w>::Q;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* R = smem;
+    float2* Z = reinterpret_cast<float2*>(smem + h * RS);
+    const int plane = blockIdx.x;
+    const int ch = plane % a.C;
+    const int tid = threadIdx.x;
+    const float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
+    const float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
+
+    // 1. t plane -> transform -> R
+    const float4* src = reinterpret_cast<const float4*>(a.t + (size_t)plane * h * w);
+    for (int i = tid; i < h * w / 4; i += FU2_THREADS) {
+        float4 v = src[i];
+        v.x = in_tf(v.x, sc, sh, a.in_relu);
+        v.y = in_tf(v.y, sc, sh, a.in_relu);
+        v.z = in_tf(v.z, sc, sh, a.in_relu);
+        v.w = in_tf(v.w, sc, sh, a.in_relu);
+        const int r = i / (w / 4), c4 = i % (w / 4);
+        *reinterpret_cast<float4*>(R + r * RS + 4 * c4) = v;
+    }
+    __syncthreads();
+
+    // 2. rows, two at a time: z = R[2g] + i R[2g+1] -> FFT -> split into the two half spectra
+    {
+        constexpr int LPR = FU2_THREADS / N1;
+        const int jj = tid % N1;
+        for (int g0 = 0; g0 < h / 2; g0 += LPR) {
+            const int g = g0 + tid / N1;
+            if (g < h / 2) {
+                float re[N2], im[N2];
+#pragma unroll
+                for (int m = 0; m < N2; ++m) {
+                    re[m] = R[(2 * g) * RS + jj + N1 * m];
+                    im[m] = R[(2 * g + 1) * RS + jj + N1 * m];
+                }
+                stage_a<w, false>(re, im, jj);
+                float2* line = Z + 2 * g * WPt;   // rows 2g, 2g+1 of Z: 2*WPt >= w slots
+                float ore[Q][N1], oim[Q][N1];
+                stage_b<w, false>(line, 1, re, im, jj, ore, oim);
+#pragma unroll
+                for (int q = 0; q < Q; ++q)
+#pragma unroll
+                    for (int k1 = 0; k1 < N1; ++k1)
+                        line[(jj + N1 * q) + N2 * k1] = make_float2(ore[q][k1], oim[q][k1]);
+                // separate: A[k] = (Z[k] + conj Z[-k]) / 2, B[k] = (Z[k] - conj Z[-k]) / 2i, k = 0..w/2
+                constexpr int KPL = (WPt + N1 - 1) / N1;
+                float2 zk[KPL], zm[KPL];
+#pragma unroll
+                for (int i = 0; i < KPL; ++i) {
+                    const int k = jj + N1 * i;
+                    if (k < WPt) {
+                        zk[i] = line[k & (w - 1)];
+                        zm[i] = line[(w - k) & (w - 1)];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < KPL; ++i) {
+                    const int k = jj + N1 * i;
+                    if (k < WPt) {
+                        line[k] = make_float2(0.5f * (zk[i].x + zm[i].x), 0.5f * (zk[i].y - zm[i].y));
+                        line[WPt + k] = make_float2(0.5f * (zk[i].y + zm[i].y), -0.5f * (zk[i].x - zm[i].x));
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // 3. columns (length h) of the half spectrum
+    column_pass<h, false>(Z, WPt, WPt, tid);
+    __syncthreads();
+
+    // 4. Z -> T (contiguous h x WPt float2; h even so the plane is whole float4s)
+    float4* dst = reinterpret_cast<float4*>(a.T + (size_t)plane * h * WPt * 2);
+    const float4* zs = reinterpret_cast<const float4*>(Z);
+    for (int i = tid; i < h * WPt / 2; i += FU2_THREADS) dst[i] = zs[i];
+}
+
+// ---------------------------------------------------------------- stage 3: C2R + residual
+struct C2rArgs {
+    const float* Y;
+    const float* t;
+    const float* in_scale;
+    const float* in_shift;
+    float* out;
+    int C, in_relu, residual;
+    float norm;
+};
+
+template <int H, int W, int UP>
+__global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
+    constexpr int WP = W / 2 + 1;
+    constexpr int N1 = Split<W>::N1, N2 = Split<W>::N2, Q = Split<W>::Q;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float2* Z = reinterpret_cast<float2*>(smem);
+    const int plane = blockIdx.x;
+    const int ch = plane % a.C;
+    const int tid = threadIdx.x;
+
+    // 1. Y plane -> LDS by LDS-DMA (H*WP float2 = H*WP/2 16-byte groups)
+    ffc::dma_copy16(a.Y + (size_t)plane * H * WP * 2, smem, H * WP / 2, tid, FU2_THREADS);
+    __syncthreads();
+
+    // 2. inverse columns (length H)
+    column_pass<H, true>(Z, WP, WP, tid);
+    __syncthreads();
+
+    // 3. rows two at a time: z[k] = A_ext[k] + i B_ext[k] (Hermitian extension of each half
+    //    spectrum, Im of bins 0 and W/2 dropped) -> inverse FFT -> Re = row 2g, Im = row 2g+1
+    const float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
+    const float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
+    constexpr int tW = W / UP;
+    const float* tpl = a.t + (size_t)plane * (H / UP) * tW;
+    float* opl = a.out + (size_t)plane * H * W;
+    {
+        constexpr int LPR = FU2_THREADS / N1;
+        const int jj = tid % N1;
+        for (int g0 = 0; g0 < H / 2; g0 += LPR) {
+            const int g = g0 + tid / N1;
+            if (g < H / 2) {
+                float2* ra = Z + 2 * g * WP;
+                float2* rb = ra + WP;
+                float re[N2], im[N2];
+#pragma unroll
+                for (int m = 0; m < N2; ++m) {
+                    const int k = jj + N1 * m;
+                    float2 A, B;
+                    if (k <= W / 2) {
+                        A = ra[k];
+                        B = rb[k];
+                        if (k == 0 || k == W / 2) {
+                            A.y = 0.0f;
+                            B.y = 0.0f;
+                        }
+                    } else {
+                        A = ra[W - k];
+                        B = rb[W - k];
+                        A.y = -A.y;
+                        B.y = -B.y;
+                    }
+                    re[m] = A.x - B.y;
+                    im[m] = A.y + B.x;
+                }
+                stage_a<W, true>(re, im, jj);
+                float ore[Q][N1], oim[Q][N1];
+                stage_b<W, true>(ra, 1, re, im, jj, ore, oim);
+                float* fa = reinterpret_cast<float*>(ra);   // 4*WP >= 2W floats: row 2g then row 2g+1
+#pragma unroll
+                for (int q = 0; q < Q; ++q)
+#pragma unroll
+                    for (int k1 = 0; k1 < N1; ++k1) {
+                        const int x = (jj + N1 * q) + N2 * k1;
+                        fa[x] = ore[q][k1];
+                        fa[W + x] = oim[q][k1];
+                    }
+                // scale, residual, store (float4 per lane, the group covers both rows)
+#pragma unroll
+                for (int i = 0; i < (2 * W / 4 + N1 - 1) / N1; ++i) {
+                    const int q4 = jj + N1 * i;
+                    if (q4 < 2 * W / 4) {
+                        const int rr = q4 / (W / 4);
+                        const int x = 4 * (q4 % (W / 4));
+                        const int y = 2 * g + rr;
+                        float4 v = *reinterpret_cast<const float4*>(fa + rr * W + x);
+                        v.x *= a.norm;
+                        v.y *= a.norm;
+                        v.z *= a.norm;
+                        v.w *= a.norm;
+                        if (a.residual) {
+                            const float* trow = tpl + (y / UP) * tW;
+                            if constexpr (UP == 1) {
+                                const float4 s = *reinterpret_cast<const float4*>(trow + x);
+                                v.x += in_tf(s.x, sc, sh, a.in_relu);
+                                v.y += in_tf(s.y, sc, sh, a.in_relu);
+                                v.z += in_tf(s.z, sc, sh, a.in_relu);
+                                v.w += in_tf(s.w, sc, sh, a.in_relu);
+                            } else {
+                                const float2 s = *reinterpret_cast<const float2*>(trow + x / 2);
+                                const float s0 = in_tf(s.x, sc, sh, a.in_relu), s1 = in_tf(s.y, sc, sh, a.in_relu);
+                                v.x += s0;
+                                v.y += s0;
+                                v.z += s1;
+                                v.w += s1;
+                            }
+                        }
+                        *reinterpret_cast<float4*>(opl + (size_t)y * W + x) = v;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- stage 2: spectral mix
+struct MixArgs {
+    const float* T;
+    const float* wmixT;   // (2C, Mpad) transposed, zero padded
+    float* slab;          // pass 0: [B*nsplit][2C] float4
+    const float* bn_scale;
+    const float* bn_shift;
+    float* Y;             // pass 1: (B, C, H, WP) float2
+    int B, C, H, W, up, nsplit, ntiles, Mpad;
+    float norm;
+};
+
+constexpr int MIX_TILES_PER_WG = 8;
+
+template <int MT, int PASS>
+__global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int C = a.C, C2 = 2 * C;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hh = lane >> 5, col = lane & 31;
+    // sample-major within an XCD: consecutive ids go to consecutive XCDs, so b = id % B keeps a
+    // sample's workgroups (and its T) on one XCD's L2 when B % 8 == 0
+    const int b = blockIdx.x % a.B;
+    const int split = blockIdx.x / a.B;
+    const int t_lo = (int)((long long)split * a.ntiles / a.nsplit);
+    const int t_hi = (int)((long long)(split + 1) * a.ntiles / a.nsplit);
+
+    float* Wm = smem;                                         // (2C, Mpad), whole 64-lane DMA groups
+    float* bnss = smem + (C2 * a.Mpad + 255) / 256 * 256;     // pass 1: scale [2C] | shift [2C]
+    float* scr = bnss;                                        // pass 0: per-wave tile scratch + merge area
+    ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
+    if constexpr (PASS == 1) {
+        for (int i = tid; i < C2; i += FU2_THREADS) {
+            bnss[i] = a.bn_scale[i];
+            bnss[C2 + i] = a.bn_shift[i];
+        }
+    }
+    __syncthreads();
+
+    const int H = a.H, W = a.W, WP = W / 2 + 1, NB = H * WP;
+    const int h = H / a.up, w = W / a.up, WPt = w / 2 + 1;
+    const size_t planeT = (size_t)h * WPt;
+    const float2* Tb = reinterpret_cast<const float2*>(a.T) + (size_t)b * C * planeT;
+    const int tstepH = 128 / H, tstepW = 128 / W;
+
+    float st_n[MT], st_mean[MT], st_m2[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) st_n[mt] = st_mean[mt] = st_m2[mt] = 0.0f;
+
+    for (int tile = t_lo + wave; tile < t_hi; tile += FU2_THREADS / 64) {
+        const int n = tile * 32 + col;
+        const bool valid = n < NB;
+        // this lane's bin: source index in T, conjugation, and factor f = X / T
+        int idx = 0;
+        bool cj = false;
+        float fr = 0.0f, fi = 0.0f;
+        if (valid) {
+            const int kh = n / WP, kw = n - kh * WP;
+            if (a.up == 1) {
+                idx = n;
+                fr = a.norm;
+            } else {
+                const int khp = kh & (h - 1), kwp = kw & (w - 1);
+                if (kwp <= w / 2) {
+                    idx = khp * WPt + kwp;
+                } else {
+                    idx = ((h - khp) & (h - 1)) * WPt + (w - kwp);
+                    cj = true;
+                }
+                const float c1 = 1.0f + c_twc[kh * tstepH], s1 = -c_tws[kh * tstepH];
+                const float c2 = 1.0f + c_twc[kw * tstepW], s2 = -c_tws[kw * tstepW];
+                fr = (c1 * c2 - s1 * s2) * a.norm;
+                fi = (c1 * s2 + s1 * c2) * a.norm;
+            }
+        }
+        floatx16 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mt][r] = 0.0f;
+        const float2* tp = Tb + idx;
+        for (int s0 = 0; s0 < C; s0 += 8) {
+            float z[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                float2 tv = make_float2(0.0f, 0.0f);
+                if (s0 + u < C) tv = tp[(size_t)(s0 + u) * planeT];
+                if (cj) tv.y = -tv.y;
+                const float xr = tv.x * fr - tv.y * fi;
+                const float xi = tv.x * fi + tv.y * fr;
+                z[u] = hh ? xi : xr;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int s = s0 + u;
+                if (s < C) {
+                    const float* wr = Wm + (2 * s + hh) * a.Mpad + col;
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z[u], acc[mt], 0, 0, 0);
+                }
+            }
+        }
+        if constexpr (PASS == 0) {
+            const int nv = min(32, NB - tile * 32);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                float mean, m2;
+                ffc::tile_row_stats(acc[mt], nv, scr + wave * ffc::TILE_SCRATCH, mean, m2);
+                const float cn = (float)nv;
+                const float tot = st_n[mt] + cn;
+                const float delta = mean - st_mean[mt];
+                st_mean[mt] += delta * (cn / tot);
+                st_m2[mt] += m2 + delta * delta * (st_n[mt] * cn / tot);
+                st_n[mt] = tot;
+            }
+        } else {
+            float2* Yb = reinterpret_cast<float2*>(a.Y) + (size_t)b * C * NB;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) {
+                    const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even: Re, o+1: Im
+                    if (valid && o < C2) {
+                        const float re = fmaxf(fmaf(acc[mt][r], bnss[o], bnss[C2 + o]), 0.0f);
+                        const float im = fmaxf(fmaf(acc[mt][r + 1], bnss[o + 1], bnss[C2 + o + 1]), 0.0f);
+                        Yb[(size_t)(o >> 1) * NB + n] = make_float2(re, im);
+                    }
+                }
+        }
+    }
+
+    if constexpr (PASS == 0) {
+        // merge the 4 waves' partials (fixed order) -> slab row blockIdx.x
+        __syncthreads();
+        float4* mg = reinterpret_cast<float4*>(scr);   // [wave][MT*32]
+        if ((lane & 1) == 0) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                mg[wave * MT * 32 + mt * 32 + (lane >> 1)] = make_float4(st_n[mt], st_mean[mt], st_m2[mt], 0.0f);
+        }
+        __syncthreads();
+        for (int o = tid; o < C2; o += FU2_THREADS) {
+            float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+            for (int wv = 0; wv < FU2_THREADS / 64; ++wv) {
+                const float4 e = mg[wv * MT * 32 + o];
+                if (e.x > 0.0f) {
+                    const float tot = nn + e.x;
+                    const float delta = e.y - mean;
+                    mean += delta * (e.x / tot);
+                    m2 += e.z + delta * delta * (nn * e.x / tot);
+                    nn = tot;
+                }
+            }
+            reinterpret_cast<float4*>(a.slab)[(size_t)blockIdx.x * C2 + o] = make_float4(nn, mean, m2, 0.0f);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- host side
+bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
+
+typedef void (*R2cKernel)(R2cArgs);
+typedef void (*C2rKernel)(C2rArgs);
+typedef void (*MixKernel)(MixArgs);
+
+R2cKernel pick_r2c(int h, int w) {
+    if (h != w) return nullptr;
+    switch (h) {
+        case 16: return fu2d_r2c_kernel<16, 16>;
+        case 32: return fu2d_r2c_kernel<32, 32>;
+        case 64: return fu2d_r2c_kernel<64, 64>;
+        case 128: return fu2d_r2c_kernel<128, 128>;
+    }
+    return nullptr;
+}
+
+template <int N>
+C2rKernel pick_c2r_up(int up) { return up == 1 ? fu2d_c2r_kernel<N, N, 1> : fu2d_c2r_kernel<N, N, 2>; }
+
+C2rKernel pick_c2r(int H, int W, int up) {
+    if (H != W) return nullptr;
+    switch (H) {
+        case 32: return pick_c2r_up<32>(up);
+        case 64: return pick_c2r_up<64>(up);
+        case 128: return pick_c2r_up<128>(up);
+    }
+    return nullptr;
+}
+
+MixKernel pick_mix(int C, int pass) {
+    const int C2 = 2 * C;
+    if (C2 <= 32) return pass ? fu2d_mix_kernel<1, 1> : fu2d_mix_kernel<1, 0>;
+    if (C2 <= 64) return pass ? fu2d_mix_kernel<2, 1> : fu2d_mix_kernel<2, 0>;
+    if (C2 <= 128) return pass ? fu2d_mix_kernel<4, 1> : fu2d_mix_kernel<4, 0>;
+    return nullptr;
+}
+
+size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * (w / 2 + 1) * 8; }
+size_t c2r_lds(int H, int W) {
+    const size_t n4 = (size_t)H * (W / 2 + 1) / 2;           // 16-byte DMA groups
+    return ((n4 + 63) / 64 * 64) * 16;                        // whole 64-lane DMA instructions
+}
+size_t mix_wm_floats(int C) { return (size_t)(2 * C) * ((2 * C + 31) / 32 * 32); }
+size_t mix_lds(int C, int pass) {
+    const size_t wm = (mix_wm_floats(C) + 255) / 256 * 256;   // <= 64 KiB for 2C <= 128
+    const size_t tail = pass ? 4 * (size_t)C : (size_t)(FU2_THREADS / 64) * ffc::TILE_SCRATCH;
+    return 4 * (wm + tail);
+}
+
+int raise_lds(const void* k, size_t lds, const char* what) {
+    if (lds <= 64 * 1024) return FFC_OK;
+    static std::mutex mu;
+    static std::set<const void*> raised;
+    std::lock_guard<std::mutex> g(mu);
+    if (raised.count(k)) return FFC_OK;
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) {
+        ffc::set_error(std::string(what) + ": hipFuncSetAttribute: " + hipGetErrorString(e));
+        return FFC_E_LAUNCH;
+    }
+    raised.insert(k);
+    return FFC_OK;
+}
+
+// workgroups per sample: ~MIX_TILES_PER_WG bin tiles each (2 per wave)
+int mix_nsplit(int H, int W) {
+    const int ntiles = (H * (W / 2 + 1) + 31) / 32;
+    return std::max(1, ntiles / MIX_TILES_PER_WG);
+}
+
+}  // namespace
+
+extern "C" int ffc_fu2d_supported(int C, int H, int W, int up) {
+    if (C <= 0 || 2 * C > 128 || H != W || !(up == 1 || up == 2)) return 0;
+    if (!pow2_in(H, 32, 128)) return 0;
+    const int h = H / up;
+    if (!pow2_in(h, 16, 128)) return 0;
+    if (r2c_lds(h, h) > 160 * 1024 || c2r_lds(H, W) > 160 * 1024) return 0;
+    return 1;
+}
+
+extern "C" int ffc_fu2d_slab_rows(int B, int C, int H, int W) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+    return B * mix_nsplit(H, W);
+}
+
+extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const float* in_scale,
+                            const float* in_shift, int in_relu, float* T, void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_r2c: B and C must be positive");
+    FFC_CHECK_ARG(t && T, "ffc_fu2d_r2c: null pointer");
+    FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_r2c: in_scale/in_shift pairing");
+    R2cKernel k = pick_r2c(h, w);
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_r2c: unsupported plane (square, power of two in [16, 128])");
+    const size_t lds = r2c_lds(h, w);
+    FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_fu2d_r2c: plane exceeds LDS");
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c");
+    if (rc) return rc;
+    R2cArgs a{t, in_scale, in_shift, T, C, in_relu};
+    hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu2d_r2c");
+}
+
+extern "C" int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, const float* wmixT, int pass,
+                            float* stats_slab, const float* bn_scale, const float* bn_shift, float* Y,
+                            void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_mix: B and C must be positive");
+    FFC_CHECK_ARG(ffc_fu2d_supported(C, H, W, up), "ffc_fu2d_mix: unsupported (C, H, W, up)");
+    FFC_CHECK_ARG(T && wmixT, "ffc_fu2d_mix: null pointer");
+    FFC_CHECK_ARG(pass == 0 || pass == 1, "ffc_fu2d_mix: pass must be 0 or 1");
+    if (pass == 0) FFC_CHECK_ARG(stats_slab != nullptr, "ffc_fu2d_mix: pass 0 needs stats_slab");
+    if (pass == 1) FFC_CHECK_ARG(bn_scale && bn_shift && Y, "ffc_fu2d_mix: pass 1 needs bn_scale/shift/Y");
+    MixKernel k = pick_mix(C, pass);
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_mix: 2C > 128");
+    MixArgs a;
+    a.T = T;
+    a.wmixT = wmixT;
+    a.slab = stats_slab;
+    a.bn_scale = bn_scale;
+    a.bn_shift = bn_shift;
+    a.Y = Y;
+    a.B = B;
+    a.C = C;
+    a.H = H;
+    a.W = W;
+    a.up = up;
+    a.ntiles = (H * (W / 2 + 1) + 31) / 32;
+    a.nsplit = mix_nsplit(H, W);
+    a.Mpad = (2 * C + 31) / 32 * 32;
+    a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
+    const size_t lds = mix_lds(C, pass);
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_mix");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k, dim3(B * a.nsplit), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu2d_mix");
+}
+
+extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                            const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
+                            void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_c2r: B and C must be positive");
+    FFC_CHECK_ARG(Y && out, "ffc_fu2d_c2r: null pointer");
+    FFC_CHECK_ARG(!residual || t, "ffc_fu2d_c2r: residual needs t");
+    FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu2d_c2r: up must be 1 or 2");
+    FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
+    C2rKernel k = pick_c2r(H, W, up);
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [32, 128])");
+    const size_t lds = c2r_lds(H, W);
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_c2r");
+    if (rc) return rc;
+    C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W))};
+    hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu2d_c2r");
+}

@@ -20,51 +20,9 @@
 #include <mutex>
 #include <set>
 
-#include "twiddles.inc"
+#include "fft_common.h"
 
 namespace {
-
-constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n >> 1); }
-constexpr int brevc(int i, int bits) {
-    int r = 0;
-    for (int b = 0; b < bits; ++b) r |= ((i >> b) & 1) << (bits - 1 - b);
-    return r;
-}
-
-// In-register radix-2 DIT FFT, fully unrolled.  INV=false: exp(-2 pi i kn/N); INV=true: exp(+..).
-template <int N, bool INV>
-__device__ __forceinline__ void fft_reg(float (&re)[N], float (&im)[N]) {
-    constexpr int L = ilog2c(N);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const int j = brevc(i, L);
-        if (j > i) {
-            float t = re[i]; re[i] = re[j]; re[j] = t;
-            t = im[i]; im[i] = im[j]; im[j] = t;
-        }
-    }
-#pragma unroll
-    for (int half = 1; half < N; half <<= 1) {
-        const int step = 128 / (2 * half);
-#pragma unroll
-        for (int j = 0; j < half; ++j) {
-            float wr = 1.0f, wi = 0.0f;
-            if (j != 0) {
-                wr = c_twc[j * step];
-                wi = INV ? c_tws[j * step] : -c_tws[j * step];
-            }
-#pragma unroll
-            for (int i = j; i < N; i += 2 * half) {
-                const float xr = re[i + half] * wr - im[i + half] * wi;
-                const float xi = re[i + half] * wi + im[i + half] * wr;
-                re[i + half] = re[i] - xr;
-                im[i + half] = im[i] - xi;
-                re[i] += xr;
-                im[i] += xi;
-            }
-        }
-    }
-}
 
 template <int N>
 __device__ __forceinline__ void load_row(const float* __restrict__ p, float (&v)[N]) {

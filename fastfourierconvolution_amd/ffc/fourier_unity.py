@@ -47,9 +47,13 @@ class FourierUnitSN(nn.Module):
         H, W = th * up, tw * up
         self._check(C)
         L = rt.lib()
-        if L.ffc_fu_lds_bytes(C, H, W) == 0:
-            raise NotImplementedError(f"fused Fourier unit supports H,W in {{4,8,16,32}} with "
-                                      f"16*C*H*(W/2+1) <= 160 KiB; got C={C}, {H}x{W}")
+        fused = L.ffc_fu_lds_bytes(C, H, W) > 0 and not rt.FORCE_FU2D
+        if not fused:
+            if L.ffc_fu2d_supported(C, H, W, up):
+                return self._run2d(t, up, in_scale, in_shift, in_relu, residual)
+            raise NotImplementedError(f"Fourier unit supports H,W in {{4,8,16,32}} with 16*C*H*(W/2+1) <= 160 KiB "
+                                      f"(fused) or square H=W in {{32,64,128}} with 2C <= 128 (staged); "
+                                      f"got C={C}, {H}x{W}")
         dev = t.device
         stream = rt.stream_of(t)
         mixT = self._packed_mix(dev, stream)
@@ -67,6 +71,41 @@ class FourierUnitSN(nn.Module):
         with rt.observe("fu_pass1", bytes=8.0 * n_r):
             check(L.ffc_fu_forward(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
                                  1, None, ptr(sc), ptr(sh), int(residual), ptr(out), stream), "ffc_fu_forward(pass 1)")
+        return out
+
+    def _run2d(self, t, up, in_scale, in_shift, in_relu, residual):
+        """large-plane FU: r2c -> mix (pass 0 stats, pass 1 BN/ReLU) -> c2r (include/ffc_amd.h ffc_fu2d_*)"""
+        B, C, h, w = t.shape
+        H, W = h * up, w * up
+        L = rt.lib()
+        dev = t.device
+        stream = rt.stream_of(t)
+        mixT = self._packed_mix(dev, stream)
+        use_batch, _ = rt.bn_mode(self.bn)
+        nT = B * C * h * (w // 2 + 1)           # complex bins of T
+        nY = B * C * H * (W // 2 + 1)           # complex bins of Y
+        mix_flops = 2.0 * (2 * C) ** 2 * (B * H * (W // 2 + 1))   # (2C x 2C) GEMM over every bin
+        T = torch.empty((B, C, h, w // 2 + 1, 2), device=dev, dtype=torch.float32)
+        with rt.observe("fu2d_r2c", bytes=4.0 * t.numel() + 8.0 * nT):
+            check(L.ffc_fu2d_r2c(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(T), stream),
+                  "ffc_fu2d_r2c")
+        if use_batch:
+            rows = L.ffc_fu2d_slab_rows(B, C, H, W)
+            slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
+            with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT):
+                check(L.ffc_fu2d_mix(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, None, stream),
+                      "ffc_fu2d_mix(pass 0)")
+            sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
+        else:
+            sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
+        Y = torch.empty((B, C, H, W // 2 + 1, 2), device=dev, dtype=torch.float32)
+        with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
+            check(L.ffc_fu2d_mix(ptr(T), B, C, H, W, up, ptr(mixT), 1, None, ptr(sc), ptr(sh), ptr(Y), stream),
+                  "ffc_fu2d_mix(pass 1)")
+        out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
+        with rt.observe("fu2d_c2r", bytes=8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)):
+            check(L.ffc_fu2d_c2r(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift), int(in_relu),
+                                 int(residual), ptr(out), stream), "ffc_fu2d_c2r")
         return out
 
     def forward(self, x, y=None):

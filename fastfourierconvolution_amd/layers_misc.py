@@ -1,8 +1,10 @@
 """Caller helpers of the FFC block: Resizer (layers/resizer.py:10-24), Print / debug_print
 (layers/print_layer.py:10-32), NoiseInjection (layers/noise_injection.py:20-32).
 
-They only move tuples around, print shapes or add learned noise (fgan128 train mode); they
-stay plain PyTorch with the reference's exact semantics.
+Resizer / Print only move tuples around or print shapes.  NoiseInjection's add (fgan128 train
+mode) runs in the HIP library (ffc_noise_inject); the noise itself is drawn with torch's device
+RNG as the reference draws it with normal_() (or passed explicitly, as in the reference's
+``forward(x, noise)``).
 """
 import torch
 import torch.nn as nn
@@ -56,7 +58,18 @@ class NoiseInjection(nn.Module):
         self.weight = nn.Parameter(torch.zeros(1, channels, 1, 1))
 
     def forward(self, x, noise=None):
+        from . import _runtime as rt
+        from ._lib import check, ptr
+        x = rt.require(x, "x")
+        batch, C, height, width = x.shape
         if noise is None:
-            batch, _, height, width = x.shape
             noise = x.new_empty(batch, 1, height, width).normal_()
-        return x + self.weight * noise
+        noise = rt.require(noise, "noise")
+        if tuple(noise.shape) != (batch, 1, height, width) or (height * width) % 4:
+            raise NotImplementedError("NoiseInjection: noise must be (B, 1, H, W) with H*W % 4 == 0")
+        w = rt.require(self.weight.detach(), "weight")
+        out = torch.empty_like(x)
+        with rt.observe("noise_inject", bytes=8.0 * x.numel() + 4.0 * noise.numel()):
+            check(rt.lib().ffc_noise_inject(ptr(x), ptr(w), ptr(noise), ptr(out), batch, C, height * width,
+                                            rt.stream_of(x)), "ffc_noise_inject")
+        return out

@@ -1,7 +1,8 @@
 """The reference's callers of the FFC block, restated over the drop-in layers.
 
-FFCModel (models/ffcmodel.py:12-110), FFCGenerator (models/ffc_generator.py:14-44) and
-FFCDiscriminator (models/ffc_discriminator.py:11-58).  The layer stacks are identical; the
+FFCModel (models/ffcmodel.py:12-110), FFCGenerator (models/ffc_generator.py:14-44),
+FFCDiscriminator (models/ffc_discriminator.py:11-58) and the fgan128 FGenerator
+(fgan128_complete.py:442-522, BASELINE config 4).  The layer stacks are identical; the
 only change is that the ``inplanes=`` keyword the reference callers pass (and its base class
 rejects, models/ffcmodel.py:17) is accepted and ignored.
 """
@@ -10,9 +11,12 @@ import os
 import torch
 import torch.nn as nn
 
+from . import _plan
+from . import _runtime as rt
+from ._lib import check, ptr
 from .config import Config
 from .ffc import FFC_BN_ACT
-from .layers_misc import Print, Resizer, debug_print
+from .layers_misc import NoiseInjection, Print, Resizer, debug_print
 
 
 class FFCModel(nn.Module):
@@ -110,3 +114,82 @@ class FFCDiscriminator(FFCModel):
         x = self.print_size(x)
         debug_print("End D --")
         return x
+
+
+class FGenerator(FFCModel):
+    """fgan128_complete.py:442-522: Linear(z, 16*1024) -> (1024, 4, 4) -> five x2 FFC_BN_ACT
+    (FFCTranspose, BatchNorm2d + GELU, train-mode NoiseInjection on both branches) -> 3x3 FFC_BN_ACT
+    head (Tanh) -> Resizer; eval mode returns the uint8 image of :516-521.
+
+    ``forward(z, noises=None)``: ``noises`` optionally supplies the train-mode noise as
+    [(lcl, glb)] * 5 ((B, 1, H, W) each) instead of drawing it (the reference draws it inside
+    NoiseInjection with normal_()); the reference's forward(z) is the noises=None call."""
+
+    def __init__(self, z_size, mg: int = 4):
+        super().__init__()
+        self.z_size = z_size
+        self.ngf = 128
+        ratio_g = 0.5
+        self.mg = mg
+        ngf = self.ngf
+        self.noise_to_feature = nn.Sequential(nn.Linear(z_size, (self.mg * self.mg) * self.ngf * 8))
+        T = dict(activation_layer=nn.GELU, norm_layer=nn.BatchNorm2d, upsampling=True, uses_noise=True,
+                 uses_sn=True)
+        self.conv2 = FFC_BN_ACT(ngf * 8, ngf * 4, 4, 0.0, ratio_g, stride=2, padding=1, **T)
+        self.lcl_noise2 = NoiseInjection(int(ngf * 4 * (1 - ratio_g)))
+        self.glb_noise2 = NoiseInjection(int(ngf * 4 * ratio_g))
+        self.conv3 = FFC_BN_ACT(ngf * 4, ngf * 2, 4, ratio_g, ratio_g, stride=2, padding=1, **T)
+        self.lcl_noise3 = NoiseInjection(int(ngf * 2 * (1 - ratio_g)))
+        self.glb_noise3 = NoiseInjection(int(ngf * 2 * ratio_g))
+        self.conv4 = FFC_BN_ACT(ngf * 2, ngf, 4, ratio_g, ratio_g, stride=2, padding=1, **T)
+        self.lcl_noise4 = NoiseInjection(int(ngf * (1 - ratio_g)))
+        self.glb_noise4 = NoiseInjection(int(ngf * ratio_g))
+        self.conv5 = FFC_BN_ACT(ngf, ngf, 4, ratio_g, ratio_g, stride=2, padding=1, **T)
+        self.lcl_noise5 = NoiseInjection(int(ngf * (1 - ratio_g)))
+        self.glb_noise5 = NoiseInjection(int(ngf * ratio_g))
+        self.conv6 = FFC_BN_ACT(ngf, ngf, 4, ratio_g, ratio_g, stride=2, padding=1, **T)
+        self.lcl_noise6 = NoiseInjection(int(ngf * (1 - ratio_g)))
+        self.glb_noise6 = NoiseInjection(int(ngf * ratio_g))
+        self.conv7 = FFC_BN_ACT(ngf, 3, 3, ratio_g, 0.0, stride=1, padding=1, activation_layer=nn.Tanh,
+                                norm_layer=nn.Identity, upsampling=False, uses_noise=True, uses_sn=True)
+        self._lin = {}
+
+    def _noise_to_feature(self, z):
+        """nn.Linear(z_size, 16*1024) on the HIP GEMM: a 1x1 'convolution' of (B, z, 1, 1)"""
+        lin = self.noise_to_feature[0]
+        z = rt.require(z, "z")
+        if z.dim() != 2 or z.shape[1] != lin.in_features:
+            raise RuntimeError(f"FGenerator: z must be (B, {lin.in_features}), got {tuple(z.shape)}")
+        B = z.shape[0]
+        w = rt.require(lin.weight.detach(), "noise_to_feature.0.weight")
+        b = rt.require(lin.bias.detach(), "noise_to_feature.0.bias") if lin.bias is not None else None
+        wt = (w, 0, 1, 1, b)
+        key = (B, str(z.device))
+        ex = self._lin.get(key)
+        if ex is None:
+            e = rt.ConvExec(B, lin.out_features, [_plan.Seg("pw", lin.in_features, 1, 1)], [wt], z.device)
+            ex = self._lin[key] = (e, rt.LaunchPlan([e], z.device))
+        e, lp = ex
+        e.ensure_packed([wt])
+        out = torch.empty((B, lin.out_features, 1, 1), device=z.device, dtype=torch.float32)
+        lp.launch([e.job([(z.view(B, -1, 1, 1), None)], out)], rt.stream_of(z), flops=e.flops)
+        return out.view(B, -1, self.mg, self.mg)
+
+    def forward_float(self, z, noises=None):
+        """FGenerator.forward up to the float image (:491-515): the eval-mode uint8 quantization of
+        :516-521 is left out"""
+        fake = self._noise_to_feature(z)                                     # :491-494
+        for i, n in enumerate((2, 3, 4, 5, 6)):                              # :496-515
+            fake = getattr(self, f"conv{n}")(fake)
+            if self.training:
+                nl, ng = noises[i] if noises is not None else (None, None)
+                fake = (getattr(self, f"lcl_noise{n}")(fake[0], nl), getattr(self, f"glb_noise{n}")(fake[1], ng))
+        return self.resizer(self.conv7(fake))
+
+    def forward(self, z, noises=None):
+        fake = self.forward_float(z, noises)
+        if self.training:
+            return fake
+        out = torch.empty(fake.shape, device=fake.device, dtype=torch.uint8)   # :516-521
+        check(rt.lib().ffc_quantize_u8(ptr(fake), ptr(out), fake.numel(), rt.stream_of(fake)), "ffc_quantize_u8")
+        return out

@@ -218,6 +218,37 @@ int ffc_fu_pack_mix(const float* w, int C2, float* wmixT, void* stream);
 /* LDS bytes the fused FU kernel needs (0 if unsupported) */
 size_t ffc_fu_lds_bytes(int C, int H, int W);
 
+/* Large-plane Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56, for planes whose
+ * per-sample spectrum does not fit one workgroup's LDS: the fgan128 generator's 64x64 and
+ * 128x128 FUs, fgan128_complete.py:474-485).  Square H = W, a power of two in [32, 128],
+ * 2C <= 128, up in {1, 2}; (h, w) = (H/up, W/up) is the grid of t.  Three stages over HBM:
+ *   ffc_fu2d_r2c: T = rfft2(s0) unnormalised, s0 = in_relu ? relu(t*in_scale + in_shift) : t;
+ *                 T (B, C, h, w/2+1) complex64 (interleaved float2)
+ *   ffc_fu2d_mix: X = rfftn(s, ortho) of s = s0 nearest-upsampled by `up`, rebuilt from T;
+ *                 Y = Wmix Z (Z: X's interleaved Re/Im channels, :40-45);
+ *                 pass 0: BN partial slab [ffc_fu2d_slab_rows()][2C] float4 {n, mean, M2}
+ *                 pass 1: Y = relu(Y*bn_scale + bn_shift) -> (B, C, H, W/2+1) complex64
+ *   ffc_fu2d_c2r: out = irfftn(Y, s=(H, W), ortho) (+ s when residual) -> (B, C, H, W)
+ * wmixT as for ffc_fu_forward. */
+int ffc_fu2d_supported(int C, int H, int W, int up);
+int ffc_fu2d_slab_rows(int B, int C, int H, int W);
+int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const float* in_scale,
+                 const float* in_shift, int in_relu, float* T, void* stream);
+int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, const float* wmixT, int pass,
+                 float* stats_slab, const float* bn_scale, const float* bn_shift, float* Y, void* stream);
+int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                 const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
+                 void* stream);
+
+/* ------------------------------------------------------------------ fgan128 caller ops
+ * NoiseInjection.forward(x, noise) (layers/noise_injection.py:25-32): out = x + weight[c]*noise[b]
+ * x, out (B, C, H, W); weight (C); noise (B, 1, H, W); HW % 4 == 0; in place allowed. */
+int ffc_noise_inject(const float* x, const float* weight, const float* noise, float* out, int B, int C,
+                     int HW, void* stream);
+/* eval-mode output of fgan128 FGenerator (fgan128_complete.py:516-521): out = uint8(255*(x*0.5+0.5))
+ * (the reference's clamp to the tensor's own min/max is the identity); n % 4 == 0 */
+int ffc_quantize_u8(const float* x, unsigned char* out, long long n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

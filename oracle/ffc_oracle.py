@@ -16,6 +16,8 @@ BASELINE.json:north_star (file:line citations into /root/reference):
 * Resizer           layers/resizer.py:15-24
 * FFCGenerator      models/ffc_generator.py:21-44
 * FFCDiscriminator  models/ffc_discriminator.py:18-58
+* NoiseInjection    layers/noise_injection.py:20-32
+* fgan128 FGenerator fgan128_complete.py:442-522 (reconstructed: the script runs main() at import)
 
 The arithmetic itself lives in the un-vendored third-party dependency PyTorch
 (pinned torch==1.10.2 at requirements.txt:5).  Its published semantics are
@@ -244,6 +246,44 @@ def ffc_discriminator(x, sd, nc, ndf, training, fft="numpy"):
     return resizer(x)
 
 
+def fgan128_layers(ngf=128, g=0.5):
+    """fgan128_complete.py:457-485: conv2..conv7 FFC_BN_ACT configs."""
+    T = lambda i, o, ri, ro: dict(in_channels=i, out_channels=o, kernel_size=4, ratio_gin=ri,  # noqa: E731
+                                  ratio_gout=ro, stride=2, padding=1, activation_layer="GELU",
+                                  norm_layer="BatchNorm2d", upsampling=True)
+    return [("conv2", T(ngf * 8, ngf * 4, 0.0, g)), ("conv3", T(ngf * 4, ngf * 2, g, g)),
+            ("conv4", T(ngf * 2, ngf, g, g)), ("conv5", T(ngf, ngf, g, g)), ("conv6", T(ngf, ngf, g, g)),
+            ("conv7", dict(in_channels=ngf, out_channels=3, kernel_size=3, ratio_gin=g, ratio_gout=0.0, stride=1,
+                           padding=1, activation_layer="Tanh", norm_layer="Identity", upsampling=False))]
+
+
+def noise_injection(x, sd, prefix, noise):
+    """NoiseInjection.forward(x, noise) (layers/noise_injection.py:25-32): x + weight * noise,
+    noise (B, 1, H, W) broadcast over channels."""
+    return x + _w(sd, prefix + "weight", x.dtype) * noise
+
+
+def fgan128_generator(z, sd, training, noises=None, mg=4, ngf=128, fft="numpy"):
+    """FGenerator.forward (fgan128_complete.py:489-522) up to (not including) the eval-mode uint8
+    quantization.  ``noises``: train-mode NoiseInjection noise, a list of (lcl, glb) pairs for
+    conv2..conv6 (the reference draws them with normal_(); parity passes them explicitly)."""
+    x = F.linear(z, _w(sd, "noise_to_feature.0.weight", z.dtype), _w(sd, "noise_to_feature.0.bias", z.dtype))
+    x = x.reshape(x.size(0), -1, mg, mg)                                        # :494
+    for i, (name, cfg) in enumerate(fgan128_layers(ngf)):
+        x = ffc_bn_act(x, sd, name + ".", cfg, training, fft)
+        if training and name != "conv7":                                        # :498-515
+            n = int(name[-1])
+            nl, ng = noises[i]
+            x = (noise_injection(x[0], sd, f"lcl_noise{n}.", nl), noise_injection(x[1], sd, f"glb_noise{n}.", ng))
+    return resizer(x)
+
+
+def quantize_u8(fake):
+    """eval-mode output (fgan128_complete.py:516-521): 255 * (clamp(x, min x, max x) * 0.5 + 0.5) -> uint8.
+    The clamp to the tensor's own range is the identity."""
+    return (255 * (fake * 0.5 + 0.5)).to(torch.uint8)
+
+
 # ----------------------------------------------------------------------------- fixture driver
 def run_fixture_case(case: dict, state: dict, inputs: dict, dtype=torch.float64, fft="numpy"):
     """Run one golden-manifest case (tests/golden/manifest.json) through the oracle.
@@ -272,6 +312,9 @@ def run_fixture_case(case: dict, state: dict, inputs: dict, dtype=torch.float64,
             out = {"out": ffc_generator(tin["z"], sd, ctor["nz"], ctor["nc"], ctor["ngf"], training, fft)}
         elif kind == "FFCDiscriminator":
             out = {"out": ffc_discriminator(tin["x"], sd, ctor["nc"], ctor["ndf"], training, fft)}
+        elif kind == "FGenerator":
+            noises = [(tin.get(f"noise{n}_l"), tin.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
+            out = {"out": fgan128_generator(tin["z"], sd, training, noises, fft=fft)}
         else:
             raise ValueError(kind)
     return out, sd

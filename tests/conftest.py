@@ -69,6 +69,9 @@ def call_dropin(case, mod, inputs):
     import torch
     t = {k: torch.from_numpy(v).cuda() for k, v in inputs.items()}
     with torch.no_grad():
+        if case["kind"] == "FGenerator":
+            noises = [(t.get(f"noise{n}_l"), t.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
+            return {"out": mod.forward_float(t["z"], noises if mod.training else None)}
         if case["kind"] == "FFC_BN_ACT":
             x = (t["x_l"], t["x_g"]) if "x_l" in t else t["x"]
             ol, og = mod(x)

@@ -74,7 +74,53 @@ def load_reference():
     return types.SimpleNamespace(
         FourierUnitSN=fu.FourierUnitSN, SpectralTransform=st.SpectralTransform,
         FFC_BN_ACT=fba.FFC_BN_ACT, FFCGenerator=fg.FFCGenerator,
-        FFCDiscriminator=fd.FFCDiscriminator, Resizer=rs.Resizer)
+        FFCDiscriminator=fd.FFCDiscriminator, Resizer=rs.Resizer, NoiseInjection=ni.NoiseInjection,
+        FFCModel=fm.FFCModel)
+
+
+def fgenerator_class(ref):
+    """fgan128_complete.py:442-522 FGenerator, rebuilt from the reference's own layers (the script
+    runs main() at import and needs torchvision/tensorboard/torch_fidelity).  Same
+    module names and state_dict keys; forward takes the train-mode NoiseInjection noise explicitly
+    (the reference draws it with normal_(), layers/noise_injection.py:26-28) and returns the float
+    output (the eval-mode uint8 quantization of :516-521 is checked separately)."""
+    class FGenerator(ref.FFCModel):
+        def __init__(self, z_size=128, mg=4):
+            super().__init__()
+            self.z_size, self.ngf, self.mg = z_size, 128, mg
+            ngf, g = self.ngf, 0.5
+            self.noise_to_feature = nn.Sequential(nn.Linear(z_size, (mg * mg) * ngf * 8))
+            T = dict(activation_layer=nn.GELU, norm_layer=nn.BatchNorm2d, upsampling=True, uses_noise=True,
+                     uses_sn=True)
+            self.conv2 = ref.FFC_BN_ACT(ngf * 8, ngf * 4, 4, 0.0, g, stride=2, padding=1, **T)
+            self.lcl_noise2 = ref.NoiseInjection(int(ngf * 4 * (1 - g)))
+            self.glb_noise2 = ref.NoiseInjection(int(ngf * 4 * g))
+            self.conv3 = ref.FFC_BN_ACT(ngf * 4, ngf * 2, 4, g, g, stride=2, padding=1, **T)
+            self.lcl_noise3 = ref.NoiseInjection(int(ngf * 2 * (1 - g)))
+            self.glb_noise3 = ref.NoiseInjection(int(ngf * 2 * g))
+            self.conv4 = ref.FFC_BN_ACT(ngf * 2, ngf, 4, g, g, stride=2, padding=1, **T)
+            self.lcl_noise4 = ref.NoiseInjection(int(ngf * (1 - g)))
+            self.glb_noise4 = ref.NoiseInjection(int(ngf * g))
+            self.conv5 = ref.FFC_BN_ACT(ngf, ngf, 4, g, g, stride=2, padding=1, **T)
+            self.lcl_noise5 = ref.NoiseInjection(int(ngf * (1 - g)))
+            self.glb_noise5 = ref.NoiseInjection(int(ngf * g))
+            self.conv6 = ref.FFC_BN_ACT(ngf, ngf, 4, g, g, stride=2, padding=1, **T)
+            self.lcl_noise6 = ref.NoiseInjection(int(ngf * (1 - g)))
+            self.glb_noise6 = ref.NoiseInjection(int(ngf * g))
+            self.conv7 = ref.FFC_BN_ACT(ngf, 3, 3, g, 0.0, stride=1, padding=1, activation_layer=nn.Tanh,
+                                        norm_layer=nn.Identity, upsampling=False, uses_noise=True, uses_sn=True)
+
+        def forward(self, z, noises=None):
+            fake = self.noise_to_feature(z)
+            fake = fake.reshape(fake.size(0), -1, self.mg, self.mg)
+            for i, n in enumerate((2, 3, 4, 5, 6)):
+                fake = getattr(self, f"conv{n}")(fake)
+                if self.training:
+                    fake = (getattr(self, f"lcl_noise{n}")(fake[0], noises[i][0]),
+                            getattr(self, f"glb_noise{n}")(fake[1], noises[i][1]))
+            fake = self.conv7(fake)
+            return self.resizer(fake)
+    return FGenerator
 
 
 def weight_specs(module: nn.Module) -> dict:
@@ -98,6 +144,8 @@ def weight_specs(module: nn.Module) -> dict:
             specs[pre + "weight"] = [list(m.weight.shape), "normal", 0.0, fan ** -0.5, "float32"]
             if m.bias is not None:
                 specs[pre + "bias"] = [list(m.bias.shape), "normal", 0.0, 0.1, "float32"]
+        elif type(m).__name__ == "NoiseInjection":
+            specs[pre + "weight"] = [list(m.weight.shape), "normal", 0.0, 0.2, "float32"]
         elif isinstance(m, nn.BatchNorm2d):
             c = m.num_features
             specs[pre + "weight"] = [[c], "normal", 1.0, 0.1, "float32"]
@@ -205,15 +253,26 @@ def build_cases():
     case("gen_nc3", "FFCGenerator", dict(nz=100, nc=3, ngf=64), {"z": [4, 100, 1, 1]})
     case("gen_nc3_eval", "FFCGenerator", dict(nz=100, nc=3, ngf=64), {"z": [4, 100, 1, 1]}, mode="eval")
     case("disc_nc3", "FFCDiscriminator", dict(nc=3, ndf=64), {"x": [2, 3, 64, 64]})
+    noise = {f"noise{n}_{br}": [2, 1, 2 ** (n + 1), 2 ** (n + 1)] for n in (2, 3, 4, 5, 6) for br in "lg"}
+    case("fgan128_train", "FGenerator", dict(z_size=128), {"z": [2, 128], **noise},
+         note="BASELINE config 4 stack (fgan128_complete.py:442-522), train mode, explicit noise")
+    case("fgan128_eval", "FGenerator", dict(z_size=128), {"z": [2, 128]}, mode="eval",
+         note="BASELINE config 4 stack, eval mode (float output before the uint8 quantization)")
 
 
 def construct(ref, c):
+    if c["kind"] == "FGenerator":
+        return fgenerator_class(ref)(**c["ctor"])
     kw = dict(c["ctor"])
     for k in ("norm_layer", "activation_layer"):
         if k in kw:
             kw[k] = getattr(nn, kw[k])
     with contextlib.redirect_stdout(io.StringIO()):  # FFC prints at construction (layers/ffc/ffc.py:38-39)
         return getattr(ref, c["kind"])(**kw)
+
+
+def shp_b(c):
+    return next(iter(c["inputs"].values()))[0]
 
 
 def run_case(ref, c):
@@ -226,6 +285,9 @@ def run_case(ref, c):
     tin = {k: torch.from_numpy(v) for k, v in inputs.items()}
 
     def call(t):
+        if c["kind"] == "FGenerator":
+            noises = [(t.get(f"noise{n}_l"), t.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
+            return mod(t["z"], noises)
         if c["kind"] == "FFC_BN_ACT" and "x_l" in t:
             return mod((t["x_l"], t["x_g"]))
         return mod(next(iter(t.values())))
@@ -234,6 +296,10 @@ def run_case(ref, c):
     if c["mode"] == "eval":
         # give the running stats realistic scales: stats of a different warm-up batch
         warm = {k: torch.from_numpy(input_array(seed + 7, k, shp)) for k, shp in c["inputs"].items()}
+        if c["kind"] == "FGenerator":   # the warm-up pass is a train-mode pass: it needs noise
+            warm.update({f"noise{n}_{br}": torch.from_numpy(input_array(seed + 7, f"noise{n}_{br}",
+                                                                        [shp_b(c), 1, 2 ** (n + 1), 2 ** (n + 1)]))
+                         for n in (2, 3, 4, 5, 6) for br in "lg"})
         set_momentum(mod, 1.0)
         mod.train()
         with torch.no_grad():
@@ -259,7 +325,14 @@ def main():
     manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
                 "numpy": np.__version__, "cases": []}
     total = 0
+    only = set(sys.argv[1:])     # regenerate only these cases (the manifest keeps the others)
+    old = {}
+    if only and os.path.exists(os.path.join(HERE, "manifest.json")):
+        old = {e["name"]: e for e in json.load(open(os.path.join(HERE, "manifest.json")))["cases"]}
     for c in CASES:
+        if only and c["name"] not in only and c["name"] in old:
+            manifest["cases"].append(old[c["name"]])
+            continue
         specs, arrays = run_case(ref, c)
         path = os.path.join(HERE, c["name"] + ".npz")
         np.savez_compressed(path, **arrays)

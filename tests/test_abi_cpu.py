@@ -46,7 +46,10 @@ def test_argument_validation_without_gpu():
     lib = _lib.load()
     # Z/Y planes (Re, Im) + the mix weight (2C x ceil32(2C), whole 256-float DMA groups)
     assert lib.ffc_fu_lds_bytes(16, 32, 32) == 16 * 16 * 32 * 17 + 4 * 32 * 32 + 4 * 4 * 16   # + BN scale/shift
-    assert lib.ffc_fu_lds_bytes(16, 64, 64) == 0          # large planes: next round
+    assert lib.ffc_fu_lds_bytes(16, 64, 64) == 0          # large planes: the staged FU (ffc_fu2d_*)
+    assert lib.ffc_fu2d_supported(16, 64, 64, 2) == 1 and lib.ffc_fu2d_supported(32, 128, 128, 1) == 1
+    assert lib.ffc_fu2d_supported(65, 64, 64, 1) == 0     # 2C > 128
+    assert lib.ffc_fu2d_supported(8, 64, 32, 1) == 0      # not square
     assert lib.ffc_fu_lds_bytes(16, 12, 12) == 0          # not a power of two
     rc = lib.ffc_fu_forward(None, 1, 4, 12, 12, 1, None, None, 0, None, 0, None, None, None, 0, None, None)
     assert rc == -1

@@ -137,7 +137,9 @@ def test_unsupported_plane_raises():
     import fastfourierconvolution_amd as F
     fu = F.FourierUnitSN(4, 4).cuda()
     with pytest.raises(NotImplementedError):
-        fu(torch.randn(1, 4, 64, 64, device="cuda"))
+        fu(torch.randn(1, 4, 48, 48, device="cuda"))     # not a power of two
+    with pytest.raises(NotImplementedError):
+        fu(torch.randn(1, 4, 64, 128, device="cuda"))    # staged FU: square planes only
 
 
 def test_conditional_path_raises_like_reference():
