@@ -80,6 +80,8 @@ SIGNATURES = [
                                        c_void_p, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     ("ffc_bn_act_apply", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float,
                                  c_void_p]),
+    ("ffc_bn_act_noise_apply", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float,
+                                       c_void_p, c_void_p, c_void_p]),
     ("ffc_se_gate", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                             c_void_p]),
     ("ffc_fu_forward", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
@@ -99,6 +101,8 @@ SIGNATURES = [
                              c_int, c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),
+    ("ffc_conv3x3_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
+                                   c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
     ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                       c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
 ]

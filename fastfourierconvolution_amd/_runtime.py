@@ -176,6 +176,24 @@ def bn_act_apply(x, scale, shift, act, param, out=None):
     return out
 
 
+def bn_act_noise_apply(x, scale, shift, act, param, noise_mod, noise=None):
+    """x <- act(x*scale + shift) + noise_mod.weight[c] * noise[b] in one pass (noise drawn with normal_()
+    as layers/noise_injection.py:26-28 does when not given)"""
+    B, C, H, W = x.shape
+    if noise is None:
+        noise = x.new_empty(B, 1, H, W).normal_()
+    noise = require(noise, "noise")
+    if tuple(noise.shape) != (B, 1, H, W):
+        raise RuntimeError(f"noise must be {(B, 1, H, W)}, got {tuple(noise.shape)}")
+    w = require(noise_mod.weight.detach(), "NoiseInjection.weight")
+    if w.numel() != C:
+        raise RuntimeError(f"NoiseInjection has {w.numel()} channels, tensor has {C}")
+    with observe("bn_act_noise", bytes=8.0 * x.numel() + 4.0 * noise.numel()):
+        check(lib().ffc_bn_act_noise_apply(ptr(x), ptr(x), B, C, H * W, ptr(scale), ptr(shift), act, float(param),
+                                           ptr(w), ptr(noise), stream_of(x)), "ffc_bn_act_noise_apply")
+    return x
+
+
 # --------------------------------------------------------------------------- convolution jobs
 def _wkey(ts):
     return tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)

@@ -170,6 +170,86 @@ __global__ void se_gate_kernel(const float* __restrict__ x, int C, int H, int W,
     }
 }
 
+// BN scale/shift + activation (+ NoiseInjection) over whole planes: every block covers one chunk
+// of one (b, c) plane, so the channel is computed once per block (no per-element division).
+// out = act(x*scale[c] + shift[c]) [+ noise_w[c] * noise[b, hw]]   (layers/noise_injection.py:25-32)
+constexpr int PLANE_CHUNK4 = 1024;   // float4 per block: 256 threads x 4
+__global__ __launch_bounds__(256) void bn_act_plane_kernel(const float4* __restrict__ x, float4* __restrict__ y,
+                                                           int C, int HW4, int chunks,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int act, float p,
+                                                           const float* __restrict__ noise_w,
+                                                           const float4* __restrict__ noise) {
+    const int plane = blockIdx.x / chunks;
+    const int chunk = blockIdx.x - plane * chunks;
+    const int c = plane % C, b = plane / C;
+    const float sc = scale[c], sh = shift[c];
+    const float nw = noise_w ? noise_w[c] : 0.0f;
+    const size_t base = (size_t)plane * HW4;
+    const float4* nz = noise ? noise + (size_t)b * HW4 : nullptr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = chunk * PLANE_CHUNK4 + u * 256 + threadIdx.x;
+        if (i < HW4) {
+            const float4 v = x[base + i];
+            float4 r = make_float4(ffc::apply_act(fmaf(v.x, sc, sh), act, p), ffc::apply_act(fmaf(v.y, sc, sh), act, p),
+                                   ffc::apply_act(fmaf(v.z, sc, sh), act, p), ffc::apply_act(fmaf(v.w, sc, sh), act, p));
+            if (nz) {
+                const float4 n = nz[i];
+                r.x = fmaf(nw, n.x, r.x);
+                r.y = fmaf(nw, n.y, r.y);
+                r.z = fmaf(nw, n.z, r.z);
+                r.w = fmaf(nw, n.w, r.w);
+            }
+            y[base + i] = r;
+        }
+    }
+}
+
+// SE gate for large planes, stage 1: one wave per (b, c) plane, float4 loads -> plane mean
+// (the per-sample kernel above leaves most CUs idle when B is small and the planes large)
+__global__ void se_mean_kernel(const float4* __restrict__ x, int planes, int HW4, float inv, float* __restrict__ mean) {
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (p >= planes) return;
+    const float4* src = x + (size_t)p * HW4;
+    float s0 = 0.0f, s1 = 0.0f;
+    int i = lane;
+    for (; i + 64 < HW4; i += 128) {
+        const float4 a = src[i], b = src[i + 64];
+        s0 += (a.x + a.y) + (a.z + a.w);
+        s1 += (b.x + b.y) + (b.z + b.w);
+    }
+    if (i < HW4) {
+        const float4 a = src[i];
+        s0 += (a.x + a.y) + (a.z + a.w);
+    }
+    const float s = ffc::wave_sum(s0 + s1);
+    if (lane == 0) mean[p] = s * inv;
+}
+
+// stage 2: per sample, gate = sigmoid(W2 relu(W1 mean))
+__global__ void se_fc_kernel(const float* means, int C, const float* __restrict__ w1,
+                             const float* __restrict__ w2, int hid, float* gate) {
+    extern __shared__ float sm[];
+    float* mean = sm;
+    float* hv = sm + C;
+    const int b = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) mean[c] = means[(size_t)b * C + c];
+    __syncthreads();
+    for (int j = threadIdx.x; j < hid; j += blockDim.x) {
+        float s = 0.0f;
+        for (int c = 0; c < C; ++c) s = fmaf(w1[(size_t)j * C + c], mean[c], s);
+        hv[j] = fmaxf(s, 0.0f);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (int j = 0; j < hid; ++j) s = fmaf(w2[(size_t)c * hid + j], hv[j], s);
+        gate[(size_t)b * C + c] = 1.0f / (1.0f + expf(-s));
+    }
+}
+
 }  // namespace
 
 extern "C" int ffc_bn_reduce(const float* slab, int nrows, int C, double* moments, void* stream) {
@@ -239,7 +319,12 @@ extern "C" int ffc_bn_act_apply(const float* x, float* y, int B, int C, int HW, 
     FFC_CHECK_ARG(x && y && scale && shift && B > 0 && C > 0 && HW > 0, "ffc_bn_act_apply: bad args");
     const long long total = (long long)B * C * HW;
     const bool vec = (total % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 == 0);
-    if (vec) {
+    if (vec && HW % 4 == 0 && HW >= 256) {
+        const int HW4 = HW / 4, chunks = (HW4 + PLANE_CHUNK4 - 1) / PLANE_CHUNK4;
+        hipLaunchKernelGGL(bn_act_plane_kernel, dim3((unsigned)(B * C * chunks)), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), C, HW4, chunks, scale,
+                           shift, act, act_param, nullptr, nullptr);
+    } else if (vec) {
         const long long t4 = total / 4;
         const int grid = (int)std::min<long long>((t4 + 255) / 256, 2048);
         hipLaunchKernelGGL(bn_act_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, y, C, HW, t4, scale,
@@ -257,7 +342,33 @@ extern "C" int ffc_se_gate(const float* x, int B, int C, int H, int W, int pool,
     FFC_CHECK_ARG(x && gate && B > 0 && C > 0 && H > 0 && W > 0 && hidden >= 0, "ffc_se_gate: bad args");
     FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_se_gate: null weights");
     const size_t lds = sizeof(float) * (C + hidden);
-    hipLaunchKernelGGL(se_gate_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, x, C, H, W, pool, w1, w2,
-                       hidden, gate);
+    const bool wide = (W % 4 == 0) && (!pool || (H % 2 == 0 && W % 2 == 0)) && H * W >= 1024 &&
+                      (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (wide) {
+        // plane means into the gate buffer, then the FCs in place (each sample's block reads its
+        // C means into LDS before any gate is written)
+        const int planes = B * C;
+        hipLaunchKernelGGL(se_mean_kernel, dim3((planes + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<const float4*>(x), planes, H * W / 4, 1.0f / (float)(H * W), gate);
+        hipLaunchKernelGGL(se_fc_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, gate, C, w1, w2, hidden, gate);
+    } else {
+        hipLaunchKernelGGL(se_gate_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, x, C, H, W, pool, w1, w2,
+                           hidden, gate);
+    }
     return ffc::launch_status("ffc_se_gate");
+}
+
+extern "C" int ffc_bn_act_noise_apply(const float* x, float* y, int B, int C, int HW, const float* scale,
+                                      const float* shift, int act, float act_param, const float* noise_w,
+                                      const float* noise, void* stream) {
+    FFC_CHECK_ARG(x && y && scale && shift && noise_w && noise && B > 0 && C > 0 && HW > 0,
+                  "ffc_bn_act_noise_apply: bad args");
+    FFC_CHECK_ARG(HW % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+                                   reinterpret_cast<uintptr_t>(noise)) & 15) == 0,
+                  "ffc_bn_act_noise_apply: H*W % 4 == 0 and 16-byte aligned tensors required");
+    const int HW4 = HW / 4, chunks = (HW4 + PLANE_CHUNK4 - 1) / PLANE_CHUNK4;
+    hipLaunchKernelGGL(bn_act_plane_kernel, dim3((unsigned)(B * C * chunks)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), C, HW4, chunks, scale, shift,
+                       act, act_param, noise_w, reinterpret_cast<const float4*>(noise));
+    return ffc::launch_status("ffc_bn_act_noise_apply");
 }

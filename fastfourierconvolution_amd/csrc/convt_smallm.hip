@@ -1,4 +1,11 @@
-// Direct (VALU) ConvTranspose2d k4 s2 p1 for very few output channels (M <= 4) on gfx950.
+// Direct (VALU) ConvTranspose2d k4 s2 p1 and Conv2d k3 s1 p1 for very few output channels
+// (M <= 4) on gfx950.
+//
+// Conv2d k3 s1 p1 (conv3x3_smallm_kernel): the fgan128 generator's head conv7
+// (FFC_BN_ACT(128, 3, 3, 0.5, 0, 1, 1, Tanh), fgan128_complete.py:484; local branch ffc.py:89-97)
+// maps 2 x 64 channels to 3 at 128x128.  Same tiling and staging as the ConvT kernel below: a
+// thread owns a 2x2 output block and reads its 4x4 input neighbourhood once per channel (16
+// patch reads feed 36M FMAs); the chunk weights are staged as [channel][m][12] (9 taps, padded).
 //
 // The FFC-DCGAN generator's last layer (FFC_BN_ACT(ngf, nc, 4, 0.5, 0, 2, 1, Tanh),
 // models/ffc_generator.py:28; local branch ffc_transpose.py:96-100) maps 2 x 32 channels
@@ -198,6 +205,151 @@ __global__ __launch_bounds__(SM_THREADS) void convt_smallm_kernel(SmallMArgs a) 
     }
 }
 
+
+constexpr int WE3 = CCH * 4 * 12;   // conv3 chunk weights [cc][m][12] (M <= 4)
+static_assert(WE3 <= WE, "conv3 weights fit the ConvT weight slot");
+
+template <int MM>
+__global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int half = threadIdx.x >> 8, tid = threadIdx.x & 255, wave = tid >> 6;
+    int bid = blockIdx.x;
+    const int tx = bid % a.ntx;
+    bid /= a.ntx;
+    const int ty = bid % a.nty;
+    const int b = bid / a.nty;
+    const int y0 = ty * TT, x0 = tx * TT;
+    const int qy = 2 * (tid >> 4), qx = 2 * (tid & 15);   // top-left of this thread's 2x2 outputs
+    const int M = a.M;
+
+    const int nch0 = (a.C[0] + CCH - 1) / CCH;
+    const int nchunks = nch0 + (a.nseg > 1 ? (a.C[1] + CCH - 1) / CCH : 0);
+
+    auto stage = [&](int ci, float* dst) {
+        const int s = ci < nch0 ? 0 : 1;
+        const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
+        const float* x = a.x[s];
+        const float* w = a.w[s];   // Conv2d weights (M, C, 3, 3)
+        const int C = a.C[s];
+        for (int e = 0; e * 256 < PE + WE3; ++e) {
+            const int n = e * 256 + tid;
+            const float* src = g_zero_sm;
+            if (n < PE) {
+                const int pc = n % PP, r = n / PP;
+                const int pr = r % PP, ch = r / PP;
+                const int iy = y0 - 1 + pr, ix = x0 - 1 + pc, c = c0 + ch;
+                if (c < C && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+                    src = x + (((size_t)b * C + c) * a.IH + iy) * a.IW + ix;
+            } else if (n - PE < WE3) {
+                const int q = n - PE;
+                const int t = q % 12, m = (q / 12) & 3, cc = q / 48;
+                if (t < 9 && m < M && c0 + cc < C) src = w + ((size_t)m * C + c0 + cc) * 9 + t;
+            }
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
+        }
+    };
+
+    float acc[MM][2][2];
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[m][i][j] = 0.0f;
+
+    const int nsteps = (nchunks + 1) / 2;   // half h takes chunks 2k + h
+    if (half < nchunks) stage(half, lds + half * EBUF);
+    for (int k = 0; k < nsteps; ++k) {
+        __syncthreads();
+        const int ci = 2 * k + half;
+        if (ci + 2 < nchunks) stage(ci + 2, lds + (((k + 1) & 1) * 2 + half) * EBUF);
+        if (ci >= nchunks) continue;
+        const float* cur = lds + ((k & 1) * 2 + half) * EBUF;
+        const int s = ci < nch0 ? 0 : 1;
+        const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
+        const int cn = min(CCH, a.C[s] - c0);
+        for (int cc = 0; cc < cn; ++cc) {
+            float v[4][4];   // input rows qy-1..qy+2, cols qx-1..qx+2
+            const float* p = cur + (cc * PP + qy) * PP + qx;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[i][j] = p[i * PP + j];
+            const float* wl = cur + PE + cc * 48;
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+                if (m < M) {
+                    float k9[12];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const float4 t = reinterpret_cast<const float4*>(wl + m * 12)[q];
+                        k9[4 * q] = t.x; k9[4 * q + 1] = t.y; k9[4 * q + 2] = t.z; k9[4 * q + 3] = t.w;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j) {
+                            float s2 = acc[m][i][j];
+#pragma unroll
+                            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                                for (int kx = 0; kx < 3; ++kx) s2 = fmaf(v[i + ky][j + kx], k9[ky * 3 + kx], s2);
+                            acc[m][i][j] = s2;
+                        }
+                }
+            }
+        }
+    }
+    // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
+    __syncthreads();
+    float* part = lds;
+    if (half == 1) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) part[((m * 2 + i) * 2 + j) * 256 + tid] = acc[m][i][j];
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[m][i][j] += part[((m * 2 + i) * 2 + j) * 256 + tid];
+    const int oy0 = y0 + qy, ox0 = x0 + qx;
+    const bool xin = ox0 + 1 < a.IW;
+    auto store = [&](auto actf) {
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            if (m >= M) break;
+            const float bv = a.bias ? a.bias[m] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int oy = oy0 + i;
+                if (oy >= a.IH) continue;
+                float* row = a.out + (((size_t)b * M + m) * a.IH + oy) * a.IW + ox0;
+                if (xin) {
+                    *reinterpret_cast<float2*>(row) = make_float2(actf(acc[m][i][0] + bv), actf(acc[m][i][1] + bv));
+                } else if (ox0 < a.IW) {
+                    row[0] = actf(acc[m][i][0] + bv);
+                }
+            }
+        }
+    };
+    const float ap = a.act_param;
+    switch (a.act) {
+        case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
+        case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
+        case FFC_ACT_TANH: store([](float v) { return tanhf(v); }); break;
+        case FFC_ACT_SIGMOID: store([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
+        case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
+        default: store([](float v) { return v; }); break;
+    }
+}
+
 }  // namespace
 
 extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
@@ -239,4 +391,45 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, c
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_convt_k4s2_smallm");
+}
+
+extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                                  const float* w1, const float* bias, int B, int H, int W, int M, float* out,
+                                  int act, float act_param, void* stream) {
+    FFC_CHECK_ARG(x0 && w0 && out && B > 0 && H > 0 && W > 0 && C0 > 0, "ffc_conv3x3_smallm: bad args");
+    FFC_CHECK_ARG(M >= 1 && M <= 4, "ffc_conv3x3_smallm: 1 <= M <= 4");
+    FFC_CHECK_ARG(!x1 || (w1 && C1 > 0), "ffc_conv3x3_smallm: second segment");
+    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 7) == 0, "ffc_conv3x3_smallm: output not 8-B aligned");
+    SmallMArgs a;
+    a.x[0] = x0;
+    a.w[0] = w0;
+    a.C[0] = C0;
+    a.x[1] = x1;
+    a.w[1] = w1;
+    a.C[1] = x1 ? C1 : 0;
+    a.nseg = x1 ? 2 : 1;
+    a.bias = bias;
+    a.out = out;
+    a.B = B;
+    a.IH = H;
+    a.IW = W;
+    a.M = M;
+    a.nty = (H + TT - 1) / TT;
+    a.ntx = (W + TT - 1) / TT;
+    a.act = act;
+    a.act_param = act_param;
+    const size_t lds = 4 * (size_t)EBUF * sizeof(float);
+    const unsigned grid = (unsigned)B * a.nty * a.ntx;
+    auto k = conv3x3_smallm_kernel<4>;
+    static bool raised = false;
+    if (!raised) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess) {
+            ffc::set_error("ffc_conv3x3_smallm: hipFuncSetAttribute failed");
+            return FFC_E_LAUNCH;
+        }
+        raised = true;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_conv3x3_smallm");
 }

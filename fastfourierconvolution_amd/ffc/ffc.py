@@ -42,7 +42,9 @@ class _FFCExec:
                 raise NotImplementedError(f"{type(mod).__name__} in an FFC branch")
         return segs, weights, inputs, addends
 
-    def _run(self, x, y=None, act_l=(0, 0.0), act_g=(0, 0.0), bn_l=None, bn_g=None):
+    def _run(self, x, y=None, act_l=(0, 0.0), act_g=(0, 0.0), bn_l=None, bn_g=None, noise=None):
+        """noise: optional {"l"|"g": (NoiseInjection, noise tensor or None)} applied after the branch's
+        BN + activation in the same pass (FFC_BN_ACT followed by the fgan128 NoiseInjection)"""
         x_l, x_g = x if type(x) is tuple else (x, 0)
         if isinstance(x_l, torch.Tensor):
             x_l = rt.require(x_l, "x_l")
@@ -71,9 +73,9 @@ class _FFCExec:
             if rt.OVERLAP_SPECTRAL == "spectral-first":
                 with torch.cuda.stream(side):
                     v = self.convg2g.spectral(x_g)
-                out_l, _ = self._launch_branches(branches, B, dev, stream)
+                out_l, _ = self._launch_branches(branches, B, dev, stream, noise)
             else:
-                out_l, _ = self._launch_branches(branches, B, dev, stream)
+                out_l, _ = self._launch_branches(branches, B, dev, stream, noise)
                 with torch.cuda.stream(side):
                     v = self.convg2g.spectral(x_g)
             main.wait_stream(side)
@@ -84,7 +86,7 @@ class _FFCExec:
             inp.append((v, None))
             M = self.convl2g.out_channels if isinstance(self.convl2g, (nn.Conv2d, nn.ConvTranspose2d)) else \
                 self.convg2g.conv2.out_channels
-            _, out_g = self._launch_branches([("g", segs, w, inp, add, act_g, bn_g, M)], B, dev, stream)
+            _, out_g = self._launch_branches([("g", segs, w, inp, add, act_g, bn_g, M)], B, dev, stream, noise)
             return out_l, out_g
         if self.ratio_gout != 0:
             segs, w, inp, add = self._branch([(self.convl2g, x_l)])
@@ -105,13 +107,14 @@ class _FFCExec:
             M = self.convl2g.out_channels if isinstance(self.convl2g, (nn.Conv2d, nn.ConvTranspose2d)) else (
                 self.convg2g.conv2.out_channels if isinstance(self.convg2g, SpectralTransform) else None)
             branches.append(("g", segs, w, inp, add, act_g, bn_g, M))
-        return self._launch_branches(branches, B, dev, stream)
+        return self._launch_branches(branches, B, dev, stream, noise)
 
-    def _launch_branches(self, branches, B, dev, stream):
+    def _launch_branches(self, branches, B, dev, stream, noise=None):
         """plan / pack / launch the GEMM(s) of the given branches (one launch per kernel kind),
         then BN statistics and BN+activation passes.  -> (out_l, out_g)"""
         outs = {"l": 0, "g": 0}
         execs, jobs, post = [], [], []
+        jb_name = {}
         for name, segs, w, inp, add, act, bn, M in branches:
             if len(add) > 1:
                 raise NotImplementedError("more than one identity pass-through in a branch")
@@ -122,10 +125,11 @@ class _FFCExec:
                     continue
                 out = addend.clone()
                 outs[name] = out
-                post.append((out, act, bn, None, 0))
+                post.append((name, out, act, bn, None, 0))
                 continue
-            if self._smallm_ok(segs, w, addend, bn, M):
-                out = self._smallm(segs, w, inp, act, M, B, dev, stream)
+            smk = self._smallm_kind(segs, w, addend, bn, M)
+            if smk is not None:
+                out = self._smallm(smk, segs, w, inp, act, M, B, dev, stream)
                 outs[name] = out
                 continue
             out_shape = None
@@ -145,6 +149,7 @@ class _FFCExec:
             if addend is not None and tuple(addend.shape) != tuple(out.shape):
                 raise RuntimeError(f"shape mismatch adding pass-through {tuple(addend.shape)} to {tuple(out.shape)}")
             outs[name] = out
+            jb_name[id(out)] = name
             execs.append(ex)
             jobs.append((ex, inp, out, act, bn, addend))
         groups = {}
@@ -164,19 +169,30 @@ class _FFCExec:
                 fused_act = act if bn is None else (0, 0.0)
                 structs.append(ex.job(inp, out, fused_act[0], fused_act[1], addend, slab))
                 if bn is not None:
-                    post.append((out, act, bn, slab, lp.stat_rows(ji)))
+                    post.append((jb_name[id(out)], out, act, bn, slab, lp.stat_rows(ji)))
             lp.launch(structs, stream, flops=sum(j[0].flops for j in gjobs))
-        for out, act, bn, slab, nrows in post:
+        noise = noise or {}
+        done = set()
+        for name, out, act, bn, slab, nrows in post:
             C = out.shape[1]
+            nz = noise.get(name)
             if bn is not None:
                 sc, sh = rt.bn_scale_shift(bn, C, slab, nrows, 1.0, dev, stream) if slab is not None or \
                     not rt.bn_mode(bn)[0] else self._bn_from_tensor(bn, out, stream)
             else:
-                if act[0] == 0:
+                if act[0] == 0 and nz is None:
                     continue
                 sc = torch.ones(C, device=dev, dtype=torch.float32)
                 sh = torch.zeros(C, device=dev, dtype=torch.float32)
-            rt.bn_act_apply(out, sc, sh, act[0], act[1])
+            if nz is not None and out.shape[2] * out.shape[3] % 4 == 0:
+                mod, n = nz
+                rt.bn_act_noise_apply(out, sc, sh, act[0], act[1], mod, n)
+                done.add(name)
+            else:
+                rt.bn_act_apply(out, sc, sh, act[0], act[1])
+        for name, (mod, n) in noise.items():   # branches without a BN/activation pass of their own
+            if name not in done and isinstance(outs[name], torch.Tensor):
+                outs[name] = mod(outs[name], n)
         return outs["l"], outs["g"]
 
     def _outer_rewrite(self, segs, w, M):
@@ -207,28 +223,39 @@ class _FFCExec:
         return segs2, w2, M * k * k, (M, k, k)
 
     @staticmethod
-    def _smallm_ok(segs, w, addend, bn, M):
-        """ConvT k4 s2 p1 into <= 4 channels (the generator's last layer) -> direct VALU kernel"""
+    def _smallm_kind(segs, w, addend, bn, M):
+        """<= 4 output channels -> direct VALU kernel: 'convT' for ConvT k4 s2 p1 (the generator's last
+        layer, models/ffc_generator.py:28), 'conv3' for Conv k3 s1 p1 (the fgan128 head conv7,
+        fgan128_complete.py:484), else None"""
         if not rt.USE_SMALLM or addend is not None or bn is not None or M is None or M > 4 or \
                 not 1 <= len(segs) <= 2:
-            return False
+            return None
         if sum(1 for x in w if x[4] is not None) > 1:
-            return False
-        return all(sg.kind == "convT" and (sg.k, sg.s, sg.p, sg.d, sg.op) == (4, 2, 1, 1, 0) and
-                   sg.IH == segs[0].IH and sg.IW == segs[0].IW for sg in segs)
+            return None
+        if not all(sg.IH == segs[0].IH and sg.IW == segs[0].IW for sg in segs):
+            return None
+        if all(sg.kind == "convT" and (sg.k, sg.s, sg.p, sg.d, sg.op) == (4, 2, 1, 1, 0) for sg in segs):
+            return "convT"
+        if all(sg.kind == "conv" and (sg.k, sg.s, sg.p, sg.d) == (3, 1, 1, 1) for sg in segs):
+            return "conv3"
+        return None
 
-    def _smallm(self, segs, w, inp, act, M, B, dev, stream):
+    def _smallm(self, kind, segs, w, inp, act, M, B, dev, stream):
         IH, IW = segs[0].IH, segs[0].IW
-        out = torch.empty((B, M, 2 * IH, 2 * IW), device=dev, dtype=torch.float32)
         x1 = inp[1][0] if len(inp) > 1 else None
         w1 = w[1][0] if len(w) > 1 else None
         bias = next((x[4] for x in w if x[4] is not None), None)
-        flops = 2.0 * B * M * sum(sg.C for sg in segs) * 4 * (2 * IH) * (2 * IW)
-        with rt.observe("convt_smallm", flops=flops):
-            rt.check(rt.lib().ffc_convt_k4s2_smallm(
-                inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(), rt.ptr(x1), segs[1].C if x1 is not None else 0,
-                rt.ptr(w1), rt.ptr(bias), B, IH, IW, M, out.data_ptr(), act[0], act[1], stream),
-                "ffc_convt_k4s2_smallm")
+        if kind == "convT":
+            out = torch.empty((B, M, 2 * IH, 2 * IW), device=dev, dtype=torch.float32)
+            fn, label, taps, OH, OW = rt.lib().ffc_convt_k4s2_smallm, "convt_smallm", 4, 2 * IH, 2 * IW
+        else:
+            out = torch.empty((B, M, IH, IW), device=dev, dtype=torch.float32)
+            fn, label, taps, OH, OW = rt.lib().ffc_conv3x3_smallm, "conv3_smallm", 9, IH, IW
+        flops = 2.0 * B * M * sum(sg.C for sg in segs) * taps * OH * OW
+        with rt.observe(label, flops=flops):
+            rt.check(fn(inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(), rt.ptr(x1),
+                        segs[1].C if x1 is not None else 0, rt.ptr(w1), rt.ptr(bias), B, IH, IW, M, out.data_ptr(),
+                        act[0], act[1], stream), f"ffc_{label}")
         return out
 
     def _bn_from_tensor(self, bn, out, stream):

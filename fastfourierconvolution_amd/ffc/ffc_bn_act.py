@@ -54,3 +54,10 @@ class FFC_BN_ACT(nn.Module):
         if y is not None and (bn_l is not None or bn_g is not None):
             raise TypeError("FFC_BN_ACT: BatchNorm2d.forward() takes no label input (reference ffc_bn_act.py:73-81)")
         return self.ffc._run(x, y, rt.act_code(self.act_l), rt.act_code(self.act_g), bn_l, bn_g)
+
+    def forward_noise(self, x, noise_l, noise_g):
+        """forward followed by NoiseInjection on both outputs (fgan128_complete.py:496-515), the noise add
+        fused into the BN + activation pass.  noise_*: (NoiseInjection module, noise tensor or None)."""
+        bn_l, bn_g = self._norm(self.bn_l), self._norm(self.bn_g)
+        return self.ffc._run(x, None, rt.act_code(self.act_l), rt.act_code(self.act_g), bn_l, bn_g,
+                             noise={"l": noise_l, "g": noise_g})

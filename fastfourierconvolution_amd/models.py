@@ -180,10 +180,13 @@ class FGenerator(FFCModel):
         :516-521 is left out"""
         fake = self._noise_to_feature(z)                                     # :491-494
         for i, n in enumerate((2, 3, 4, 5, 6)):                              # :496-515
-            fake = getattr(self, f"conv{n}")(fake)
-            if self.training:
+            conv = getattr(self, f"conv{n}")
+            if self.training:   # NoiseInjection fused into conv{n}'s BN + GELU pass
                 nl, ng = noises[i] if noises is not None else (None, None)
-                fake = (getattr(self, f"lcl_noise{n}")(fake[0], nl), getattr(self, f"glb_noise{n}")(fake[1], ng))
+                fake = conv.forward_noise(fake, (getattr(self, f"lcl_noise{n}"), nl),
+                                          (getattr(self, f"glb_noise{n}"), ng))
+            else:
+                fake = conv(fake)
         return self.resizer(self.conv7(fake))
 
     def forward(self, z, noises=None):

@@ -175,6 +175,12 @@ int ffc_bn_reduce_finalize(const float* slab, int nrows, int C, double* moments,
 /* y = act(x*scale[c] + shift[c]) elementwise (in place allowed) */
 int ffc_bn_act_apply(const float* x, float* y, int B, int C, int HW, const float* scale,
                      const float* shift, int act, float act_param, void* stream);
+/* y = act(x*scale[c] + shift[c]) + noise_w[c] * noise[b] (FFC_BN_ACT followed by the fgan128
+ * NoiseInjection, fgan128_complete.py:496-515 / layers/noise_injection.py:25-32); noise (B, 1, H, W),
+ * HW % 4 == 0, 16-byte aligned tensors; in place allowed */
+int ffc_bn_act_noise_apply(const float* x, float* y, int B, int C, int HW, const float* scale,
+                           const float* shift, int act, float act_param, const float* noise_w,
+                           const float* noise, void* stream);
 
 /* ------------------------------------------------------------------ spectral branch
  * SELayer gate (spectral_transform.py:12-28): gate[b][c] = sigmoid(W2 relu(W1 mean_hw x)),
@@ -200,6 +206,12 @@ int ffc_pack_transpose(const float* w, int R, int K, float* wT, void* stream);
 int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
                           const float* w1, const float* bias, int B, int IH, int IW, int M,
                           float* out, int act, float act_param, void* stream);
+/* Direct Conv2d(k=3, s=1, p=1) for M <= 4 output channels (the fgan128 generator's head conv7,
+ * fgan128_complete.py:484): out = act(conv(x0; w0) [+ conv(x1; w1)] + bias), (B, M, H, W).
+ * w*: raw Conv2d weights (M, C, 3, 3); x1/w1 may be NULL. */
+int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                       const float* w1, const float* bias, int B, int H, int W, int M, float* out,
+                       int act, float act_param, void* stream);
 
 /* Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56), fused per sample:
  *   s   = in_relu ? relu(t*in_scale + in_shift) : t, nearest-upsampled by `up` (1|2)

@@ -183,3 +183,50 @@ def test_noise_injection_kernel():
     x = torch.randn(2, 6, 8, 8, device="cuda")
     n = torch.randn(2, 1, 8, 8, device="cuda")
     torch.testing.assert_close(ni(x, n), x + ni.weight * n, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("cin,M,H,W,bias,rin", [(128, 3, 128, 128, False, 0.5), (16, 1, 40, 24, True, 0.0),
+                                                 (6, 4, 33, 17, False, 0.5)])
+def test_conv3x3_smallm_head_vs_oracle(cin, M, H, W, bias, rin):
+    """FFC_BN_ACT(cin, M, 3, 0.5, 0, 1, 1, Tanh) (the fgan128 head conv7, fgan128_complete.py:484):
+    the direct small-M 3x3 kernel, ragged tiles included"""
+    import torch.nn as nn
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import _runtime as rt
+    from oracle.ffc_oracle import ffc_bn_act
+    gen = torch.Generator().manual_seed(cin + H)
+    with contextlib.redirect_stdout(io.StringIO()):
+        blk = _randomize(F.FFC_BN_ACT(cin, M, 3, rin, 0.0, 1, 1, bias=bias, activation_layer=nn.Tanh), gen)
+    sd = _sd64(blk)
+    cfg = dict(in_channels=cin, out_channels=M, kernel_size=3, ratio_gin=rin, ratio_gout=0.0, stride=1, padding=1,
+               activation_layer="Tanh")
+    blk = blk.cuda()
+    cg = int(cin * rin)
+    xl = torch.randn((2, cin - cg, H, W), generator=gen)
+    xg = torch.randn((2, cg, H, W), generator=gen) if cg else None
+    obs = rt.LaunchObserver()
+    rt.set_observer(obs)
+    try:
+        with torch.no_grad():
+            out, og = blk((xl.cuda(), xg.cuda()) if cg else xl.cuda())
+    finally:
+        rt.set_observer(None)
+    assert og == 0 and "conv3_smallm" in obs.summary()
+    ref, _ = ffc_bn_act((xl.double(), xg.double()) if cg else xl.double(), sd, "", cfg, True)
+    assert normwise_err(out.cpu(), ref) <= TOL
+
+
+@pytest.mark.parametrize("H,pool", [(64, False), (64, True), (128, False)])
+def test_se_gate_wide_planes(H, pool):
+    """SELayer gate on large planes (plane-mean kernel + per-sample FC) vs the oracle's se_layer"""
+    import fastfourierconvolution_amd as F
+    import torch.nn.functional as Fn
+    gen = torch.Generator().manual_seed(H)
+    se = _randomize(F.SELayer(64), gen)
+    sd = _sd64(se)
+    x = torch.randn((3, 64, H, H), generator=gen)
+    g = se.cuda().gate(x.cuda(), pool).cpu()
+    xr = Fn.avg_pool2d(x.double(), 2) if pool else x.double()
+    y = xr.mean(dim=(2, 3))                      # spectral_transform.py:23-28
+    ref = torch.sigmoid(Fn.linear(torch.relu(Fn.linear(y, sd["fc.0.weight"])), sd["fc.2.weight"]))
+    assert normwise_err(g, ref) <= 1e-5
