@@ -206,135 +206,165 @@ __global__ __launch_bounds__(SM_THREADS) void convt_smallm_kernel(SmallMArgs a) 
 }
 
 
-constexpr int WE3 = CCH * 4 * 12;   // conv3 chunk weights [cc][m][12] (M <= 4)
-static_assert(WE3 <= WE, "conv3 weights fit the ConvT weight slot");
+// ---- Conv2d k3 s1 p1, M <= 4: 64x64 output tile per workgroup, 4x4 outputs per thread.
+// The input patch row covers ix = x0-4 .. x0+67 (72 floats = 18 aligned float4 groups; W % 4 == 0,
+// so a group is wholly inside or outside the image).  The two halves of the workgroup take
+// alternate channels; each stages one channel per step through registers: the global loads of
+// channel k+1 are issued before channel k's FMAs and written to the other LDS buffer after them
+// (an LDS-DMA pipeline would not overlap: the compiler waits for every outstanding LDS-DMA before
+// any LDS read).  All weights are staged once, as [channel][m][12] (9 taps, padded).
+// Per channel a thread reads its 6x6 neighbourhood as 6 x (b32 + b128 + b32) and 3 x 3 broadcast
+// b128 of weights: 18 + 3M LDS reads feed 144M FMAs.
+constexpr int T3 = 64;                      // output tile side
+constexpr int R3 = T3 + 2;                  // patch rows (halo 1)
+constexpr int S3 = T3 + 8;                  // patch row: 18 float4 groups
+constexpr int G3 = R3 * (S3 / 4);           // float4 groups per channel
+constexpr int GT3 = (G3 + 255) / 256;       // groups per thread
+constexpr int PB3 = G3 * 4;                 // floats per patch buffer
+constexpr int CMAX3 = 256;                  // channels (both segments) whose weights fit the LDS slot
 
 template <int MM>
 __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int half = threadIdx.x >> 8, tid = threadIdx.x & 255, wave = tid >> 6;
+    const int half = threadIdx.x >> 8, tid = threadIdx.x & 255;
     int bid = blockIdx.x;
     const int tx = bid % a.ntx;
     bid /= a.ntx;
     const int ty = bid % a.nty;
     const int b = bid / a.nty;
-    const int y0 = ty * TT, x0 = tx * TT;
-    const int qy = 2 * (tid >> 4), qx = 2 * (tid & 15);   // top-left of this thread's 2x2 outputs
+    const int y0 = ty * T3, x0 = tx * T3;
+    const int qy = 4 * (tid >> 4), qx = 4 * (tid & 15);   // this thread's 4x4 outputs (tile coords)
     const int M = a.M;
+    const int nchunks = a.C[0] + (a.nseg > 1 ? a.C[1] : 0);   // one channel per chunk
+    float* wl_all = lds;                                      // [nchunks][4][12]
+    float* pbuf = lds + CMAX3 * 48;                           // [2 buffers][2 halves][PB3]
 
-    const int nch0 = (a.C[0] + CCH - 1) / CCH;
-    const int nchunks = nch0 + (a.nseg > 1 ? (a.C[1] + CCH - 1) / CCH : 0);
+    for (int q = threadIdx.x; q < nchunks * 48; q += SM_THREADS) {
+        const int ci = q / 48, m = (q / 12) & 3, t = q % 12;
+        const int s = ci < a.C[0] ? 0 : 1;
+        const int c = s == 0 ? ci : ci - a.C[0];
+        wl_all[q] = (t < 9 && m < M) ? a.w[s][((size_t)m * a.C[s] + c) * 9 + t] : 0.0f;
+    }
 
-    auto stage = [&](int ci, float* dst) {
-        const int s = ci < nch0 ? 0 : 1;
-        const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
-        const float* x = a.x[s];
-        const float* w = a.w[s];   // Conv2d weights (M, C, 3, 3)
-        const int C = a.C[s];
-        for (int e = 0; e * 256 < PE + WE3; ++e) {
-            const int n = e * 256 + tid;
-            const float* src = g_zero_sm;
-            if (n < PE) {
-                const int pc = n % PP, r = n / PP;
-                const int pr = r % PP, ch = r / PP;
-                const int iy = y0 - 1 + pr, ix = x0 - 1 + pc, c = c0 + ch;
-                if (c < C && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
-                    src = x + (((size_t)b * C + c) * a.IH + iy) * a.IW + ix;
-            } else if (n - PE < WE3) {
-                const int q = n - PE;
-                const int t = q % 12, m = (q / 12) & 3, cc = q / 48;
-                if (t < 9 && m < M && c0 + cc < C) src = w + ((size_t)m * C + c0 + cc) * 9 + t;
-            }
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
+    auto load = [&](int ci, float4 (&r)[GT3]) {
+        const int s = ci < a.C[0] ? 0 : 1;
+        const int c = s == 0 ? ci : ci - a.C[0];
+        const float* x = a.x[s] + ((size_t)b * a.C[s] + c) * a.IH * a.IW;
+#pragma unroll
+        for (int j = 0; j < GT3; ++j) {
+            const int n = j * 256 + tid;
+            const int g = n % (S3 / 4), pr = n / (S3 / 4);
+            const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
+            r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (n < G3 && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
+                r[j] = *reinterpret_cast<const float4*>(x + (size_t)iy * a.IW + ix);
         }
     };
+    auto put = [&](float* dst, const float4 (&r)[GT3]) {
+#pragma unroll
+        for (int j = 0; j < GT3; ++j) {
+            const int n = j * 256 + tid;
+            if (n < G3) reinterpret_cast<float4*>(dst)[n] = r[j];
+        }
+    };
+    auto buf = [&](int k) { return pbuf + ((k & 1) * 2 + half) * PB3; };
 
-    float acc[MM][2][2];
+    float acc[MM][4][4];
 #pragma unroll
     for (int m = 0; m < MM; ++m)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[m][i][j] = 0.0f;
+            for (int j = 0; j < 4; ++j) acc[m][i][j] = 0.0f;
 
-    const int nsteps = (nchunks + 1) / 2;   // half h takes chunks 2k + h
-    if (half < nchunks) stage(half, lds + half * EBUF);
-    for (int k = 0; k < nsteps; ++k) {
-        __syncthreads();
+    const int nsteps = (nchunks + 1) / 2;   // half h takes chunks 2k + h (its k-th channel)
+    auto compute = [&](int k) {
         const int ci = 2 * k + half;
-        if (ci + 2 < nchunks) stage(ci + 2, lds + (((k + 1) & 1) * 2 + half) * EBUF);
-        if (ci >= nchunks) continue;
-        const float* cur = lds + ((k & 1) * 2 + half) * EBUF;
-        const int s = ci < nch0 ? 0 : 1;
-        const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
-        const int cn = min(CCH, a.C[s] - c0);
-        for (int cc = 0; cc < cn; ++cc) {
-            float v[4][4];   // input rows qy-1..qy+2, cols qx-1..qx+2
-            const float* p = cur + (cc * PP + qy) * PP + qx;
+        if (ci >= nchunks) return;
+        const float* cur = buf(k);
+        float v[6][6];   // input rows qy-1..qy+4, cols qx-1..qx+4 = patch rows qy..qy+5, cols qx+3..qx+8
+        const float* p = cur + qy * S3 + qx + 3;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const float4 l4 = *reinterpret_cast<const float4*>(p + i * S3 + 1);
+            v[i][0] = p[i * S3];
+            v[i][1] = l4.x; v[i][2] = l4.y; v[i][3] = l4.z; v[i][4] = l4.w;
+            v[i][5] = p[i * S3 + 5];
+        }
+        const float* wl = wl_all + ci * 48;
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            float k9[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const float4 t = reinterpret_cast<const float4*>(wl + m * 12)[q];
+                k9[4 * q] = t.x; k9[4 * q + 1] = t.y; k9[4 * q + 2] = t.z; k9[4 * q + 3] = t.w;
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[i][j] = p[i * PP + j];
-            const float* wl = cur + PE + cc * 48;
+                for (int j = 0; j < 4; ++j) {
+                    float s2 = acc[m][i][j];
 #pragma unroll
-            for (int m = 0; m < MM; ++m) {
-                if (m < M) {
-                    float k9[12];
+                    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const float4 t = reinterpret_cast<const float4*>(wl + m * 12)[q];
-                        k9[4 * q] = t.x; k9[4 * q + 1] = t.y; k9[4 * q + 2] = t.z; k9[4 * q + 3] = t.w;
-                    }
-#pragma unroll
-                    for (int i = 0; i < 2; ++i)
-#pragma unroll
-                        for (int j = 0; j < 2; ++j) {
-                            float s2 = acc[m][i][j];
-#pragma unroll
-                            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                                for (int kx = 0; kx < 3; ++kx) s2 = fmaf(v[i + ky][j + kx], k9[ky * 3 + kx], s2);
-                            acc[m][i][j] = s2;
-                        }
+                        for (int kx = 0; kx < 3; ++kx) s2 = fmaf(v[i + ky][j + kx], k9[ky * 3 + kx], s2);
+                    acc[m][i][j] = s2;
                 }
-            }
         }
+    };
+    // one channel of prefetch in registers: channel k+1's loads are in flight under channel k's FMAs
+    // (a second register set measured slower: 196 VGPRs, same occupancy)
+    float4 r[GT3];
+    if (half < nchunks) {
+        load(half, r);
+        put(buf(0), r);
+    }
+    __syncthreads();
+    for (int k = 0; k < nsteps; ++k) {
+        const int cn = 2 * (k + 1) + half;
+        if (cn < nchunks) load(cn, r);
+        compute(k);
+        if (cn < nchunks) put(buf(k + 1), r);
+        __syncthreads();
     }
     // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
-    __syncthreads();
-    float* part = lds;
+    float* part = pbuf;   // 256 threads x MM x 16 floats <= 4 * PB3
     if (half == 1) {
 #pragma unroll
         for (int m = 0; m < MM; ++m)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) part[((m * 2 + i) * 2 + j) * 256 + tid] = acc[m][i][j];
+                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * 256 + tid] = acc[m][i][j];
     }
     __syncthreads();
     if (half == 1) return;
 #pragma unroll
     for (int m = 0; m < MM; ++m)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[m][i][j] += part[((m * 2 + i) * 2 + j) * 256 + tid];
+            for (int j = 0; j < 4; ++j) acc[m][i][j] += part[((m * 4 + i) * 4 + j) * 256 + tid];
     const int oy0 = y0 + qy, ox0 = x0 + qx;
-    const bool xin = ox0 + 1 < a.IW;
+    const bool xin = ox0 + 3 < a.IW;
     auto store = [&](auto actf) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             if (m >= M) break;
             const float bv = a.bias ? a.bias[m] : 0.0f;
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < 4; ++i) {
                 const int oy = oy0 + i;
                 if (oy >= a.IH) continue;
                 float* row = a.out + (((size_t)b * M + m) * a.IH + oy) * a.IW + ox0;
                 if (xin) {
-                    *reinterpret_cast<float2*>(row) = make_float2(actf(acc[m][i][0] + bv), actf(acc[m][i][1] + bv));
-                } else if (ox0 < a.IW) {
-                    row[0] = actf(acc[m][i][0] + bv);
+                    *reinterpret_cast<float4*>(row) = make_float4(actf(acc[m][i][0] + bv), actf(acc[m][i][1] + bv),
+                                                                  actf(acc[m][i][2] + bv), actf(acc[m][i][3] + bv));
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (ox0 + j < a.IW) row[j] = actf(acc[m][i][j] + bv);
                 }
             }
         }
@@ -399,7 +429,8 @@ extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, cons
     FFC_CHECK_ARG(x0 && w0 && out && B > 0 && H > 0 && W > 0 && C0 > 0, "ffc_conv3x3_smallm: bad args");
     FFC_CHECK_ARG(M >= 1 && M <= 4, "ffc_conv3x3_smallm: 1 <= M <= 4");
     FFC_CHECK_ARG(!x1 || (w1 && C1 > 0), "ffc_conv3x3_smallm: second segment");
-    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 7) == 0, "ffc_conv3x3_smallm: output not 8-B aligned");
+    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0 && W % 4 == 0,
+                  "ffc_conv3x3_smallm: output not 16-B aligned or W % 4 != 0");
     SmallMArgs a;
     a.x[0] = x0;
     a.w[0] = w0;
@@ -414,21 +445,24 @@ extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, cons
     a.IH = H;
     a.IW = W;
     a.M = M;
-    a.nty = (H + TT - 1) / TT;
-    a.ntx = (W + TT - 1) / TT;
+    a.nty = (H + T3 - 1) / T3;
+    a.ntx = (W + T3 - 1) / T3;
     a.act = act;
     a.act_param = act_param;
-    const size_t lds = 4 * (size_t)EBUF * sizeof(float);
+    FFC_CHECK_ARG(C0 + (x1 ? C1 : 0) <= CMAX3, "ffc_conv3x3_smallm: at most 256 input channels");
+    const size_t lds = (CMAX3 * 48 + 4 * (size_t)PB3) * sizeof(float);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
-    auto k = conv3x3_smallm_kernel<4>;
-    static bool raised = false;
-    if (!raised) {
+    // M is a template parameter: no runtime m < M branches in the FMA body
+    auto k = M == 1 ? conv3x3_smallm_kernel<1> : M == 2 ? conv3x3_smallm_kernel<2>
+           : M == 3 ? conv3x3_smallm_kernel<3> : conv3x3_smallm_kernel<4>;
+    static bool raised[5] = {false, false, false, false, false};
+    if (!raised[M]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) {
             ffc::set_error("ffc_conv3x3_smallm: hipFuncSetAttribute failed");
             return FFC_E_LAUNCH;
         }
-        raised = true;
+        raised[M] = true;
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_conv3x3_smallm");

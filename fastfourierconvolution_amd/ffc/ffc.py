@@ -236,7 +236,7 @@ class _FFCExec:
             return None
         if all(sg.kind == "convT" and (sg.k, sg.s, sg.p, sg.d, sg.op) == (4, 2, 1, 1, 0) for sg in segs):
             return "convT"
-        if all(sg.kind == "conv" and (sg.k, sg.s, sg.p, sg.d) == (3, 1, 1, 1) for sg in segs):
+        if segs[0].IW % 4 == 0 and all(sg.kind == "conv" and (sg.k, sg.s, sg.p, sg.d) == (3, 1, 1, 1) for sg in segs):
             return "conv3"
         return None
 

@@ -186,7 +186,7 @@ def test_noise_injection_kernel():
 
 
 @pytest.mark.parametrize("cin,M,H,W,bias,rin", [(128, 3, 128, 128, False, 0.5), (16, 1, 40, 24, True, 0.0),
-                                                 (6, 4, 33, 17, False, 0.5)])
+                                                 (6, 4, 33, 20, False, 0.5), (64, 3, 96, 72, False, 0.5)])
 def test_conv3x3_smallm_head_vs_oracle(cin, M, H, W, bias, rin):
     """FFC_BN_ACT(cin, M, 3, 0.5, 0, 1, 1, Tanh) (the fgan128 head conv7, fgan128_complete.py:484):
     the direct small-M 3x3 kernel, ragged tiles included"""
