@@ -103,6 +103,10 @@ SIGNATURES = [
     ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),
     ("ffc_conv3x3_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                    c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
+    ("ffc_pw_gate_blocks", c_int, [c_int]),
+    ("ffc_pw_gate_lds_bytes", c_size_t, [c_int, c_int]),
+    ("ffc_pw_gate_conv", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p]),
     ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                       c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
 ]

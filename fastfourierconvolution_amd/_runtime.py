@@ -226,6 +226,11 @@ USE_PATCH = True   # LDS-patch kernel where it applies (tests flip this to cover
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
+# Fourier-unit path where both apply: the fused one-workgroup-per-sample kernel fills the chip only
+# with B >= ~CUs/2 samples; smaller batches (fgan128's 64-sample shards) run the staged kernels,
+# which spread every sample over many workgroups.  "auto" | "fused" | "staged"
+FU_PATH = __import__("os").environ.get("FFC_FU_PATH", "auto")
+FU_FUSED_MIN_BATCH = 128
 # Run SpectralTransform's kernels on a side stream beside the local-branch GEMM of the same FFC
 # layer ("gemm-first" / "spectral-first": which is issued first).  Off by default: measured on
 # MI355X (B=256 generator) 10-18 % slower than one launch pairing the local and global GEMMs,

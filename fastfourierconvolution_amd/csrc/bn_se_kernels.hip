@@ -342,7 +342,7 @@ extern "C" int ffc_se_gate(const float* x, int B, int C, int H, int W, int pool,
     FFC_CHECK_ARG(x && gate && B > 0 && C > 0 && H > 0 && W > 0 && hidden >= 0, "ffc_se_gate: bad args");
     FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_se_gate: null weights");
     const size_t lds = sizeof(float) * (C + hidden);
-    const bool wide = (W % 4 == 0) && (!pool || (H % 2 == 0 && W % 2 == 0)) && H * W >= 1024 &&
+    const bool wide = (W % 4 == 0) && (!pool || (H % 2 == 0 && W % 2 == 0)) && H * W >= 64 &&
                       (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     if (wide) {
         // plane means into the gate buffer, then the FCs in place (each sample's block reads its

@@ -505,6 +505,7 @@ typedef void (*MixKernel)(MixArgs);
 R2cKernel pick_r2c(int h, int w) {
     if (h != w) return nullptr;
     switch (h) {
+        case 8: return fu2d_r2c_kernel<8, 8>;
         case 16: return fu2d_r2c_kernel<16, 16>;
         case 32: return fu2d_r2c_kernel<32, 32>;
         case 64: return fu2d_r2c_kernel<64, 64>;
@@ -519,6 +520,7 @@ C2rKernel pick_c2r_up(int up) { return up == 1 ? fu2d_c2r_kernel<N, N, 1> : fu2d
 C2rKernel pick_c2r(int H, int W, int up) {
     if (H != W) return nullptr;
     switch (H) {
+        case 16: return pick_c2r_up<16>(up);
         case 32: return pick_c2r_up<32>(up);
         case 64: return pick_c2r_up<64>(up);
         case 128: return pick_c2r_up<128>(up);
@@ -561,26 +563,28 @@ int raise_lds(const void* k, size_t lds, const char* what) {
     return FFC_OK;
 }
 
-// workgroups per sample: ~MIX_TILES_PER_WG bin tiles each (2 per wave)
-int mix_nsplit(int H, int W) {
+// workgroups per sample: ~MIX_TILES_PER_WG bin tiles each (2 per wave), but enough workgroups
+// (>= ~1024) to fill the chip when the batch is small, down to one tile per workgroup
+int mix_nsplit(int B, int H, int W) {
     const int ntiles = (H * (W / 2 + 1) + 31) / 32;
-    return std::max(1, ntiles / MIX_TILES_PER_WG);
+    const int fill = (1024 + B - 1) / B;
+    return std::max(1, std::min(ntiles, std::max(ntiles / MIX_TILES_PER_WG, fill)));
 }
 
 }  // namespace
 
 extern "C" int ffc_fu2d_supported(int C, int H, int W, int up) {
     if (C <= 0 || 2 * C > 128 || H != W || !(up == 1 || up == 2)) return 0;
-    if (!pow2_in(H, 32, 128)) return 0;
+    if (!pow2_in(H, 16, 128)) return 0;
     const int h = H / up;
-    if (!pow2_in(h, 16, 128)) return 0;
+    if (!pow2_in(h, 8, 128)) return 0;
     if (r2c_lds(h, h) > 160 * 1024 || c2r_lds(H, W) > 160 * 1024) return 0;
     return 1;
 }
 
 extern "C" int ffc_fu2d_slab_rows(int B, int C, int H, int W) {
     if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
-    return B * mix_nsplit(H, W);
+    return B * mix_nsplit(B, H, W);
 }
 
 extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const float* in_scale,
@@ -589,7 +593,7 @@ extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const fl
     FFC_CHECK_ARG(t && T, "ffc_fu2d_r2c: null pointer");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_r2c: in_scale/in_shift pairing");
     R2cKernel k = pick_r2c(h, w);
-    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_r2c: unsupported plane (square, power of two in [16, 128])");
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_r2c: unsupported plane (square, power of two in [8, 128])");
     const size_t lds = r2c_lds(h, w);
     FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_fu2d_r2c: plane exceeds LDS");
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c");
@@ -623,7 +627,7 @@ extern "C" int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, 
     a.W = W;
     a.up = up;
     a.ntiles = (H * (W / 2 + 1) + 31) / 32;
-    a.nsplit = mix_nsplit(H, W);
+    a.nsplit = mix_nsplit(B, H, W);
     a.Mpad = (2 * C + 31) / 32 * 32;
     a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
     const size_t lds = mix_lds(C, pass);
@@ -642,7 +646,7 @@ extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const fl
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu2d_c2r: up must be 1 or 2");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
     C2rKernel k = pick_c2r(H, W, up);
-    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [32, 128])");
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [16, 128])");
     const size_t lds = c2r_lds(H, W);
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_c2r");
     if (rc) return rc;

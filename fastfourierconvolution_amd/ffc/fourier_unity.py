@@ -48,11 +48,14 @@ class FourierUnitSN(nn.Module):
         self._check(C)
         L = rt.lib()
         fused = L.ffc_fu_lds_bytes(C, H, W) > 0 and not rt.FORCE_FU2D
+        staged_ok = L.ffc_fu2d_supported(C, H, W, up)
+        if fused and staged_ok and (rt.FU_PATH == "staged" or (rt.FU_PATH == "auto" and B < rt.FU_FUSED_MIN_BATCH)):
+            fused = False
         if not fused:
             if L.ffc_fu2d_supported(C, H, W, up):
                 return self._run2d(t, up, in_scale, in_shift, in_relu, residual)
             raise NotImplementedError(f"Fourier unit supports H,W in {{4,8,16,32}} with 16*C*H*(W/2+1) <= 160 KiB "
-                                      f"(fused) or square H=W in {{32,64,128}} with 2C <= 128 (staged); "
+                                      f"(fused) or square H=W in {{16,32,64,128}} with 2C <= 128 (staged); "
                                       f"got C={C}, {H}x{W}")
         dev = t.device
         stream = rt.stream_of(t)

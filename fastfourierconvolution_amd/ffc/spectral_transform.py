@@ -132,6 +132,16 @@ class SpectralTransform(nn.Module):
                 check(L.ffc_st_prologue(ptr(x), B, Cin, H, W, int(pool), ptr(se1), ptr(se2), hid, ptr(wc), c, ptr(t),
                                         ptr(slab), None, stream), "ffc_st_prologue")
             nrows = B
+        elif not pool and L.ffc_pw_gate_lds_bytes(Cin, c) > 0:
+            # large planes: SE gate (plane means + FCs), then conv1 with the gate folded into the
+            # per-sample weights and the bn1 partials in the epilogue (csrc/st_pw.hip)
+            gate = self.se_block.gate(x, pool)
+            w1 = rt.require(self.conv1.weight.detach(), "conv1.weight")
+            nrows = B * L.ffc_pw_gate_blocks(h2 * w2)
+            slab = torch.empty((nrows, c, 4), device=dev, dtype=torch.float32) if use_batch else None
+            with rt.observe("st_conv1", flops=2.0 * B * c * Cin * h2 * w2, bytes=4.0 * B * (Cin + c) * h2 * w2):
+                check(L.ffc_pw_gate_conv(ptr(x), ptr(gate), ptr(w1), B, Cin, c, h2 * w2, ptr(t), ptr(slab), stream),
+                      "ffc_pw_gate_conv")
         else:
             gate = self.se_block.gate(x, pool)
             key = ("conv1", B, Cin, h2, w2, pool, str(dev))

@@ -197,6 +197,14 @@ size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, in
 int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
                     const float* w2, int hidden, const float* wconv1T, int c, float* t, float* slab,
                     float* gate_out, void* stream);
+/* SpectralTransform conv1 with the SE gate for planes the fused prologue cannot hold
+ * (spectral_transform.py:87-89): t[b,o,p] = sum_c w[o,c] * gate[b,c] * x[b,c,p], p < HW, plus
+ * bn1 partials slab [B * ffc_pw_gate_blocks(HW)][M] float4 {n, mean, M2} (slab may be NULL).
+ * w: conv1 weight (M, Cin); gate (B, Cin) or NULL.  ffc_pw_gate_lds_bytes() == 0: unsupported. */
+int ffc_pw_gate_blocks(int HW);
+size_t ffc_pw_gate_lds_bytes(int Cin, int M);
+int ffc_pw_gate_conv(const float* x, const float* gate, const float* w, int B, int Cin, int M, int HW,
+                     float* t, float* slab, void* stream);
 /* wT[k][o] = w[o][k] for a row-major (R, K) matrix, o zero-padded to ceil32(R) */
 int ffc_pack_transpose(const float* w, int R, int K, float* wT, void* stream);
 
@@ -232,7 +240,7 @@ size_t ffc_fu_lds_bytes(int C, int H, int W);
 
 /* Large-plane Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56, for planes whose
  * per-sample spectrum does not fit one workgroup's LDS: the fgan128 generator's 64x64 and
- * 128x128 FUs, fgan128_complete.py:474-485).  Square H = W, a power of two in [32, 128],
+ * 128x128 FUs, fgan128_complete.py:474-485).  Square H = W, a power of two in [16, 128],
  * 2C <= 128, up in {1, 2}; (h, w) = (H/up, W/up) is the grid of t.  Three stages over HBM:
  *   ffc_fu2d_r2c: T = rfft2(s0) unnormalised, s0 = in_relu ? relu(t*in_scale + in_shift) : t;
  *                 T (B, C, h, w/2+1) complex64 (interleaved float2)

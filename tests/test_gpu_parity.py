@@ -17,7 +17,7 @@ CASES = golden_cases()
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
-def test_golden(case):
+def test_golden(case, fu_path):
     state, inputs, data = load_case(case)
     mod = build_dropin(case, state)
     out = call_dropin(case, mod, inputs)
@@ -109,8 +109,18 @@ def test_generator_eval_matches_oracle():
     assert normwise_err(out, ref) <= TOL
 
 
-def test_fu_sizes_vs_oracle():
-    """every supported FU plane size, train + eval, several channel counts"""
+@pytest.fixture(params=["fused", "staged"])
+def fu_path(request):
+    """run a test under each Fourier-unit path (the auto choice depends on the batch size)"""
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.FU_PATH
+    rt.FU_PATH = request.param
+    yield request.param
+    rt.FU_PATH = old
+
+
+def test_fu_sizes_vs_oracle(fu_path):
+    """every supported FU plane size, train + eval, several channel counts, fused and staged paths"""
     import fastfourierconvolution_amd as F
     from oracle.ffc_oracle import fourier_unit
     gen = torch.Generator().manual_seed(11)
