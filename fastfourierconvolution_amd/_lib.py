@@ -107,6 +107,8 @@ SIGNATURES = [
     ("ffc_pw_gate_lds_bytes", c_size_t, [c_int, c_int]),
     ("ffc_pw_gate_conv", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p]),
+    ("ffc_dense_forward", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                  c_int, c_float, c_void_p]),
     ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                       c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
 ]

@@ -239,11 +239,21 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
     float* wl_all = lds;                                      // [nchunks][4][12]
     float* pbuf = lds + CMAX3 * 48;                           // [2 buffers][2 halves][PB3]
 
-    for (int q = threadIdx.x; q < nchunks * 48; q += SM_THREADS) {
-        const int ci = q / 48, m = (q / 12) & 3, t = q % 12;
-        const int s = ci < a.C[0] ? 0 : 1;
-        const int c = s == 0 ? ci : ci - a.C[0];
-        wl_all[q] = (t < 9 && m < M) ? a.w[s][((size_t)m * a.C[s] + c) * 9 + t] : 0.0f;
+    for (int q0 = 0; q0 < nchunks * 48; q0 += 8 * SM_THREADS) {   // 8 loads in flight per thread
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * SM_THREADS + threadIdx.x;
+            const int ci = q / 48, m = (q / 12) & 3, t = q % 12;
+            const int s = ci < a.C[0] ? 0 : 1;
+            const int c = s == 0 ? ci : ci - a.C[0];
+            v[u] = (q < nchunks * 48 && t < 9 && m < M) ? a.w[s][((size_t)m * a.C[s] + c) * 9 + t] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + u * SM_THREADS + threadIdx.x;
+            if (q < nchunks * 48) wl_all[q] = v[u];
+        }
     }
 
     auto load = [&](int ci, float4 (&r)[GT3]) {

@@ -1,0 +1,116 @@
+// Dense GEMM + bias + activation for gfx950 (v_mfma_f32_32x32x2_f32, exact fp32):
+//   out[b][n] = act(sum_k A[b][k] * Wt[k][n] + bias[n])
+// Used where a layer is a plain matrix product:
+//   - ConvTranspose2d(k, s=1, p=0) on a 1x1 input (the FFC-DCGAN generator's first layer,
+//     models/ffc_generator.py:24; ffc_transpose.py:79-86): n = (m, ky, kx), so the (B, M*k*k)
+//     result IS the (B, M, k, k) output; its l and g branches go to two outputs of one launch.
+//   - the fgan128 generator's nn.Linear(z, 16*1024) (fgan128_complete.py:453-455).
+// Workgroup tile: 64 rows (b) x 64 columns (n), A staged in LDS; each of the 4 waves owns 32 x 32.
+#include "ffc_internal.h"
+
+namespace {
+
+constexpr int DN_THREADS = 256;
+constexpr int DN_BM = 64, DN_BN = 64;   // 4 waves, each 32 x 32
+constexpr int DN_KMAX = 256;            // A tile (64 x K) staged in LDS, rows padded to K+1
+
+struct DenseArgs {
+    const float* A;      // (B, K)
+    const float* Wt;     // (K, N) row-major
+    const float* bias;   // (N) or null
+    float* out0;         // columns [0, N0): (B, N0)
+    float* out1;         // columns [N0, N): (B, N - N0), or null when N0 == N
+    int B, K, N, N0;
+    int act;
+    float act_param;
+};
+
+__global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
+    extern __shared__ float As[];   // [64][K+1]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hh = lane >> 5, col = lane & 31;
+    const int ntn = (a.N + DN_BN - 1) / DN_BN;
+    const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+    const int b0 = tm * DN_BM;
+    const int KS = a.K + 1;
+    // coalesced rows of A, 8 loads in flight per thread before their LDS stores
+    for (int i0 = 0; i0 < DN_BM * a.K; i0 += 8 * DN_THREADS) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * DN_THREADS + tid;
+            const int r = i / a.K;
+            v[u] = (i < DN_BM * a.K && b0 + r < a.B) ? a.A[(size_t)b0 * a.K + i] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * DN_THREADS + tid;
+            const int r = i / a.K, k = i - r * a.K;
+            if (i < DN_BM * a.K) As[r * KS + k] = v[u];
+        }
+    }
+    __syncthreads();
+    const int wr = wave >> 1, wc = wave & 1;
+    const int n = tn * DN_BN + wc * 32 + col;
+    const bool nv = n < a.N;
+    const float* ar = As + (wr * 32 + col) * KS;   // this lane's A row
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    auto load = [&](int k0, float (&wa)[8]) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + 2 * u + hh;
+            wa[u] = (k < a.K && nv) ? a.Wt[(size_t)k * a.N + n] : 0.0f;
+        }
+    };
+    auto mma = [&](int k0, const float (&wa)[8]) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + 2 * u + hh;
+            const float av = k < a.K ? ar[k] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wa[u], acc, 0, 0, 0);
+        }
+    };
+    float w0[8], w1[8];
+    load(0, w0);
+    for (int k0 = 0; k0 < a.K; k0 += 32) {   // the next 16-deep chunk's loads under this chunk's MFMAs
+        if (k0 + 16 < a.K) load(k0 + 16, w1);
+        mma(k0, w0);
+        if (k0 + 16 >= a.K) break;
+        if (k0 + 32 < a.K) load(k0 + 32, w0);
+        mma(k0 + 16, w1);
+    }
+    if (!nv) return;
+    const float bv = a.bias ? a.bias[n] : 0.0f;
+    float* dst;
+    int ld, nn;
+    if (n < a.N0) {
+        dst = a.out0;
+        ld = a.N0;
+        nn = n;
+    } else {
+        dst = a.out1;
+        ld = a.N - a.N0;
+        nn = n - a.N0;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int b = b0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (b < a.B) dst[(size_t)b * ld + nn] = ffc::apply_act(acc[r] + bv, a.act, a.act_param);
+    }
+}
+
+}  // namespace
+
+extern "C" int ffc_dense_forward(const float* A, const float* Wt, const float* bias, int B, int K, int N, int N0,
+                                 float* out0, float* out1, int act, float act_param, void* stream) {
+    FFC_CHECK_ARG(A && Wt && out0 && B > 0 && K > 0 && N > 0, "ffc_dense_forward: bad args");
+    FFC_CHECK_ARG(N0 > 0 && N0 <= N && (N0 == N || out1 != nullptr), "ffc_dense_forward: output split");
+    FFC_CHECK_ARG(K <= DN_KMAX, "ffc_dense_forward: K > 256");
+    DenseArgs a{A, Wt, bias, out0, out1, B, K, N, N0, act, act_param};
+    const int grid = ((B + DN_BM - 1) / DN_BM) * ((N + DN_BN - 1) / DN_BN);
+    const size_t lds = sizeof(float) * DN_BM * (K + 1);
+    hipLaunchKernelGGL(dense_kernel, dim3(grid), dim3(DN_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_dense_forward");
+}

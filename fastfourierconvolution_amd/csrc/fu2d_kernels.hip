@@ -154,14 +154,25 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
 
     // 1. t plane -> transform -> R
     const float4* src = reinterpret_cast<const float4*>(a.t + (size_t)plane * h * w);
-    for (int i = tid; i < h * w / 4; i += FU2_THREADS) {
-        float4 v = src[i];
-        v.x = in_tf(v.x, sc, sh, a.in_relu);
-        v.y = in_tf(v.y, sc, sh, a.in_relu);
-        v.z = in_tf(v.z, sc, sh, a.in_relu);
-        v.w = in_tf(v.w, sc, sh, a.in_relu);
-        const int r = i / (w / 4), c4 = i % (w / 4);
-        *reinterpret_cast<float4*>(R + r * RS + 4 * c4) = v;
+    constexpr int NV = (h * w / 4 + FU2_THREADS - 1) / FU2_THREADS;   // float4 per thread, all in flight
+    float4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = j * FU2_THREADS + tid;
+        if (i < h * w / 4) v[j] = src[i];
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = j * FU2_THREADS + tid;
+        if (i < h * w / 4) {
+            float4 q = v[j];
+            q.x = in_tf(q.x, sc, sh, a.in_relu);
+            q.y = in_tf(q.y, sc, sh, a.in_relu);
+            q.z = in_tf(q.z, sc, sh, a.in_relu);
+            q.w = in_tf(q.w, sc, sh, a.in_relu);
+            const int r = i / (w / 4), c4 = i % (w / 4);
+            *reinterpret_cast<float4*>(R + r * RS + 4 * c4) = q;
+        }
     }
     __syncthreads();
 

@@ -31,10 +31,23 @@ __global__ __launch_bounds__(PW_THREADS) void pw_gate_kernel(PwArgs a) {
     const int hh = lane >> 5, col = lane & 31;
     const int b = blockIdx.x / a.nblk, blk = blockIdx.x - b * a.nblk;
     const int C = a.Cin, M = a.M;
-    for (int i = tid; i < C * a.Mpad; i += PW_THREADS) {
-        const int c = i / a.Mpad, o = i - c * a.Mpad;
-        const float g = a.gate ? a.gate[(size_t)b * C + c] : 1.0f;
-        Wg[i] = o < M ? a.w[(size_t)o * C + c] * g : 0.0f;
+    // 8 weight loads in flight per thread before their LDS stores (a load -> store loop would
+    // serialise one L2 round trip per iteration)
+    for (int i0 = 0; i0 < C * a.Mpad; i0 += 8 * PW_THREADS) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * PW_THREADS + tid;
+            const int c = i / a.Mpad, o = i - c * a.Mpad;
+            v[u] = 0.0f;
+            if (i < C * a.Mpad && o < M)
+                v[u] = a.w[(size_t)o * C + c] * (a.gate ? a.gate[(size_t)b * C + c] : 1.0f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = i0 + u * PW_THREADS + tid;
+            if (i < C * a.Mpad) Wg[i] = v[u];
+        }
     }
     __syncthreads();
 

@@ -115,6 +115,7 @@ class _FFCExec:
         outs = {"l": 0, "g": 0}
         execs, jobs, post = [], [], []
         jb_name = {}
+        dense = []   # (name, (W (M', C, 1, 1), layout, 1, 1, bias), input, out, act, M')
         for name, segs, w, inp, add, act, bn, M in branches:
             if len(add) > 1:
                 raise NotImplementedError("more than one identity pass-through in a branch")
@@ -135,6 +136,13 @@ class _FFCExec:
             out_shape = None
             if addend is None and bn is None:
                 rw = self._outer_rewrite(segs, w, M)
+                if rw is not None and len(segs) == 1:
+                    # a plain GEMM: batched with the other branch's into one dense launch below
+                    segs2, w2, M2, chw = rw
+                    out = torch.empty((B,) + chw, device=dev, dtype=torch.float32)
+                    outs[name] = out
+                    dense.append((name, w2[0], inp[0][0], out, act, M2))
+                    continue
                 if rw is not None:
                     segs, w, M, chw = rw
                     out_shape = (B,) + chw
@@ -152,6 +160,8 @@ class _FFCExec:
             jb_name[id(out)] = name
             execs.append(ex)
             jobs.append((ex, inp, out, act, bn, addend))
+        if dense:
+            self._launch_dense(dense, B, stream)
         groups = {}
         for jb in jobs:
             groups.setdefault(jb[0].launch_key, []).append(jb)
@@ -221,6 +231,41 @@ class _FFCExec:
             segs2.append(_plan.Seg("pw", sg.C, 1, 1))
             w2.append((hit[0], 0, 1, 1, hit[1]))
         return segs2, w2, M * k * k, (M, k, k)
+
+    def _launch_dense(self, dense, B, stream):
+        """outer-product branches (ConvT on a 1x1 input) as ffc_dense_forward launches; two branches with
+        the same input and activation share one launch (their weights concatenated along N, cached)"""
+        cache = self._ffc_cache()
+        groups = []
+        for d in dense:
+            for g in groups:
+                if len(g) == 1 and g[0][2].data_ptr() == d[2].data_ptr() and g[0][4] == d[4]:
+                    g.append(d)
+                    break
+            else:
+                groups.append([d])
+        for g in groups:
+            wts = [d[1] for d in g]
+            key = ("dense",) + tuple((wt[0].data_ptr(), wt[0]._version,
+                                      None if wt[4] is None else (wt[4].data_ptr(), wt[4]._version)) for wt in wts)
+            hit = cache.get(key)
+            if hit is None:
+                for old in [kk for kk in cache if kk[0] == "dense" and kk[1][0] == key[1][0]]:
+                    del cache[old]
+                Wt = torch.cat([wt[0].reshape(wt[0].shape[0], -1).t() for wt in wts], dim=1).contiguous()
+                has_b = any(wt[4] is not None for wt in wts)
+                bias = torch.cat([wt[4] if wt[4] is not None else torch.zeros(wt[0].shape[0], device=Wt.device)
+                                  for wt in wts]).contiguous() if has_b else None
+                hit = cache[key] = (Wt, bias)
+            Wt, bias = hit
+            x = g[0][2]
+            K, N = Wt.shape
+            N0 = g[0][5]
+            act = g[0][4]
+            with rt.observe("dense", flops=2.0 * B * K * N):
+                rt.check(rt.lib().ffc_dense_forward(x.data_ptr(), Wt.data_ptr(), rt.ptr(bias), B, K, N, N0,
+                                                    g[0][3].data_ptr(), rt.ptr(g[1][3]) if len(g) > 1 else None,
+                                                    act[0], act[1], stream), "ffc_dense_forward")
 
     @staticmethod
     def _smallm_kind(segs, w, addend, bn, M):

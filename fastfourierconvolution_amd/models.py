@@ -11,7 +11,6 @@ import os
 import torch
 import torch.nn as nn
 
-from . import _plan
 from . import _runtime as rt
 from ._lib import check, ptr
 from .config import Config
@@ -155,7 +154,7 @@ class FGenerator(FFCModel):
         self._lin = {}
 
     def _noise_to_feature(self, z):
-        """nn.Linear(z_size, 16*1024) on the HIP GEMM: a 1x1 'convolution' of (B, z, 1, 1)"""
+        """nn.Linear(z_size, 16*1024) (fgan128_complete.py:453-455) on the HIP dense GEMM"""
         lin = self.noise_to_feature[0]
         z = rt.require(z, "z")
         if z.dim() != 2 or z.shape[1] != lin.in_features:
@@ -163,16 +162,16 @@ class FGenerator(FFCModel):
         B = z.shape[0]
         w = rt.require(lin.weight.detach(), "noise_to_feature.0.weight")
         b = rt.require(lin.bias.detach(), "noise_to_feature.0.bias") if lin.bias is not None else None
-        wt = (w, 0, 1, 1, b)
-        key = (B, str(z.device))
-        ex = self._lin.get(key)
-        if ex is None:
-            e = rt.ConvExec(B, lin.out_features, [_plan.Seg("pw", lin.in_features, 1, 1)], [wt], z.device)
-            ex = self._lin[key] = (e, rt.LaunchPlan([e], z.device))
-        e, lp = ex
-        e.ensure_packed([wt])
-        out = torch.empty((B, lin.out_features, 1, 1), device=z.device, dtype=torch.float32)
-        lp.launch([e.job([(z.view(B, -1, 1, 1), None)], out)], rt.stream_of(z), flops=e.flops)
+        key = (w.data_ptr(), w._version)
+        if self._lin.get("key") != key:
+            self._lin["Wt"] = w.t().contiguous()
+            self._lin["key"] = key
+        Wt = self._lin["Wt"]
+        out = torch.empty((B, lin.out_features), device=z.device, dtype=torch.float32)
+        with rt.observe("dense", flops=2.0 * B * lin.in_features * lin.out_features):
+            check(rt.lib().ffc_dense_forward(ptr(z), ptr(Wt), ptr(b), B, lin.in_features, lin.out_features,
+                                             lin.out_features, ptr(out), None, 0, 0.0, rt.stream_of(z)),
+                  "ffc_dense_forward")
         return out.view(B, -1, self.mg, self.mg)
 
     def forward_float(self, z, noises=None):

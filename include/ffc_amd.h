@@ -155,6 +155,13 @@ int ffc_conv_pack(const ffc_conv_job* job, const float* const* seg_weight, const
                   const int* kh, const int* kw, const float* const* seg_bias,
                   float* A_out, float* bias_out, void* stream);
 
+/* Dense GEMM + bias + activation: out[b][n] = act(sum_k A[b][k] Wt[k][n] + bias[n]), A (B, K),
+ * Wt (K, N) row-major, K <= 256.  Columns [0, N0) go to out0 (B, N0), [N0, N) to out1 (B, N - N0).
+ * Replaces ConvTranspose2d(k, 1, 0) on a 1x1 input (ffc_transpose.py:79-86 in the generator's first
+ * layer, models/ffc_generator.py:24: n = (m, ky, kx)) and nn.Linear (fgan128_complete.py:453-455). */
+int ffc_dense_forward(const float* A, const float* Wt, const float* bias, int B, int K, int N, int N0,
+                      float* out0, float* out1, int act, float act_param, void* stream);
+
 /* ------------------------------------------------------------------ batch norm
  * nn.BatchNorm2d semantics (train: biased var normalises, unbiased var -> running_var,
  * num_batches_tracked += 1, momentum<0 means cumulative average; eval: running stats).
