@@ -24,6 +24,7 @@
 // mix reads the 4x smaller T, so HBM carries: r2c t + T, mix T (+ Y), c2r Y + t + out.
 #include "ffc_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <set>
@@ -112,16 +113,22 @@ __device__ __forceinline__ void line_fft(float2* line, int stride, int jj) {
 }
 
 // Column pass over an (rows x ZS) float2 plane: length-`rows` FFTs of columns 0..ncols-1.
-template <int ROWS, bool INV>
+template <int ROWS, bool INV, int NT = FU2_THREADS>
 __device__ __forceinline__ void column_pass(float2* Z, int ZS, int ncols, int tid) {
     constexpr int N1 = Split<ROWS>::N1;
-    constexpr int LPR = FU2_THREADS / N1;   // lines per round
+    constexpr int LPR = NT / N1;   // lines per round
     const int jj = tid % N1;
     for (int c0 = 0; c0 < ncols; c0 += LPR) {
         const int col = c0 + tid / N1;
         if (col < ncols) line_fft<ROWS, INV>(Z + col, ZS, jj);
     }
 }
+
+// LDS row stride (float2) of a half-spectrum plane with WP = W/2+1 columns: WP rounded up to 4 mod 8,
+// so the 8 lanes x 8 adjacent columns of a wave in the column pass (row stride * jj + column) and
+// the 8 row pairs x 8 lanes of the row pass spread over the 64 banks (the unpadded odd stride put
+// a wave on ~15 bank pairs).
+constexpr int zstride(int WP) { return ((WP + 3) & ~7) + 4; }
 
 __device__ __forceinline__ float in_tf(float v, float sc, float sh, int relu) {
     v = fmaf(v, sc, sh);
@@ -141,6 +148,7 @@ struct R2cArgs {
 template <int h, int w>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     constexpr int WPt = w / 2 + 1;
+    constexpr int ZS = zstride(WPt);
     constexpr int RS = w + 4;
     constexpr int N1 = Split<w>::N1, N2 = Split<w>::N2, Q = Split<w>::Q;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -190,7 +198,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
                     im[m] = R[(2 * g + 1) * RS + jj + N1 * m];
                 }
                 stage_a<w, false>(re, im, jj);
-                float2* line = Z + 2 * g * WPt;   // rows 2g, 2g+1 of Z: 2*WPt >= w slots
+                float2* line = Z + 2 * g * ZS;    // rows 2g, 2g+1 of Z: 2*ZS >= w slots
                 float ore[Q][N1], oim[Q][N1];
                 stage_b<w, false>(line, 1, re, im, jj, ore, oim);
 #pragma unroll
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
                     const int k = jj + N1 * i;
                     if (k < WPt) {
                         line[k] = make_float2(0.5f * (zk[i].x + zm[i].x), 0.5f * (zk[i].y - zm[i].y));
-                        line[WPt + k] = make_float2(0.5f * (zk[i].y + zm[i].y), -0.5f * (zk[i].x - zm[i].x));
+                        line[ZS + k] = make_float2(0.5f * (zk[i].y + zm[i].y), -0.5f * (zk[i].x - zm[i].x));
                     }
                 }
             }
@@ -223,13 +231,15 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     __syncthreads();
 
     // 3. columns (length h) of the half spectrum
-    column_pass<h, false>(Z, WPt, WPt, tid);
+    column_pass<h, false>(Z, ZS, WPt, tid);
     __syncthreads();
 
-    // 4. Z -> T (contiguous h x WPt float2; h even so the plane is whole float4s)
-    float4* dst = reinterpret_cast<float4*>(a.T + (size_t)plane * h * WPt * 2);
-    const float4* zs = reinterpret_cast<const float4*>(Z);
-    for (int i = tid; i < h * WPt / 2; i += FU2_THREADS) dst[i] = zs[i];
+    // 4. Z -> T (contiguous h x WPt float2)
+    float2* dst = reinterpret_cast<float2*>(a.T) + (size_t)plane * h * WPt;
+    for (int i = tid; i < h * WPt; i += FU2_THREADS) {
+        const int r = i / WPt, k = i - r * WPt;
+        dst[i] = Z[r * ZS + k];
+    }
 }
 
 // ---------------------------------------------------------------- stage 3: C2R + residual
@@ -246,6 +256,7 @@ struct C2rArgs {
 template <int H, int W, int UP>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     constexpr int WP = W / 2 + 1;
+    constexpr int ZS = zstride(WP);
     constexpr int N1 = Split<W>::N1, N2 = Split<W>::N2, Q = Split<W>::Q;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float2* Z = reinterpret_cast<float2*>(smem);
@@ -253,12 +264,32 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     const int ch = plane % a.C;
     const int tid = threadIdx.x;
 
-    // 1. Y plane -> LDS by LDS-DMA (H*WP float2 = H*WP/2 16-byte groups)
-    ffc::dma_copy16(a.Y + (size_t)plane * H * WP * 2, smem, H * WP / 2, tid, FU2_THREADS);
+    // 1. Y plane -> LDS rows of stride ZS (16 float2 loads in flight per thread per batch)
+    {
+        const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)plane * H * WP;
+        for (int i0 = 0; i0 < H * WP; i0 += 16 * FU2_THREADS) {
+            float2 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * FU2_THREADS + tid;
+                if (i < H * WP) v[u] = src[i];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * FU2_THREADS + tid;
+                if (i < H * WP) {
+                    const int r = i / WP, k = i - r * WP;
+                    Z[r * ZS + k] = v[u];
+                }
+            }
+        }
+    }
     __syncthreads();
 
     // 2. inverse columns (length H)
-    column_pass<H, true>(Z, WP, WP, tid);
+#ifndef FFC_C2R_SKIP_COL   // timing probes only (tools/build_variant.sh): results are wrong without it
+    column_pass<H, true>(Z, ZS, WP, tid);
+#endif
     __syncthreads();
 
     // 3. rows two at a time: z[k] = A_ext[k] + i B_ext[k] (Hermitian extension of each half
@@ -274,8 +305,8 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
         for (int g0 = 0; g0 < H / 2; g0 += LPR) {
             const int g = g0 + tid / N1;
             if (g < H / 2) {
-                float2* ra = Z + 2 * g * WP;
-                float2* rb = ra + WP;
+                float2* ra = Z + 2 * g * ZS;
+                float2* rb = ra + ZS;
                 float re[N2], im[N2];
 #pragma unroll
                 for (int m = 0; m < N2; ++m) {
@@ -297,10 +328,18 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                     re[m] = A.x - B.y;
                     im[m] = A.y + B.x;
                 }
+#ifndef FFC_C2R_SKIP_ROW
                 stage_a<W, true>(re, im, jj);
                 float ore[Q][N1], oim[Q][N1];
                 stage_b<W, true>(ra, 1, re, im, jj, ore, oim);
-                float* fa = reinterpret_cast<float*>(ra);   // 4*WP >= 2W floats: row 2g then row 2g+1
+#else
+                float ore[Q][N1], oim[Q][N1];
+#pragma unroll
+                for (int q = 0; q < Q; ++q)
+#pragma unroll
+                    for (int k1 = 0; k1 < N1; ++k1) { ore[q][k1] = re[q * N1 + k1]; oim[q][k1] = im[q * N1 + k1]; }
+#endif
+                float* fa = reinterpret_cast<float*>(ra);   // 4*ZS >= 2W floats: row 2g then row 2g+1
 #pragma unroll
                 for (int q = 0; q < Q; ++q)
 #pragma unroll
@@ -359,12 +398,14 @@ struct MixArgs {
     float norm;
 };
 
-constexpr int MIX_TILES_PER_WG = 8;
+constexpr int MIX_TILES_PER_WG = 32;   // 8 per wave: amortises the weight staging
 
-template <int MT, int PASS>
+// CC: compile-time channel count (0: runtime a.C) -- with it the k-loop unrolls fully and all C
+// gathered B loads of a tile are issued before its MFMAs
+template <int MT, int PASS, int CC = 0>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int C = a.C, C2 = 2 * C;
+    const int C = CC ? CC : a.C, C2 = 2 * C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hh = lane >> 5, col = lane & 31;
     // sample-major within an XCD: consecutive ids go to consecutive XCDs, so b = id % B keeps a
@@ -396,14 +437,24 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) st_n[mt] = st_mean[mt] = st_m2[mt] = 0.0f;
 
-    for (int tile = t_lo + wave; tile < t_hi; tile += FU2_THREADS / 64) {
+    // compile-time C with C*MT <= 64: the wave's A fragments live in registers for all its tiles
+    constexpr bool AREG = CC > 0 && CC * MT <= 64;
+    float areg[AREG ? CC : 1][MT];
+    if constexpr (AREG) {
+#pragma unroll
+        for (int s = 0; s < CC; ++s)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) areg[s][mt] = Wm[(2 * s + hh) * a.Mpad + mt * 32 + col];
+    }
+
+    // this lane's bin of a tile: source index in T, conjugation, and factor f = X / T
+    auto binp = [&](int tile, int& idx, bool& cj, float& fr, float& fi) {
         const int n = tile * 32 + col;
-        const bool valid = n < NB;
-        // this lane's bin: source index in T, conjugation, and factor f = X / T
-        int idx = 0;
-        bool cj = false;
-        float fr = 0.0f, fi = 0.0f;
-        if (valid) {
+        idx = 0;
+        cj = false;
+        fr = 0.0f;
+        fi = 0.0f;
+        if (n < NB) {
             const int kh = n / WP, kw = n - kh * WP;
             if (a.up == 1) {
                 idx = n;
@@ -422,31 +473,67 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
                 fi = (c1 * s2 + s1 * c2) * a.norm;
             }
         }
+    };
+    for (int tile = t_lo + wave; tile < t_hi; tile += FU2_THREADS / 64) {
+        const int n = tile * 32 + col;
+        const bool valid = n < NB;
         floatx16 acc[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mt][r] = 0.0f;
-        const float2* tp = Tb + idx;
-        for (int s0 = 0; s0 < C; s0 += 8) {
-            float z[8];
+        if constexpr (CC > 0) {
+            // all C gathered loads of the tile issued before its MFMAs (a register prefetch of the next
+            // tile measured slower: 276 VGPRs, one wave per SIMD)
+            int idx;
+            bool cj;
+            float fr, fi;
+            binp(tile, idx, cj, fr, fi);
+            float2 tv[CC];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                float2 tv = make_float2(0.0f, 0.0f);
-                if (s0 + u < C) tv = tp[(size_t)(s0 + u) * planeT];
-                if (cj) tv.y = -tv.y;
-                const float xr = tv.x * fr - tv.y * fi;
-                const float xi = tv.x * fi + tv.y * fr;
-                z[u] = hh ? xi : xr;
-            }
+            for (int s = 0; s < CC; ++s) tv[s] = Tb[idx + (size_t)s * planeT];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int s = s0 + u;
-                if (s < C) {
+            for (int s = 0; s < CC; ++s) {
+                float2 t2 = tv[s];
+                if (cj) t2.y = -t2.y;
+                const float z = hh ? (t2.x * fi + t2.y * fr) : (t2.x * fr - t2.y * fi);
+                if constexpr (AREG) {
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(areg[s][mt], z, acc[mt], 0, 0, 0);
+                } else {
                     const float* wr = Wm + (2 * s + hh) * a.Mpad + col;
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt)
-                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z[u], acc[mt], 0, 0, 0);
+                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z, acc[mt], 0, 0, 0);
+                }
+            }
+        } else {
+            int idx;
+            bool cj;
+            float fr, fi;
+            binp(tile, idx, cj, fr, fi);
+            const float2* tp = Tb + idx;
+            for (int s0 = 0; s0 < C; s0 += 8) {
+                float z[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    float2 tv = make_float2(0.0f, 0.0f);
+                    if (s0 + u < C) tv = tp[(size_t)(s0 + u) * planeT];
+                    if (cj) tv.y = -tv.y;
+                    const float xr = tv.x * fr - tv.y * fi;
+                    const float xi = tv.x * fi + tv.y * fr;
+                    z[u] = hh ? xi : xr;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int s = s0 + u;
+                    if (s < C) {
+                        const float* wr = Wm + (2 * s + hh) * a.Mpad + col;
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z[u], acc[mt], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -541,17 +628,16 @@ C2rKernel pick_c2r(int H, int W, int up) {
 
 MixKernel pick_mix(int C, int pass) {
     const int C2 = 2 * C;
+    if (C == 32) return pass ? fu2d_mix_kernel<2, 1, 32> : fu2d_mix_kernel<2, 0, 32>;   // fgan128 64^2 / 128^2
+    if (C == 16) return pass ? fu2d_mix_kernel<1, 1, 16> : fu2d_mix_kernel<1, 0, 16>;
     if (C2 <= 32) return pass ? fu2d_mix_kernel<1, 1> : fu2d_mix_kernel<1, 0>;
     if (C2 <= 64) return pass ? fu2d_mix_kernel<2, 1> : fu2d_mix_kernel<2, 0>;
     if (C2 <= 128) return pass ? fu2d_mix_kernel<4, 1> : fu2d_mix_kernel<4, 0>;
     return nullptr;
 }
 
-size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * (w / 2 + 1) * 8; }
-size_t c2r_lds(int H, int W) {
-    const size_t n4 = (size_t)H * (W / 2 + 1) / 2;           // 16-byte DMA groups
-    return ((n4 + 63) / 64 * 64) * 16;                        // whole 64-lane DMA instructions
-}
+size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * zstride(w / 2 + 1) * 8; }
+size_t c2r_lds(int H, int W) { return (size_t)H * zstride(W / 2 + 1) * 8; }
 size_t mix_wm_floats(int C) { return (size_t)(2 * C) * ((2 * C + 31) / 32 * 32); }
 size_t mix_lds(int C, int pass) {
     const size_t wm = (mix_wm_floats(C) + 255) / 256 * 256;   // <= 64 KiB for 2C <= 128
@@ -578,7 +664,7 @@ int raise_lds(const void* k, size_t lds, const char* what) {
 // (>= ~1024) to fill the chip when the batch is small, down to one tile per workgroup
 int mix_nsplit(int B, int H, int W) {
     const int ntiles = (H * (W / 2 + 1) + 31) / 32;
-    const int fill = (1024 + B - 1) / B;
+    const int fill = (512 + B - 1) / B;
     return std::max(1, std::min(ntiles, std::max(ntiles / MIX_TILES_PER_WG, fill)));
 }
 
@@ -656,12 +742,12 @@ extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const fl
     FFC_CHECK_ARG(!residual || t, "ffc_fu2d_c2r: residual needs t");
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu2d_c2r: up must be 1 or 2");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
+    C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W))};
     C2rKernel k = pick_c2r(H, W, up);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [16, 128])");
     const size_t lds = c2r_lds(H, W);
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_c2r");
     if (rc) return rc;
-    C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W))};
     hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r");
 }
