@@ -43,13 +43,17 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["gen64", "fgan128"], default="gen64",
+    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn"], default="gen64",
                    help="gen64: FFCGenerator 64x64 (BASELINE metric, configs[1]/[2]); "
-                        "fgan128: fgan128 FGenerator 128x128x3 (configs[3], per-GPU shard)")
+                        "fgan128: fgan128 FGenerator 128x128x3 (configs[3], 64 per GPU = B 512 / 8); "
+                        "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4], 128 per GPU)")
+    p.add_argument("--mix", choices=["fp32", "fp16"], default=None,
+                   help="spectral mix arithmetic (default: fp16 for fgan128sn, fp32 otherwise)")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=None, help="samples per GPU (gen64: 256, fgan128: 64)")
+    p.add_argument("--batch", type=int, default=None, help="samples per GPU (gen64: 256, fgan128: 64, "
+                                                                     "fgan128sn: 128)")
     p.add_argument("--nz", type=int, default=100)
     p.add_argument("--nc", type=int, default=3)
     p.add_argument("--ngf", type=int, default=64)
@@ -84,38 +88,48 @@ def pmc_traffic(label):
             "source": os.path.relpath(files[-1], ROOT)}
 
 
-def fgan_cpu_baseline(args, G, cpu_state, z_cpu, step):
-    """fgan128: the oracle's fp32 torch-CPU FGenerator (train mode draws its noise on the CPU) on a
-    bounded sample of the batch; parity in eval mode (noise-free) on the same sample."""
-    from oracle.ffc_oracle import fgan128_generator, normwise_err
+def fgan_cpu_baseline(args, G, z_cpu, sn):
+    """fgan128: the oracle's fp32 torch-CPU FGenerator on a bounded sample of the batch (train mode
+    draws its noise on the CPU); parity of the GPU forward against the fp64 oracle in train mode on
+    the same sample with the same explicit NoiseInjection noise (BN batch statistics and, for the SN
+    variant, one power iteration from the same u / v on both sides)."""
+    import torch.nn as nn
+    from oracle.ffc_oracle import fgan128_generator, normwise_err, sn_materialize
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     nb = min(args.batch, 8)
-    training = args.bn_mode == "train"
     zs = z_cpu[:nb]
+    dims = {n: 1 for n, m in G.named_modules() if isinstance(m, nn.ConvTranspose2d)}
+    gen = torch.Generator().manual_seed(7)
 
     def noises():
-        return [(torch.randn(nb, 1, 2 ** (n + 1), 2 ** (n + 1)), torch.randn(nb, 1, 2 ** (n + 1), 2 ** (n + 1)))
-                for n in (2, 3, 4, 5, 6)] if training else None
+        return [(torch.randn((nb, 1, 2 ** (n + 1), 2 ** (n + 1)), generator=gen),
+                 torch.randn((nb, 1, 2 ** (n + 1), 2 ** (n + 1)), generator=gen)) for n in (2, 3, 4, 5, 6)]
+    state = {k: v.detach().cpu().clone() for k, v in G.state_dict().items()}
     with torch.no_grad():
-        sd = {k: v.clone() for k, v in cpu_state.items()}
+        sd = {k: v.clone() for k, v in state.items()}
+        if sn:
+            sn_materialize(sd, dims, True)
         iters, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < args.cpu_seconds or iters == 0:
-            fgan128_generator(zs, sd, training, noises(), fft="torch")
+            fgan128_generator(zs, sd, True, noises(), fft="torch")
             iters += 1
         el = time.perf_counter() - t0
-        # parity: eval mode on the GPU model's running stats
-        G.eval()
-        sd = {k: v.detach().cpu().clone() for k, v in G.state_dict().items()}
-        ref = fgan128_generator(zs.double(), {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()},
-                                False)
-        got = G.forward_float(zs.to(next(G.parameters()).device)).cpu()
-        G.train(training)
+        nz = noises()
+        sd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in state.items()}
+        if sn:
+            sn_materialize(sd, dims, True)
+        ref = fgan128_generator(zs.double(), sd, True, [(a.double(), b.double()) for a, b in nz])
+        G.train()
+        dev = next(G.parameters()).device
+        got = G.forward_float(zs.to(dev), [(a.to(dev), b.to(dev)) for a, b in nz]).cpu()
+        G.train(args.bn_mode == "train")
     cpu = {"value": round(nb * iters / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
-           "sample": f"oracle fp32 torch-CPU fgan128 FGenerator fwd, B={nb} (bounded sample), {iters} iterations "
-                     f"in {el:.1f}s, {args.bn_mode}-mode BN"}
-    parity = {"normwise_err_vs_cpu_ref": normwise_err(got, ref), "mode": "eval (fp64 oracle, same weights/stats)",
-              "tolerance": 1e-4}
+           "sample": f"oracle fp32 torch-CPU fgan128 FGenerator{' + spectral norm' if sn else ''} fwd, B={nb} "
+                     f"(bounded sample), {iters} iterations in {el:.1f}s, train-mode BN"}
+    tol = 1e-2 if args.mix == "fp16" else 1e-4
+    parity = {"normwise_err_vs_cpu_ref": normwise_err(got, ref), "mode": f"train, B={nb}, explicit noise, fp64 oracle",
+              "mix": args.mix, "tolerance": tol}
     return cpu, parity
 
 
@@ -133,8 +147,11 @@ def weights_init(m):
 def main():
     args = parse()
     if args.batch is None:
-        args.batch = 256 if args.workload == "gen64" else 64
-    fgan = args.workload == "fgan128"
+        args.batch = {"gen64": 256, "fgan128": 64, "fgan128sn": 128}[args.workload]
+    fgan = args.workload in ("fgan128", "fgan128sn")
+    sn = args.workload == "fgan128sn"
+    if args.mix is None:
+        args.mix = "fp16" if sn else "fp32"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -151,6 +168,9 @@ def main():
     with contextlib.redirect_stdout(io.StringIO()):
         G = F.FGenerator(128) if fgan else F.FFCGenerator(args.nz, args.nc, args.ngf)
     G.apply(weights_init)
+    if sn:
+        F.spectral_norm_ffc(G)          # SNFFC wrapping of l2l / l2g / g2l + ST conv1 / conv2
+    F.set_mix_precision(G, args.mix)
     cpu_state = {k: v.clone() for k, v in G.state_dict().items()}
     G = G.to(dev).train(args.bn_mode == "train")
     if world > 1:
@@ -244,7 +264,7 @@ def main():
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and fgan:
-        cpu, parity = fgan_cpu_baseline(args, G, cpu_state, z_cpu, step)
+        cpu, parity = fgan_cpu_baseline(args, G, z_cpu, sn)
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.ffc_oracle import ffc_generator, normwise_err
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -273,11 +293,13 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.mix == "fp32" else "f32 (fp16 spectral mix)",
             "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
-            "config": {"workload": ("fgan128 FGenerator(z=128, ngf=128) forward 128x128x3 (float output)" if fgan else
+            "config": {"workload": (f"fgan128 FGenerator(z=128, ngf=128){' + spectral norm (SNFFC)' if sn else ''} "
+                                    "forward 128x128x3 (float output)" if fgan else
                                     f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) forward 64x64x{args.nc}"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch, "bn_mode": args.bn_mode,
+                       "spectral_mix": args.mix,
                        "hipgraph": use_graph, "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and
                                                                           args.bn_mode == "train" else "")},
             "roofline": roof, "fft_roofline": fft_roof, "cpu_baseline": cpu, "parity": parity,

@@ -97,6 +97,9 @@ SIGNATURES = [
     ("ffc_fu2d_r2c", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_fu2d_mix", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                              c_void_p, c_void_p, c_void_p]),
+    ("ffc_fu_pack_mix_f16", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_fu2d_mix_f16", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_void_p]),
     ("ffc_fu2d_c2r", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                              c_int, c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),

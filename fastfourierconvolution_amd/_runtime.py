@@ -397,6 +397,30 @@ class LaunchPlan:
                       "ffc_conv_forward")
 
 
+def sn_refresh(mod):
+    """Run a module's torch.nn.utils.spectral_norm pre-hook (W <- W_orig / sigma, with one power
+    iteration in training mode) at the point where the reference's forward would call the module
+    (layers/snffc/snffc.py:23-33); the HIP path reads module.weight without calling the module.
+    The power iteration stays host-driven PyTorch, as in the reference."""
+    hooks = getattr(mod, "_forward_pre_hooks", None)
+    if not hooks:
+        return
+    from torch.nn.utils.spectral_norm import SpectralNorm
+    for h in hooks.values():
+        if isinstance(h, SpectralNorm):
+            h(mod, None)
+            # keep the normalised weight in one persistent tensor updated in place: its version
+            # changes every refresh, so the packed-weight caches (keyed by pointer + version) repack
+            w = getattr(mod, h.name)
+            buf = mod.__dict__.get("_ffc_sn_" + h.name)
+            if buf is None or buf.shape != w.shape or buf.device != w.device:
+                buf = w.detach().clone()
+                mod.__dict__["_ffc_sn_" + h.name] = buf
+            else:
+                buf.copy_(w.detach())
+            setattr(mod, h.name, buf)
+
+
 def conv_weight(mod):
     """(weight, layout, kh, kw, bias) for nn.Conv2d (layout 0) / nn.ConvTranspose2d (layout 1)."""
     w = mod.weight.detach()

@@ -402,8 +402,14 @@ constexpr int MIX_TILES_PER_WG = 32;   // 8 per wave: amortises the weight stagi
 
 // CC: compile-time channel count (0: runtime a.C) -- with it the k-loop unrolls fully and all C
 // gathered B loads of a tile are issued before its MFMAs
-template <int MT, int PASS, int CC = 0>
+// F16 (config 5, "fp16 MFMA channel-mix"): the weights (a.wmixT -> fp16 [Mpad][2C]) and the rebuilt
+// spectrum are rounded to fp16 and multiplied on v_mfma_f32_32x32x16_f16 with fp32 accumulation;
+// lane (h, r) of k-block kb carries channels 8kb + 4h + 0..3 as (Re, Im) pairs.  Needs CC % 8 == 0.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+template <int MT, int PASS, int CC = 0, bool F16 = false>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
+    static_assert(!F16 || (CC > 0 && CC % 8 == 0), "fp16 mix: compile-time C, multiple of 8");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int C = CC ? CC : a.C, C2 = 2 * C;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -416,9 +422,18 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
     const int t_hi = (int)((long long)(split + 1) * a.ntiles / a.nsplit);
 
     float* Wm = smem;                                         // (2C, Mpad), whole 64-lane DMA groups
-    float* bnss = smem + (C2 * a.Mpad + 255) / 256 * 256;     // pass 1: scale [2C] | shift [2C]
+    float* bnss = F16 ? smem : smem + (C2 * a.Mpad + 255) / 256 * 256;   // pass 1: scale [2C] | shift [2C]
     float* scr = bnss;                                        // pass 0: per-wave tile scratch + merge area
-    ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
+    if constexpr (!F16) ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
+    half8 a16[F16 ? MT : 1][F16 ? CC / 8 : 1];
+    if constexpr (F16) {   // A fragments straight from L2 into registers: W16[o][k], 8 consecutive k
+        const _Float16* W16 = reinterpret_cast<const _Float16*>(a.wmixT);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int kb = 0; kb < CC / 8; ++kb)
+                a16[mt][kb] = *reinterpret_cast<const half8*>(W16 + (size_t)(mt * 32 + col) * C2 + 16 * kb + 8 * hh);
+    }
     if constexpr (PASS == 1) {
         for (int i = tid; i < C2; i += FU2_THREADS) {
             bnss[i] = a.bn_scale[i];
@@ -438,7 +453,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
     for (int mt = 0; mt < MT; ++mt) st_n[mt] = st_mean[mt] = st_m2[mt] = 0.0f;
 
     // compile-time C with C*MT <= 64: the wave's A fragments live in registers for all its tiles
-    constexpr bool AREG = CC > 0 && CC * MT <= 64;
+    constexpr bool AREG = !F16 && CC > 0 && CC * MT <= 64;
     float areg[AREG ? CC : 1][MT];
     if constexpr (AREG) {
 #pragma unroll
@@ -482,7 +497,31 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[mt][r] = 0.0f;
-        if constexpr (CC > 0) {
+        if constexpr (F16) {
+            int idx;
+            bool cj;
+            float fr, fi;
+            binp(tile, idx, cj, fr, fi);
+            float2 tv[CC / 2];   // this lane half's channels 8kb + 4hh + q
+#pragma unroll
+            for (int kb = 0; kb < CC / 8; ++kb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tv[kb * 4 + q] = Tb[idx + (size_t)(8 * kb + 4 * hh + q) * planeT];
+#pragma unroll
+            for (int kb = 0; kb < CC / 8; ++kb) {
+                half8 bz;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float2 t2 = tv[kb * 4 + q];
+                    if (cj) t2.y = -t2.y;
+                    bz[2 * q] = (_Float16)(t2.x * fr - t2.y * fi);
+                    bz[2 * q + 1] = (_Float16)(t2.x * fi + t2.y * fr);
+                }
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a16[mt][kb], bz, acc[mt], 0, 0, 0);
+            }
+        } else if constexpr (CC > 0) {
             // all C gathered loads of the tile issued before its MFMAs (a register prefetch of the next
             // tile measured slower: 276 VGPRs, one wave per SIMD)
             int idx;
@@ -636,11 +675,26 @@ MixKernel pick_mix(int C, int pass) {
     return nullptr;
 }
 
+MixKernel pick_mix16(int C, int pass) {
+    if (C == 16) return pass ? fu2d_mix_kernel<1, 1, 16, true> : fu2d_mix_kernel<1, 0, 16, true>;
+    if (C == 32) return pass ? fu2d_mix_kernel<2, 1, 32, true> : fu2d_mix_kernel<2, 0, 32, true>;
+    if (C == 64) return pass ? fu2d_mix_kernel<4, 1, 64, true> : fu2d_mix_kernel<4, 0, 64, true>;
+    return nullptr;
+}
+
+// fp16 mix weight [Mpad][2C] (row o = output channel, k contiguous), rows >= 2C zero
+__global__ void pack_mix_f16_kernel(const float* __restrict__ w, int C2, int Mpad, _Float16* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Mpad * C2) return;
+    const int o = i / C2;
+    out[i] = o < C2 ? (_Float16)w[i] : (_Float16)0.0f;
+}
+
 size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * zstride(w / 2 + 1) * 8; }
 size_t c2r_lds(int H, int W) { return (size_t)H * zstride(W / 2 + 1) * 8; }
 size_t mix_wm_floats(int C) { return (size_t)(2 * C) * ((2 * C + 31) / 32 * 32); }
-size_t mix_lds(int C, int pass) {
-    const size_t wm = (mix_wm_floats(C) + 255) / 256 * 256;   // <= 64 KiB for 2C <= 128
+size_t mix_lds(int C, int pass, bool f16 = false) {
+    const size_t wm = f16 ? 0 : (mix_wm_floats(C) + 255) / 256 * 256;   // <= 64 KiB for 2C <= 128
     const size_t tail = pass ? 4 * (size_t)C : (size_t)(FU2_THREADS / 64) * ffc::TILE_SCRATCH;
     return 4 * (wm + tail);
 }
@@ -732,6 +786,47 @@ extern "C" int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, 
     if (rc) return rc;
     hipLaunchKernelGGL(k, dim3(B * a.nsplit), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_mix");
+}
+
+extern "C" int ffc_fu_pack_mix_f16(const float* w, int C2, void* w16, void* stream) {
+    FFC_CHECK_ARG(w && w16 && C2 > 0, "ffc_fu_pack_mix_f16: bad args");
+    const int Mpad = (C2 + 31) / 32 * 32;
+    const int n = Mpad * C2;
+    hipLaunchKernelGGL(pack_mix_f16_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, C2, Mpad,
+                       reinterpret_cast<_Float16*>(w16));
+    return ffc::launch_status("ffc_fu_pack_mix_f16");
+}
+
+extern "C" int ffc_fu2d_mix_f16(const float* T, int B, int C, int H, int W, int up, const void* wmix16, int pass,
+                                float* stats_slab, const float* bn_scale, const float* bn_shift, float* Y,
+                                void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_mix_f16: B and C must be positive");
+    FFC_CHECK_ARG(ffc_fu2d_supported(C, H, W, up), "ffc_fu2d_mix_f16: unsupported (C, H, W, up)");
+    FFC_CHECK_ARG(T && wmix16, "ffc_fu2d_mix_f16: null pointer");
+    FFC_CHECK_ARG(pass == 0 || pass == 1, "ffc_fu2d_mix_f16: pass must be 0 or 1");
+    if (pass == 0) FFC_CHECK_ARG(stats_slab != nullptr, "ffc_fu2d_mix_f16: pass 0 needs stats_slab");
+    if (pass == 1) FFC_CHECK_ARG(bn_scale && bn_shift && Y, "ffc_fu2d_mix_f16: pass 1 needs bn_scale/shift/Y");
+    MixKernel k = pick_mix16(C, pass);
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_mix_f16: C must be 16, 32 or 64");
+    MixArgs a;
+    a.T = T;
+    a.wmixT = reinterpret_cast<const float*>(wmix16);
+    a.slab = stats_slab;
+    a.bn_scale = bn_scale;
+    a.bn_shift = bn_shift;
+    a.Y = Y;
+    a.B = B;
+    a.C = C;
+    a.H = H;
+    a.W = W;
+    a.up = up;
+    a.ntiles = (H * (W / 2 + 1) + 31) / 32;
+    a.nsplit = mix_nsplit(B, H, W);
+    a.Mpad = (2 * C + 31) / 32 * 32;
+    a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
+    const size_t lds = mix_lds(C, pass, true);
+    hipLaunchKernelGGL(k, dim3(B * a.nsplit), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu2d_mix_f16");
 }
 
 extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,

@@ -32,6 +32,7 @@ class _FFCExec:
             if isinstance(mod, (nn.Conv2d, nn.ConvTranspose2d)):
                 if not isinstance(inp, torch.Tensor):
                     raise TypeError(f"{type(mod).__name__} got {type(inp).__name__} input")
+                rt.sn_refresh(mod)
                 segs.append(rt.conv_seg(mod, inp))
                 weights.append(rt.conv_weight(mod))
                 inputs.append((inp, None))
@@ -81,6 +82,7 @@ class _FFCExec:
             main.wait_stream(side)
             v.record_stream(main)
             segs, w, inp, add = self._branch([(self.convl2g, x_l)])
+            rt.sn_refresh(self.convg2g.conv2)
             segs.append(_plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]))
             w.append(rt.conv_weight(self.convg2g.conv2))
             inp.append((v, None))
@@ -99,6 +101,7 @@ class _FFCExec:
                         raise TypeError("spectral branch needs a tensor x_g")
                     v = self.convg2g.spectral(x_g)
                     st = self.convg2g
+                    rt.sn_refresh(st.conv2)
                     segs.append(_plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]))
                     w.append(rt.conv_weight(st.conv2))
                     inp.append((v, None))

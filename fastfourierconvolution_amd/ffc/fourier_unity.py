@@ -21,6 +21,9 @@ class FourierUnitSN(nn.Module):
         self.relu = torch.nn.ReLU(inplace=True)
         self._mix_key = None
         self._mixT = None
+        # "fp32" (exact, the reference's arithmetic) or "fp16": fp16 operands on the f16 MFMA with fp32
+        # accumulation (BASELINE config 5); fp16 runs the staged FU (C in {16, 32, 64})
+        self.mix_precision = "fp32"
 
     # ------------------------------------------------------------------ internals
     def _check(self, C):
@@ -49,6 +52,10 @@ class FourierUnitSN(nn.Module):
         L = rt.lib()
         fused = L.ffc_fu_lds_bytes(C, H, W) > 0 and not rt.FORCE_FU2D
         staged_ok = L.ffc_fu2d_supported(C, H, W, up)
+        if self.mix_precision == "fp16":
+            if not (staged_ok and C in (16, 32, 64)):
+                raise NotImplementedError(f"fp16 mix: staged FU with C in {{16, 32, 64}} only; got C={C}, {H}x{W}")
+            fused = False
         if fused and staged_ok and (rt.FU_PATH == "staged" or (rt.FU_PATH == "auto" and B < rt.FU_FUSED_MIN_BATCH)):
             fused = False
         if not fused:
@@ -76,6 +83,16 @@ class FourierUnitSN(nn.Module):
                                  1, None, ptr(sc), ptr(sh), int(residual), ptr(out), stream), "ffc_fu_forward(pass 1)")
         return out
 
+    def _packed_mix16(self, device, stream):
+        w = rt.require(self.conv_layer.weight.detach(), "conv_layer.weight")
+        key = (w.data_ptr(), w._version)
+        if key != self.__dict__.get("_mix16_key"):
+            C2 = w.shape[0]
+            self._mix16 = torch.empty((-(-C2 // 32) * 32, C2), device=device, dtype=torch.float16)
+            check(rt.lib().ffc_fu_pack_mix_f16(ptr(w), C2, ptr(self._mix16), stream), "ffc_fu_pack_mix_f16")
+            self.__dict__["_mix16_key"] = key
+        return self._mix16
+
     def _run2d(self, t, up, in_scale, in_shift, in_relu, residual):
         """large-plane FU: r2c -> mix (pass 0 stats, pass 1 BN/ReLU) -> c2r (include/ffc_amd.h ffc_fu2d_*)"""
         B, C, h, w = t.shape
@@ -83,7 +100,9 @@ class FourierUnitSN(nn.Module):
         L = rt.lib()
         dev = t.device
         stream = rt.stream_of(t)
-        mixT = self._packed_mix(dev, stream)
+        f16 = self.mix_precision == "fp16"
+        mixT = self._packed_mix16(dev, stream) if f16 else self._packed_mix(dev, stream)
+        mixfn = L.ffc_fu2d_mix_f16 if f16 else L.ffc_fu2d_mix
         use_batch, _ = rt.bn_mode(self.bn)
         nT = B * C * h * (w // 2 + 1)           # complex bins of T
         nY = B * C * H * (W // 2 + 1)           # complex bins of Y
@@ -96,14 +115,14 @@ class FourierUnitSN(nn.Module):
             rows = L.ffc_fu2d_slab_rows(B, C, H, W)
             slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
             with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT):
-                check(L.ffc_fu2d_mix(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, None, stream),
+                check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, None, stream),
                       "ffc_fu2d_mix(pass 0)")
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
         else:
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
         Y = torch.empty((B, C, H, W // 2 + 1, 2), device=dev, dtype=torch.float32)
         with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
-            check(L.ffc_fu2d_mix(ptr(T), B, C, H, W, up, ptr(mixT), 1, None, ptr(sc), ptr(sh), ptr(Y), stream),
+            check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 1, None, ptr(sc), ptr(sh), ptr(Y), stream),
                   "ffc_fu2d_mix(pass 1)")
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         with rt.observe("fu2d_c2r", bytes=8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)):

@@ -110,6 +110,7 @@ class SpectralTransform(nn.Module):
         B, Cin, H, W = x.shape
         if Cin != self.conv1.in_channels:
             raise RuntimeError(f"SpectralTransform expected {self.conv1.in_channels} channels, got {Cin}")
+        rt.sn_refresh(self.conv1)
         pool = self.stride == 2 and not self.upsample
         up = 2 if (self.stride == 2 and self.upsample) else 1
         if pool and (H % 2 or W % 2):
@@ -164,6 +165,7 @@ class SpectralTransform(nn.Module):
             raise TypeError("SpectralTransform: the conditional (y) path is not supported (the reference raises "
                             "in FourierUnitSN, fourier_unity.py:46-47)")
         v = self.spectral(x)
+        rt.sn_refresh(self.conv2)
         B, c, H, W = v.shape
         key = ("conv2", B, c, H, W, str(v.device))
         ex = self._cache.get(key)

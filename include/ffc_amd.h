@@ -263,6 +263,12 @@ int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const float* in_sca
                  const float* in_shift, int in_relu, float* T, void* stream);
 int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, const float* wmixT, int pass,
                  float* stats_slab, const float* bn_scale, const float* bn_shift, float* Y, void* stream);
+/* fp16-operand variant of ffc_fu2d_mix (BASELINE config 5 "fp16 MFMA channel-mix"): the spectrum and
+ * the weights are rounded to fp16, products accumulate in fp32 (v_mfma_f32_32x32x16_f16); C in
+ * {16, 32, 64}.  wmix16 from ffc_fu_pack_mix_f16: fp16 [ceil32(2C)][2C] = conv_layer.weight rows. */
+int ffc_fu_pack_mix_f16(const float* w, int C2, void* wmix16, void* stream);
+int ffc_fu2d_mix_f16(const float* T, int B, int C, int H, int W, int up, const void* wmix16, int pass,
+                     float* stats_slab, const float* bn_scale, const float* bn_shift, float* Y, void* stream);
 int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
                  const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
                  void* stream);

@@ -18,6 +18,7 @@ BASELINE.json:north_star (file:line citations into /root/reference):
 * FFCDiscriminator  models/ffc_discriminator.py:18-58
 * NoiseInjection    layers/noise_injection.py:20-32
 * fgan128 FGenerator fgan128_complete.py:442-522 (reconstructed: the script runs main() at import)
+* SNFFC             layers/snffc/snffc.py:12-33 (torch.nn.utils.spectral_norm restated: sn_materialize)
 
 The arithmetic itself lives in the un-vendored third-party dependency PyTorch
 (pinned torch==1.10.2 at requirements.txt:5).  Its published semantics are
@@ -284,6 +285,29 @@ def quantize_u8(fake):
     return (255 * (fake * 0.5 + 0.5)).to(torch.uint8)
 
 
+def sn_materialize(sd, dims, training, n_power_iterations=1, eps=1e-12):
+    """torch.nn.utils.spectral_norm's SpectralNorm.compute_weight (torch/nn/utils/spectral_norm.py,
+    the un-vendored dependency the reference's layers/snffc/*.py call) for every ``<m>.weight_orig``
+    in ``sd``: sd[<m>.weight] = W / sigma, sigma = u . (W_mat v); in training mode one power
+    iteration first updates u and v in place (v = normalize(W_mat^T u), u = normalize(W_mat v)).
+    ``dims[m]``: the reshape dim (0 for Conv2d / Linear, 1 for ConvTranspose2d)."""
+    for key in [k for k in sd if k.endswith(".weight_orig")]:
+        m = key[: -len(".weight_orig")]
+        W = sd[key]
+        d = dims.get(m, 0)
+        Wm = W.permute(d, *[i for i in range(W.dim()) if i != d]).reshape(W.shape[d], -1) if d else \
+            W.reshape(W.shape[0], -1)
+        u, v = sd[m + ".weight_u"], sd[m + ".weight_v"]
+        if training:
+            for _ in range(n_power_iterations):
+                v = F.normalize(torch.mv(Wm.t(), u), dim=0, eps=eps)
+                u = F.normalize(torch.mv(Wm, v), dim=0, eps=eps)
+            sd[m + ".weight_u"], sd[m + ".weight_v"] = u, v
+        sigma = torch.dot(u, torch.mv(Wm, v))
+        sd[m + ".weight"] = W / sigma
+    return sd
+
+
 # ----------------------------------------------------------------------------- fixture driver
 def run_fixture_case(case: dict, state: dict, inputs: dict, dtype=torch.float64, fft="numpy"):
     """Run one golden-manifest case (tests/golden/manifest.json) through the oracle.
@@ -312,6 +336,15 @@ def run_fixture_case(case: dict, state: dict, inputs: dict, dtype=torch.float64,
             out = {"out": ffc_generator(tin["z"], sd, ctor["nz"], ctor["nc"], ctor["ngf"], training, fft)}
         elif kind == "FFCDiscriminator":
             out = {"out": ffc_discriminator(tin["x"], sd, ctor["nc"], ctor["ndf"], training, fft)}
+        elif kind == "SNFFC":
+            sn_materialize(sd, {}, training)
+            x = (tin["x_l"], tin["x_g"]) if "x_l" in tin else tin["x"]
+            ol, og = ffc(x, sd, "", ctor, training, fft)
+            out = {}
+            if not isinstance(ol, int):
+                out["out_l"] = ol
+            if not isinstance(og, int):
+                out["out_g"] = og
         elif kind == "FGenerator":
             noises = [(tin.get(f"noise{n}_l"), tin.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
             out = {"out": fgan128_generator(tin["z"], sd, training, noises, fft=fft)}

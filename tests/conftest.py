@@ -72,7 +72,7 @@ def call_dropin(case, mod, inputs):
         if case["kind"] == "FGenerator":
             noises = [(t.get(f"noise{n}_l"), t.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
             return {"out": mod.forward_float(t["z"], noises if mod.training else None)}
-        if case["kind"] == "FFC_BN_ACT":
+        if case["kind"] in ("FFC_BN_ACT", "SNFFC"):
             x = (t["x_l"], t["x_g"]) if "x_l" in t else t["x"]
             ol, og = mod(x)
             res = {}

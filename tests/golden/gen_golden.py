@@ -55,6 +55,7 @@ def load_reference():
     import layers.noise_injection as ni
     import layers.print_layer as pl
     import layers.resizer as rs
+    import layers.snffc.snffc as snf
     for mod in (fba, fu, st, ni, pl, rs):
         for name in dir(mod):
             if not name.startswith("_"):
@@ -75,7 +76,7 @@ def load_reference():
         FourierUnitSN=fu.FourierUnitSN, SpectralTransform=st.SpectralTransform,
         FFC_BN_ACT=fba.FFC_BN_ACT, FFCGenerator=fg.FFCGenerator,
         FFCDiscriminator=fd.FFCDiscriminator, Resizer=rs.Resizer, NoiseInjection=ni.NoiseInjection,
-        FFCModel=fm.FFCModel)
+        FFCModel=fm.FFCModel, SNFFC=snf.SNFFC)
 
 
 def fgenerator_class(ref):
@@ -128,7 +129,16 @@ def weight_specs(module: nn.Module) -> dict:
     specs = {}
     for mname, m in module.named_modules():
         pre = (mname + ".") if mname else ""
-        if isinstance(m, nn.ConvTranspose2d):
+        if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)) and hasattr(m, "weight_orig"):
+            # torch.nn.utils.spectral_norm: weight_orig + power-iteration vectors u (rows) / v (cols)
+            w = m.weight_orig
+            fan = w[0].numel()
+            specs[pre + "weight_orig"] = [list(w.shape), "normal", 0.0, fan ** -0.5, "float32"]
+            specs[pre + "weight_u"] = [list(m.weight_u.shape), "normal", 0.0, 1.0, "float32"]
+            specs[pre + "weight_v"] = [list(m.weight_v.shape), "normal", 0.0, 1.0, "float32"]
+            if m.bias is not None:
+                specs[pre + "bias"] = [list(m.bias.shape), "normal", 0.0, 0.1, "float32"]
+        elif isinstance(m, nn.ConvTranspose2d):
             i, o, kh, kw = m.weight.shape
             fan = max(1.0, i * kh * kw / float(m.stride[0] * m.stride[1]))
             specs[pre + "weight"] = [list(m.weight.shape), "normal", 0.0, fan ** -0.5, "float32"]
@@ -167,7 +177,7 @@ def load_specs(module, seed, specs):
 def bn_buffers(module):
     out = {}
     for k, v in module.state_dict().items():
-        if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+        if k.endswith(("running_mean", "running_var", "num_batches_tracked", "weight_u", "weight_v")):
             out[k] = v.detach().cpu().numpy()
     return out
 
@@ -253,6 +263,11 @@ def build_cases():
     case("gen_nc3", "FFCGenerator", dict(nz=100, nc=3, ngf=64), {"z": [4, 100, 1, 1]})
     case("gen_nc3_eval", "FFCGenerator", dict(nz=100, nc=3, ngf=64), {"z": [4, 100, 1, 1]}, mode="eval")
     case("disc_nc3", "FFCDiscriminator", dict(nc=3, ndf=64), {"x": [2, 3, 64, 64]})
+    blk = dict(in_channels=32, out_channels=32, kernel_size=3, ratio_gin=0.5, ratio_gout=0.5, stride=1, padding=1)
+    case("snffc_block", "SNFFC", blk, {"x_l": [2, 16, 16, 16], "x_g": [2, 16, 16, 16]},
+         note="layers/snffc/snffc.py: spectral norm, one power iteration (train)")
+    case("snffc_block_eval", "SNFFC", blk, {"x_l": [2, 16, 16, 16], "x_g": [2, 16, 16, 16]}, mode="eval",
+         note="layers/snffc/snffc.py: spectral norm with the stored u, v (eval)")
     noise = {f"noise{n}_{br}": [2, 1, 2 ** (n + 1), 2 ** (n + 1)] for n in (2, 3, 4, 5, 6) for br in "lg"}
     case("fgan128_train", "FGenerator", dict(z_size=128), {"z": [2, 128], **noise},
          note="BASELINE config 4 stack (fgan128_complete.py:442-522), train mode, explicit noise")
@@ -288,7 +303,7 @@ def run_case(ref, c):
         if c["kind"] == "FGenerator":
             noises = [(t.get(f"noise{n}_l"), t.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
             return mod(t["z"], noises)
-        if c["kind"] == "FFC_BN_ACT" and "x_l" in t:
+        if c["kind"] in ("FFC_BN_ACT", "SNFFC") and "x_l" in t:
             return mod((t["x_l"], t["x_g"]))
         return mod(next(iter(t.values())))
 
