@@ -100,6 +100,11 @@ SIGNATURES = [
     ("ffc_fu_pack_mix_f16", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_fu2d_mix_f16", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_void_p]),
+    ("ffc_fu2d_cols_supported", c_int, [c_int, c_int, c_int, c_int, c_int]),
+    ("ffc_fu2d_mix_cols", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
+    ("ffc_fu2d_c2r_rows", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                  c_int, c_void_p, c_void_p]),
     ("ffc_fu2d_c2r", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                              c_int, c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),

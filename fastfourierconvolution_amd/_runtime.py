@@ -231,6 +231,7 @@ FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU a
 # which spread every sample over many workgroups.  "auto" | "fused" | "staged"
 FU_PATH = __import__("os").environ.get("FFC_FU_PATH", "auto")
 FU_FUSED_MIN_BATCH = 128
+FU_COLS = True      # staged FU: inverse column FFT fused into mix pass 1, rows-only C2R (H in 32..128)
 # Run SpectralTransform's kernels on a side stream beside the local-branch GEMM of the same FFC
 # layer ("gemm-first" / "spectral-first": which is issued first).  Off by default: measured on
 # MI355X (B=256 generator) 10-18 % slower than one launch pairing the local and global GEMMs,

@@ -400,13 +400,175 @@ struct MixArgs {
 
 constexpr int MIX_TILES_PER_WG = 32;   // 8 per wave: amortises the weight staging
 
-// CC: compile-time channel count (0: runtime a.C) -- with it the k-loop unrolls fully and all C
-// gathered B loads of a tile are issued before its MFMAs
-// F16 (config 5, "fp16 MFMA channel-mix"): the weights (a.wmixT -> fp16 [Mpad][2C]) and the rebuilt
-// spectrum are rounded to fp16 and multiplied on v_mfma_f32_32x32x16_f16 with fp32 accumulation;
-// lane (h, r) of k-block kb carries channels 8kb + 4h + 0..3 as (Re, Im) pairs.  Needs CC % 8 == 0.
+// Geometry of one sample's spectrum as the mix sees it (rebuilt from T, see the file comment).
+struct MixGeom {
+    const float2* Tb;   // this sample's T
+    size_t planeT;      // complex bins per channel of T
+    int WP, NB, h, w, WPt, up, tstepH, tstepW;
+    float norm;
+};
+
+// source index in T, conjugation and factor f = X / T of flat bin n (zero factor beyond the plane)
+__device__ __forceinline__ void bin_params(const MixGeom& g, int n, int& idx, bool& cj, float& fr, float& fi) {
+    idx = 0;
+    cj = false;
+    fr = 0.0f;
+    fi = 0.0f;
+    if (n < g.NB) {
+        const int kh = n / g.WP, kw = n - kh * g.WP;
+        if (g.up == 1) {
+            idx = n;
+            fr = g.norm;
+        } else {
+            const int khp = kh & (g.h - 1), kwp = kw & (g.w - 1);
+            if (kwp <= g.w / 2) {
+                idx = khp * g.WPt + kwp;
+            } else {
+                idx = ((g.h - khp) & (g.h - 1)) * g.WPt + (g.w - kwp);
+                cj = true;
+            }
+            const float c1 = 1.0f + c_twc[kh * g.tstepH], s1 = -c_tws[kh * g.tstepH];
+            const float c2 = 1.0f + c_twc[kw * g.tstepW], s2 = -c_tws[kw * g.tstepW];
+            fr = (c1 * c2 - s1 * s2) * g.norm;
+            fi = (c1 * s2 + s1 * c2) * g.norm;
+        }
+    }
+}
+
+// F16 (config 5, "fp16 MFMA channel-mix"): the weights (fp16 [Mpad][2C]) and the rebuilt spectrum
+// are rounded to fp16 and multiplied on v_mfma_f32_32x32x16_f16 with fp32 accumulation; lane (h, r)
+// of k-block kb carries channels 8kb + 4h + 0..3 as (Re, Im) pairs.  Needs CC % 8 == 0.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
+// The wave's A operand: fp32 fragments in registers (compile-time C, C*MT <= 64), fp16 fragments in
+// registers (F16), or read from the LDS copy Wm per k-step.
+template <int MT, int CC, bool F16, bool NOAREG = false>
+struct MixA {
+    static constexpr bool AREG = !NOAREG && !F16 && CC > 0 && CC * MT <= 64;
+    float areg[AREG ? CC : 1][MT];
+    half8 a16[F16 ? MT : 1][F16 ? CC / 8 : 1];
+    const float* Wm;
+    int Mpad;
+    __device__ void load(const float* Wm_, const void* wsrc, int Mpad_, int C2, int hh, int col) {
+        Wm = Wm_;
+        Mpad = Mpad_;
+        if constexpr (F16) {   // straight from L2: W16[o][k], 8 consecutive k
+            const _Float16* W16 = reinterpret_cast<const _Float16*>(wsrc);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int kb = 0; kb < CC / 8; ++kb)
+                    a16[mt][kb] = *reinterpret_cast<const half8*>(W16 + (size_t)(mt * 32 + col) * C2 + 16 * kb + 8 * hh);
+        }
+        if constexpr (AREG) {
+#pragma unroll
+            for (int s = 0; s < CC; ++s)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) areg[s][mt] = Wm[(2 * s + hh) * Mpad + mt * 32 + col];
+        }
+    }
+};
+
+// acc[mt] = Wmix[mt rows] . Z[:, bin n of this lane] (Z rebuilt from T on the fly)
+template <int MT, int CC, bool F16, bool NOAREG = false>
+__device__ __forceinline__ void mix_tile(floatx16 (&acc)[MT], const MixGeom& g, const MixA<MT, CC, F16, NOAREG>& A, int n,
+                                         int C, int hh, int col) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mt][r] = 0.0f;
+    int idx;
+    bool cj;
+    float fr, fi;
+    bin_params(g, n, idx, cj, fr, fi);
+    if constexpr (F16) {
+        float2 tv[CC / 2];   // this lane half's channels 8kb + 4hh + q
+#pragma unroll
+        for (int kb = 0; kb < CC / 8; ++kb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tv[kb * 4 + q] = g.Tb[idx + (size_t)(8 * kb + 4 * hh + q) * g.planeT];
+#pragma unroll
+        for (int kb = 0; kb < CC / 8; ++kb) {
+            half8 bz;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float2 t2 = tv[kb * 4 + q];
+                if (cj) t2.y = -t2.y;
+                bz[2 * q] = (_Float16)(t2.x * fr - t2.y * fi);
+                bz[2 * q + 1] = (_Float16)(t2.x * fi + t2.y * fr);
+            }
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+                acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.a16[mt][kb], bz, acc[mt], 0, 0, 0);
+        }
+    } else if constexpr (CC > 0) {
+        // all C gathered loads of the tile issued before its MFMAs (a register prefetch of the next
+        // tile measured slower: 276 VGPRs, one wave per SIMD)
+        float2 tv[CC];
+#pragma unroll
+        for (int s = 0; s < CC; ++s) tv[s] = g.Tb[idx + (size_t)s * g.planeT];
+#pragma unroll
+        for (int s = 0; s < CC; ++s) {
+            float2 t2 = tv[s];
+            if (cj) t2.y = -t2.y;
+            const float z = hh ? (t2.x * fi + t2.y * fr) : (t2.x * fr - t2.y * fi);
+            if constexpr (MixA<MT, CC, F16, NOAREG>::AREG) {
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(A.areg[s][mt], z, acc[mt], 0, 0, 0);
+            } else {
+                const float* wr = A.Wm + (2 * s + hh) * A.Mpad + col;
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z, acc[mt], 0, 0, 0);
+            }
+        }
+    } else {
+        const float2* tp = g.Tb + idx;
+        for (int s0 = 0; s0 < C; s0 += 8) {
+            float z[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                float2 tv = make_float2(0.0f, 0.0f);
+                if (s0 + u < C) tv = tp[(size_t)(s0 + u) * g.planeT];
+                if (cj) tv.y = -tv.y;
+                const float xr = tv.x * fr - tv.y * fi;
+                const float xi = tv.x * fi + tv.y * fr;
+                z[u] = hh ? xi : xr;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int s = s0 + u;
+                if (s < C) {
+                    const float* wr = A.Wm + (2 * s + hh) * A.Mpad + col;
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z[u], acc[mt], 0, 0, 0);
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ MixGeom mix_geom(const MixArgs& a, int b, int C) {
+    MixGeom g;
+    const int H = a.H, W = a.W;
+    g.WP = W / 2 + 1;
+    g.NB = H * g.WP;
+    g.h = H / a.up;
+    g.w = W / a.up;
+    g.WPt = g.w / 2 + 1;
+    g.planeT = (size_t)g.h * g.WPt;
+    g.Tb = reinterpret_cast<const float2*>(a.T) + (size_t)b * C * g.planeT;
+    g.up = a.up;
+    g.tstepH = 128 / H;
+    g.tstepW = 128 / W;
+    g.norm = a.norm;
+    return g;
+}
+
+// CC: compile-time channel count (0: runtime a.C) -- with it the k-loop unrolls fully and all C
+// gathered B loads of a tile are issued before its MFMAs
 template <int MT, int PASS, int CC = 0, bool F16 = false>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
     static_assert(!F16 || (CC > 0 && CC % 8 == 0), "fp16 mix: compile-time C, multiple of 8");
@@ -425,15 +587,6 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
     float* bnss = F16 ? smem : smem + (C2 * a.Mpad + 255) / 256 * 256;   // pass 1: scale [2C] | shift [2C]
     float* scr = bnss;                                        // pass 0: per-wave tile scratch + merge area
     if constexpr (!F16) ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
-    half8 a16[F16 ? MT : 1][F16 ? CC / 8 : 1];
-    if constexpr (F16) {   // A fragments straight from L2 into registers: W16[o][k], 8 consecutive k
-        const _Float16* W16 = reinterpret_cast<const _Float16*>(a.wmixT);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int kb = 0; kb < CC / 8; ++kb)
-                a16[mt][kb] = *reinterpret_cast<const half8*>(W16 + (size_t)(mt * 32 + col) * C2 + 16 * kb + 8 * hh);
-    }
     if constexpr (PASS == 1) {
         for (int i = tid; i < C2; i += FU2_THREADS) {
             bnss[i] = a.bn_scale[i];
@@ -441,141 +594,20 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
         }
     }
     __syncthreads();
-
-    const int H = a.H, W = a.W, WP = W / 2 + 1, NB = H * WP;
-    const int h = H / a.up, w = W / a.up, WPt = w / 2 + 1;
-    const size_t planeT = (size_t)h * WPt;
-    const float2* Tb = reinterpret_cast<const float2*>(a.T) + (size_t)b * C * planeT;
-    const int tstepH = 128 / H, tstepW = 128 / W;
+    MixA<MT, CC, F16> A;
+    A.load(Wm, a.wmixT, a.Mpad, C2, hh, col);
+    const MixGeom g = mix_geom(a, b, C);
+    const int NB = g.NB;
 
     float st_n[MT], st_mean[MT], st_m2[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) st_n[mt] = st_mean[mt] = st_m2[mt] = 0.0f;
 
-    // compile-time C with C*MT <= 64: the wave's A fragments live in registers for all its tiles
-    constexpr bool AREG = !F16 && CC > 0 && CC * MT <= 64;
-    float areg[AREG ? CC : 1][MT];
-    if constexpr (AREG) {
-#pragma unroll
-        for (int s = 0; s < CC; ++s)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) areg[s][mt] = Wm[(2 * s + hh) * a.Mpad + mt * 32 + col];
-    }
-
-    // this lane's bin of a tile: source index in T, conjugation, and factor f = X / T
-    auto binp = [&](int tile, int& idx, bool& cj, float& fr, float& fi) {
-        const int n = tile * 32 + col;
-        idx = 0;
-        cj = false;
-        fr = 0.0f;
-        fi = 0.0f;
-        if (n < NB) {
-            const int kh = n / WP, kw = n - kh * WP;
-            if (a.up == 1) {
-                idx = n;
-                fr = a.norm;
-            } else {
-                const int khp = kh & (h - 1), kwp = kw & (w - 1);
-                if (kwp <= w / 2) {
-                    idx = khp * WPt + kwp;
-                } else {
-                    idx = ((h - khp) & (h - 1)) * WPt + (w - kwp);
-                    cj = true;
-                }
-                const float c1 = 1.0f + c_twc[kh * tstepH], s1 = -c_tws[kh * tstepH];
-                const float c2 = 1.0f + c_twc[kw * tstepW], s2 = -c_tws[kw * tstepW];
-                fr = (c1 * c2 - s1 * s2) * a.norm;
-                fi = (c1 * s2 + s1 * c2) * a.norm;
-            }
-        }
-    };
     for (int tile = t_lo + wave; tile < t_hi; tile += FU2_THREADS / 64) {
         const int n = tile * 32 + col;
         const bool valid = n < NB;
         floatx16 acc[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[mt][r] = 0.0f;
-        if constexpr (F16) {
-            int idx;
-            bool cj;
-            float fr, fi;
-            binp(tile, idx, cj, fr, fi);
-            float2 tv[CC / 2];   // this lane half's channels 8kb + 4hh + q
-#pragma unroll
-            for (int kb = 0; kb < CC / 8; ++kb)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) tv[kb * 4 + q] = Tb[idx + (size_t)(8 * kb + 4 * hh + q) * planeT];
-#pragma unroll
-            for (int kb = 0; kb < CC / 8; ++kb) {
-                half8 bz;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    float2 t2 = tv[kb * 4 + q];
-                    if (cj) t2.y = -t2.y;
-                    bz[2 * q] = (_Float16)(t2.x * fr - t2.y * fi);
-                    bz[2 * q + 1] = (_Float16)(t2.x * fi + t2.y * fr);
-                }
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a16[mt][kb], bz, acc[mt], 0, 0, 0);
-            }
-        } else if constexpr (CC > 0) {
-            // all C gathered loads of the tile issued before its MFMAs (a register prefetch of the next
-            // tile measured slower: 276 VGPRs, one wave per SIMD)
-            int idx;
-            bool cj;
-            float fr, fi;
-            binp(tile, idx, cj, fr, fi);
-            float2 tv[CC];
-#pragma unroll
-            for (int s = 0; s < CC; ++s) tv[s] = Tb[idx + (size_t)s * planeT];
-#pragma unroll
-            for (int s = 0; s < CC; ++s) {
-                float2 t2 = tv[s];
-                if (cj) t2.y = -t2.y;
-                const float z = hh ? (t2.x * fi + t2.y * fr) : (t2.x * fr - t2.y * fi);
-                if constexpr (AREG) {
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(areg[s][mt], z, acc[mt], 0, 0, 0);
-                } else {
-                    const float* wr = Wm + (2 * s + hh) * a.Mpad + col;
-#pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-                        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z, acc[mt], 0, 0, 0);
-                }
-            }
-        } else {
-            int idx;
-            bool cj;
-            float fr, fi;
-            binp(tile, idx, cj, fr, fi);
-            const float2* tp = Tb + idx;
-            for (int s0 = 0; s0 < C; s0 += 8) {
-                float z[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    float2 tv = make_float2(0.0f, 0.0f);
-                    if (s0 + u < C) tv = tp[(size_t)(s0 + u) * planeT];
-                    if (cj) tv.y = -tv.y;
-                    const float xr = tv.x * fr - tv.y * fi;
-                    const float xi = tv.x * fi + tv.y * fr;
-                    z[u] = hh ? xi : xr;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int s = s0 + u;
-                    if (s < C) {
-                        const float* wr = Wm + (2 * s + hh) * a.Mpad + col;
-#pragma unroll
-                        for (int mt = 0; mt < MT; ++mt)
-                            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(wr[mt * 32], z[u], acc[mt], 0, 0, 0);
-                    }
-                }
-            }
-        }
+        mix_tile<MT, CC, F16>(acc, g, A, n, C, hh, col);
         if constexpr (PASS == 0) {
             const int nv = min(32, NB - tile * 32);
 #pragma unroll
@@ -628,6 +660,193 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
                 }
             }
             reinterpret_cast<float4*>(a.slab)[(size_t)blockIdx.x * C2 + o] = make_float4(nn, mean, m2, 0.0f);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- pass 1 + inverse column FFT
+// Mix pass 1 for HC = H in {32, 64, 128} with the C2R's inverse column FFT fused in: a workgroup
+// owns whole spectral columns (CPW = 128 / HC columns, TPC = HC / 32 bin tiles each, one tile per
+// wave), so after BN + ReLU the columns are in LDS and the length-HC inverse FFTs run there -- VALU /
+// LDS work beside the MFMA-bound mix -- and the column-transformed spectrum goes out column-major
+// Yc (B, C, W/2+1, H).  The C2R that follows is then rows only (fu2d_c2r_rows_kernel).
+template <int MT, int CC, bool F16, int HC>
+__global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_cols_kernel(MixArgs a) {
+    static_assert(CC > 0 && HC >= 32 && HC <= 128, "column-fused mix: compile-time C, H in [32, 128]");
+    constexpr int TPC = HC / 32, CPW = 4 / TPC, LS = HC + 4;   // LS: padded column stride (float2)
+    constexpr int C = CC, C2 = 2 * CC;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hh = lane >> 5, col = lane & 31;
+    const int b = blockIdx.x % a.B, cg0 = blockIdx.x / a.B, gstride = a.nsplit;   // nsplit: workgroups per sample
+    const int wfl = F16 ? 0 : (C2 * a.Mpad + 255) / 256 * 256;
+    float* Wm = smem;
+    float* bnss = smem + wfl;                                         // scale [2C] | shift [2C]
+    float2* Ycol = reinterpret_cast<float2*>(smem + wfl + 4 * C);     // [C][CPW][LS]
+    if constexpr (!F16) ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
+    for (int i = tid; i < C2; i += FU2_THREADS) {
+        bnss[i] = a.bn_scale[i];
+        bnss[C2 + i] = a.bn_shift[i];
+    }
+    __syncthreads();
+    MixA<MT, CC, F16> A;
+    A.load(Wm, a.wmixT, a.Mpad, C2, hh, col);
+    const MixGeom g = mix_geom(a, b, C);
+    const int cs = wave / TPC, kb = wave % TPC;
+    const int ncg = (g.WP + CPW - 1) / CPW;
+    constexpr int N1 = Split<HC>::N1;
+    const int jj = tid % N1;
+    float2* Yc = reinterpret_cast<float2*>(a.Y);
+    // column groups cg0, cg0 + gstride, ...: the weight staging above is paid once per workgroup
+    for (int cg = cg0; cg < ncg; cg += gstride) {
+        const int kw = cg * CPW + cs, kh = kb * 32 + col;
+        const bool kwv = kw < g.WP;
+        floatx16 acc[MT];
+        mix_tile<MT, CC, F16>(acc, g, A, kwv ? kh * g.WP + kw : g.NB, C, hh, col);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even: Re, o+1: Im
+                if (o < C2) {
+                    const float re = fmaxf(fmaf(acc[mt][r], bnss[o], bnss[C2 + o]), 0.0f);
+                    const float im = fmaxf(fmaf(acc[mt][r + 1], bnss[o + 1], bnss[C2 + o + 1]), 0.0f);
+                    Ycol[((o >> 1) * CPW + cs) * LS + kh] = make_float2(re, im);
+                }
+            }
+        __syncthreads();
+        for (int l0 = 0; l0 < C * CPW; l0 += FU2_THREADS / N1) {   // inverse column FFTs (length HC)
+            const int line = l0 + tid / N1;
+            if (line < C * CPW) line_fft<HC, true>(Ycol + line * LS, 1, jj);
+        }
+        __syncthreads();
+        for (int i = tid; i < C * CPW * (HC / 2); i += FU2_THREADS) {
+            const int line = i / (HC / 2), q = i - line * (HC / 2);
+            const int ch = line / CPW, c2 = line - ch * CPW;
+            const int kwo = cg * CPW + c2;
+            if (kwo < g.WP) {
+                const float2 v0 = Ycol[line * LS + 2 * q], v1 = Ycol[line * LS + 2 * q + 1];
+                *reinterpret_cast<float4*>(Yc + (((size_t)b * C + ch) * g.WP + kwo) * HC + 2 * q) =
+                    make_float4(v0.x, v0.y, v1.x, v1.y);
+            }
+        }
+        __syncthreads();   // Ycol is rewritten by the next column group
+    }
+}
+
+// Row C2R + residual from the column-transformed Yc (B, C, W/2+1, H): a workgroup takes RB rows of one
+// plane (small LDS, many workgroups per CU to cover HBM latency); rows in pairs as in fu2d_c2r_kernel.
+template <int H, int W, int UP>
+__global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_rows_kernel(C2rArgs a) {
+    constexpr int WP = W / 2 + 1;
+    constexpr int ZS = zstride(WP);
+    constexpr int RB = H < 64 ? H : 64;
+    constexpr int N1 = Split<W>::N1, N2 = Split<W>::N2, Q = Split<W>::Q;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float2* Z = reinterpret_cast<float2*>(smem);
+    const int plane = blockIdx.x / (H / RB), rb = blockIdx.x - plane * (H / RB);
+    const int kh0 = rb * RB;
+    const int ch = plane % a.C;
+    const int tid = threadIdx.x;
+    {   // Yc[plane][kw][kh0 .. kh0+RB) -> Z rows (16 loads in flight per thread per batch)
+        const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)plane * WP * H + kh0;
+        for (int i0 = 0; i0 < WP * RB; i0 += 16 * FU2_THREADS) {
+            float2 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * FU2_THREADS + tid;
+                if (i < WP * RB) {
+                    const int kw = i / RB, r = i - kw * RB;
+                    v[u] = src[(size_t)kw * H + r];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * FU2_THREADS + tid;
+                if (i < WP * RB) {
+                    const int kw = i / RB, r = i - kw * RB;
+                    Z[r * ZS + kw] = v[u];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
+    const float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
+    constexpr int tW = W / UP;
+    const float* tpl = a.t + (size_t)plane * (H / UP) * tW;
+    float* opl = a.out + (size_t)plane * H * W;
+    constexpr int LPR = FU2_THREADS / N1;
+    const int jj = tid % N1;
+    for (int g0 = 0; g0 < RB / 2; g0 += LPR) {
+        const int g = g0 + tid / N1;
+        if (g >= RB / 2) continue;
+        float2* ra = Z + 2 * g * ZS;
+        float2* rbp = ra + ZS;
+        float re[N2], im[N2];
+#pragma unroll
+        for (int m = 0; m < N2; ++m) {
+            const int k = jj + N1 * m;
+            float2 Av, Bv;
+            if (k <= W / 2) {
+                Av = ra[k];
+                Bv = rbp[k];
+                if (k == 0 || k == W / 2) {
+                    Av.y = 0.0f;
+                    Bv.y = 0.0f;
+                }
+            } else {
+                Av = ra[W - k];
+                Bv = rbp[W - k];
+                Av.y = -Av.y;
+                Bv.y = -Bv.y;
+            }
+            re[m] = Av.x - Bv.y;
+            im[m] = Av.y + Bv.x;
+        }
+        stage_a<W, true>(re, im, jj);
+        float ore[Q][N1], oim[Q][N1];
+        stage_b<W, true>(ra, 1, re, im, jj, ore, oim);
+        float* fa = reinterpret_cast<float*>(ra);   // 4*ZS >= 2W floats: row 2g then row 2g+1
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+            for (int k1 = 0; k1 < N1; ++k1) {
+                const int x = (jj + N1 * q) + N2 * k1;
+                fa[x] = ore[q][k1];
+                fa[W + x] = oim[q][k1];
+            }
+#pragma unroll
+        for (int i = 0; i < (2 * W / 4 + N1 - 1) / N1; ++i) {
+            const int q4 = jj + N1 * i;
+            if (q4 < 2 * W / 4) {
+                const int rr = q4 / (W / 4);
+                const int x = 4 * (q4 % (W / 4));
+                const int y = kh0 + 2 * g + rr;
+                float4 v = *reinterpret_cast<const float4*>(fa + rr * W + x);
+                v.x *= a.norm;
+                v.y *= a.norm;
+                v.z *= a.norm;
+                v.w *= a.norm;
+                if (a.residual) {
+                    const float* trow = tpl + (y / UP) * tW;
+                    if constexpr (UP == 1) {
+                        const float4 s4 = *reinterpret_cast<const float4*>(trow + x);
+                        v.x += in_tf(s4.x, sc, sh, a.in_relu);
+                        v.y += in_tf(s4.y, sc, sh, a.in_relu);
+                        v.z += in_tf(s4.z, sc, sh, a.in_relu);
+                        v.w += in_tf(s4.w, sc, sh, a.in_relu);
+                    } else {
+                        const float2 s2 = *reinterpret_cast<const float2*>(trow + x / 2);
+                        const float s0 = in_tf(s2.x, sc, sh, a.in_relu), s1 = in_tf(s2.y, sc, sh, a.in_relu);
+                        v.x += s0;
+                        v.y += s0;
+                        v.z += s1;
+                        v.w += s1;
+                    }
+                }
+                *reinterpret_cast<float4*>(opl + (size_t)y * W + x) = v;
+            }
         }
     }
 }
@@ -688,6 +907,42 @@ __global__ void pack_mix_f16_kernel(const float* __restrict__ w, int C2, int Mpa
     if (i >= Mpad * C2) return;
     const int o = i / C2;
     out[i] = o < C2 ? (_Float16)w[i] : (_Float16)0.0f;
+}
+
+typedef void (*MixKernel2)(MixArgs);
+template <int MT, int CC, bool F16>
+MixKernel2 pick_cols_h(int H) {
+    switch (H) {
+        case 32: return fu2d_mix_cols_kernel<MT, CC, F16, 32>;
+        case 64: return fu2d_mix_cols_kernel<MT, CC, F16, 64>;
+        case 128: return fu2d_mix_cols_kernel<MT, CC, F16, 128>;
+    }
+    return nullptr;
+}
+MixKernel2 pick_cols(int C, int H, int f16) {
+    if (f16) {
+        if (C == 16) return pick_cols_h<1, 16, true>(H);
+        if (C == 32) return pick_cols_h<2, 32, true>(H);
+        if (C == 64) return pick_cols_h<4, 64, true>(H);
+        return nullptr;
+    }
+    if (C == 16) return pick_cols_h<1, 16, false>(H);
+    if (C == 32) return pick_cols_h<2, 32, false>(H);
+    return nullptr;
+}
+size_t cols_lds(int C, int f16) {
+    const int Mpad = (2 * C + 31) / 32 * 32;
+    const size_t wfl = f16 ? 0 : ((size_t)2 * C * Mpad + 255) / 256 * 256;
+    return 4 * (wfl + 4 * (size_t)C) + 8 * (size_t)C * 128 / 32 * 36;   // Ycol: C * CPW * (HC + 4) float2
+}
+C2rKernel pick_rows(int H, int W, int up) {
+    if (H != W) return nullptr;
+    switch (H) {
+        case 32: return up == 1 ? fu2d_c2r_rows_kernel<32, 32, 1> : fu2d_c2r_rows_kernel<32, 32, 2>;
+        case 64: return up == 1 ? fu2d_c2r_rows_kernel<64, 64, 1> : fu2d_c2r_rows_kernel<64, 64, 2>;
+        case 128: return up == 1 ? fu2d_c2r_rows_kernel<128, 128, 1> : fu2d_c2r_rows_kernel<128, 128, 2>;
+    }
+    return nullptr;
 }
 
 size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * zstride(w / 2 + 1) * 8; }
@@ -845,4 +1100,55 @@ extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const fl
     if (rc) return rc;
     hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r");
+}
+
+extern "C" int ffc_fu2d_cols_supported(int C, int H, int W, int up, int f16) {
+    if (!ffc_fu2d_supported(C, H, W, up) || !pick_cols(C, H, f16) || !pick_rows(H, W, up)) return 0;
+    return cols_lds(C, f16) <= 160 * 1024;
+}
+
+extern "C" int ffc_fu2d_mix_cols(const float* T, int B, int C, int H, int W, int up, const void* wmix, int f16,
+                                 const float* bn_scale, const float* bn_shift, float* Yc, void* stream) {
+    FFC_CHECK_ARG(B > 0 && T && wmix && bn_scale && bn_shift && Yc, "ffc_fu2d_mix_cols: bad args");
+    FFC_CHECK_ARG(ffc_fu2d_cols_supported(C, H, W, up, f16), "ffc_fu2d_mix_cols: unsupported (C, H, W, up)");
+    MixKernel2 k = pick_cols(C, H, f16);
+    MixArgs a;
+    a.T = T;
+    a.wmixT = reinterpret_cast<const float*>(wmix);
+    a.slab = nullptr;
+    a.bn_scale = bn_scale;
+    a.bn_shift = bn_shift;
+    a.Y = Yc;
+    a.B = B;
+    a.C = C;
+    a.H = H;
+    a.W = W;
+    a.up = up;
+    a.ntiles = 0;
+    a.Mpad = (2 * C + 31) / 32 * 32;
+    a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
+    const size_t lds = cols_lds(C, f16);
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_mix_cols");
+    if (rc) return rc;
+    const int cpw = 4 / (H / 32);
+    const int ncg = (W / 2 + 1 + cpw - 1) / cpw;
+    // ~4 column groups per workgroup, but >= ~512 workgroups in all
+    a.nsplit = std::max(1, std::min(ncg, std::max(ncg / 4, (512 + B - 1) / B)));
+    hipLaunchKernelGGL(k, dim3(B * a.nsplit), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu2d_mix_cols");
+}
+
+extern "C" int ffc_fu2d_c2r_rows(const float* Yc, int B, int C, int H, int W, const float* t, int up,
+                                 const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
+                                 void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0 && Yc && out, "ffc_fu2d_c2r_rows: bad args");
+    FFC_CHECK_ARG(!residual || t, "ffc_fu2d_c2r_rows: residual needs t");
+    FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r_rows: in_scale/in_shift pairing");
+    C2rKernel k = pick_rows(H, W, up);
+    FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r_rows: unsupported plane (square, 32..128)");
+    const int RB = H < 64 ? H : 64;
+    const size_t lds = (size_t)RB * zstride(W / 2 + 1) * 8;
+    C2rArgs a{Yc, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W))};
+    hipLaunchKernelGGL(k, dim3(B * C * (H / RB)), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_fu2d_c2r_rows");
 }

@@ -120,11 +120,21 @@ class FourierUnitSN(nn.Module):
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
         else:
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
+        out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
+        if rt.FU_COLS and L.ffc_fu2d_cols_supported(C, H, W, up, int(f16)):
+            # pass 1 with the inverse column FFT fused in (column-major Yc), then rows-only C2R
+            Yc = torch.empty((B, C, W // 2 + 1, H, 2), device=dev, dtype=torch.float32)
+            with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
+                check(L.ffc_fu2d_mix_cols(ptr(T), B, C, H, W, up, ptr(mixT), int(f16), ptr(sc), ptr(sh), ptr(Yc),
+                                          stream), "ffc_fu2d_mix_cols")
+            with rt.observe("fu2d_c2r", bytes=8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)):
+                check(L.ffc_fu2d_c2r_rows(ptr(Yc), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
+                                          int(in_relu), int(residual), ptr(out), stream), "ffc_fu2d_c2r_rows")
+            return out
         Y = torch.empty((B, C, H, W // 2 + 1, 2), device=dev, dtype=torch.float32)
         with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
             check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 1, None, ptr(sc), ptr(sh), ptr(Y), stream),
                   "ffc_fu2d_mix(pass 1)")
-        out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         with rt.observe("fu2d_c2r", bytes=8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)):
             check(L.ffc_fu2d_c2r(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift), int(in_relu),
                                  int(residual), ptr(out), stream), "ffc_fu2d_c2r")

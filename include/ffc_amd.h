@@ -269,6 +269,17 @@ int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, const float
 int ffc_fu_pack_mix_f16(const float* w, int C2, void* wmix16, void* stream);
 int ffc_fu2d_mix_f16(const float* T, int B, int C, int H, int W, int up, const void* wmix16, int pass,
                      float* stats_slab, const float* bn_scale, const float* bn_shift, float* Y, void* stream);
+/* Column-fused variant of pass 1 + C2R for H = W in {32, 64, 128} (C in {16, 32}, or {16, 32, 64} with
+ * f16): ffc_fu2d_mix_cols writes Yc (B, C, W/2+1, H) complex64 = the inverse column FFT (over H,
+ * unnormalised) of relu(Y*bn_scale + bn_shift) -- the mix's workgroups own whole columns, so the
+ * column FFT runs beside the MFMAs; ffc_fu2d_c2r_rows then finishes irfftn (rows, Im of bins 0 and
+ * W/2 ignored, ortho scale) + residual.  wmix: fp32 wmixT (f16 = 0) or the fp16 weight (f16 = 1). */
+int ffc_fu2d_cols_supported(int C, int H, int W, int up, int f16);
+int ffc_fu2d_mix_cols(const float* T, int B, int C, int H, int W, int up, const void* wmix, int f16,
+                      const float* bn_scale, const float* bn_shift, float* Yc, void* stream);
+int ffc_fu2d_c2r_rows(const float* Yc, int B, int C, int H, int W, const float* t, int up,
+                      const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
+                      void* stream);
 int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
                  const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
                  void* stream);

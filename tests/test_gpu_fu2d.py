@@ -102,6 +102,33 @@ def test_st_upsample_large_vs_oracle(cin, cout, n_in, B, train):
             torch.testing.assert_close(after[k].cpu().double(), sd[k], rtol=1e-4, atol=1e-5, msg=k)
 
 
+@pytest.mark.parametrize("c,n,up,train", [(32, 128, 2, True), (32, 64, 2, False), (16, 32, 1, True), (32, 32, 2, False)])
+def test_fu2d_column_fused_matches_unfused(c, n, up, train):
+    """mix pass 1 with the inverse column FFT fused in + rows-only C2R == the unfused pass 1 + C2R,
+    and both match the oracle"""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import _runtime as rt
+    from oracle.ffc_oracle import fourier_unit
+    gen = torch.Generator().manual_seed(n + c)
+    fu = _randomize(F.FourierUnitSN(c, c), gen)
+    sd = _sd64(fu)
+    fu = fu.cuda().train(train)
+    t = torch.randn((2, c, n // up, n // up), generator=gen).cuda()
+    outs = []
+    for cols in (True, False):
+        rt.FU_COLS = cols
+        try:
+            fu.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in sd.items()})
+            with torch.no_grad():
+                outs.append(fu._run(t, up=up).cpu())
+        finally:
+            rt.FU_COLS = True
+    s = torch.repeat_interleave(torch.repeat_interleave(t.cpu().double(), up, 2), up, 3)
+    ref = fourier_unit(s, sd, "", train)
+    assert normwise_err(outs[0], ref) <= TOL and normwise_err(outs[1], ref) <= TOL
+    assert normwise_err(outs[0], outs[1]) <= 1e-5
+
+
 def test_fu2d_deterministic():
     import fastfourierconvolution_amd as F
     gen = torch.Generator().manual_seed(3)
