@@ -68,15 +68,19 @@ def parse():
 # kernel-name prefixes behind each observed launch label (for the PMC traffic lookup)
 LABEL_KERNELS = {"conv_gemm": ("convp_kernel", "conv_gemm_kernel"), "fu_pass0": ("fu_kernel",),
                  "fu_pass1": ("fu_kernel",), "st_prologue": ("st_prologue_kernel",),
-                 "convt_smallm": ("convt_smallm_kernel",)}
+                 "convt_smallm": ("convt_smallm_kernel",), "fu2d_r2c": ("fu2d_r2c_kernel",),
+                 "fu2d_mix0": ("fu2d_mix_kernel",), "fu2d_mix1": ("fu2d_mix_cols_kernel", "fu2d_mix_kernel"),
+                 "fu2d_c2r": ("fu2d_c2r",), "conv3_smallm": ("conv3x3_smallm_kernel",),
+                 "dense": ("dense_kernel",)}
 
 
-def pmc_traffic(label):
+def pmc_traffic(label, workload="gen64"):
     """HBM bytes per launch of the kernels behind `label`, from the newest committed
     profiles/<round>/pmc_traffic.json (tools/pmc_traffic.sh: FETCH_SIZE / WRITE_SIZE passes,
     corrected per MI355X_MICROARCH.md), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    name = "pmc_traffic.json" if workload == "gen64" else f"pmc_traffic_{workload}.json"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
     if not files or label not in LABEL_KERNELS:
         return None
     kern = json.load(open(files[-1]))["kernels"]
@@ -247,7 +251,7 @@ def main():
         achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4)}
-    tr = pmc_traffic(dom)
+    tr = pmc_traffic(dom, args.workload)
     roof["traffic"] = tr["bytes_per_launch"] if tr else None
     if tr:
         roof["traffic_source"] = tr["source"]

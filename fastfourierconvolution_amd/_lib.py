@@ -117,7 +117,9 @@ SIGNATURES = [
                                  c_void_p]),
     ("ffc_dense_forward", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                   c_int, c_float, c_void_p]),
-    ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
+    ("ffc_convt_smallm_pack_floats", c_size_t, [c_int, c_int]),
+    ("ffc_convt_smallm_pack", c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                       c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
 ]
 

@@ -259,8 +259,12 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
             a1[g] = n1[g];
         }
         if (ci + 1 < nchunks) {  // next chunk's A and patch stay in flight under this chunk's MFMAs
+#ifndef FFC_PROBE_NOA   // timing-probe builds only (wrong results): drop the A loads / patch staging
             load_A(sch, n0, n1);
+#endif
+#ifndef FFC_PROBE_NOSTAGE
             stage_issue(sch, patch + ((ci + 1) & 1) * ebuf);
+#endif
             sch += CC;
             if (sch >= st.Cpad && ss + 1 < nseg) {
                 ++ss;
@@ -273,6 +277,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         tr_stg += tr_a - tr_b;
 #endif
         const int T = cp.T;
+#ifndef FFC_PROBE_NOMFMA
         if (T > 0) {
             const int base = ((ci & 1) * ebuf) * 4;   // byte offset of this chunk's buffer
 #pragma unroll
@@ -291,10 +296,10 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
                             acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
                         }
                     }
-
                 }
             }
         }
+#endif
 #ifdef FFC_TRACE
         FFC_STAMP(tr_b);
         tr_mf += tr_b - tr_a;

@@ -9,187 +9,231 @@
 //
 // The FFC-DCGAN generator's last layer (FFC_BN_ACT(ngf, nc, 4, 0.5, 0, 2, 1, Tanh),
 // models/ffc_generator.py:28; local branch ffc_transpose.py:96-100) maps 2 x 32 channels
-// to nc = 1 or 3 channels at 64x64.  An MFMA tile would be >90% padding, so this kernel
-// computes it on the VALU.  Each thread owns a 2x2 block of input pixels (my, mx) and
-// produces their 4x4 output pixels (2my+py, 2mx+px) for all M channels from the 4x4 input
-// neighbourhood it reads once per channel:
+// to nc = 1 or 3 channels at 64x64 (convt_smallm_kernel).  An MFMA tile would be >90% padding,
+// so it runs on the VALU.  Each thread owns a 2x2 block of input pixels (my, mx) and produces
+// their 4x4 output pixels (2my+py, 2mx+px) for all M channels from the 4x4 input neighbourhood
+// it reads once per channel:
 //     py = 0: (ky=1, dy=0), (ky=3, dy=-1)      py = 1: (ky=0, dy=+1), (ky=2, dy=0)
-// A workgroup covers a 32x32 input tile (+1 halo) with two halves of 256 threads that split the
-// channel chunks (even / odd 8-channel chunks; two waves per SIMD) and add their partial sums
-// in a fixed order at the end.  Each half's chunk of the tile and of the weights is staged in
-// LDS by LDS-DMA (global_load_lds_dword, zero fill outside the image), double buffered; the
-// weights of a channel are read as wave-uniform (broadcast) ds_read_b128 and reused by the
-// thread's 4 pixels: per channel 16 patch reads + 4M broadcast reads feed 64M FMAs.
+// A workgroup covers a 32x16 input tile (+1 halo) with four quarters of 128 threads that take
+// alternate channels and add their partial sums in a fixed order at the end; two workgroups per
+// CU.  All weights are staged once as [channel][tap][m 0..3], so the FMAs run as v_pk_fma_f32 on
+// output-channel pairs (one input value against two channels' weights).  Each quarter stages
+// its next channel's patch through registers (float4 loads issued before the current channel's
+// FMAs, written to the other LDS buffer after them).
 #include "ffc_internal.h"
 
 namespace {
 
-constexpr int CCH = 8;       // channels per chunk
-constexpr int TT = 32;       // input tile (TT x TT), 16 x 16 threads x 2 x 2 pixels
-constexpr int PP = TT + 2;   // patch side with halo
-constexpr int PE = CCH * PP * PP;
-constexpr int WE = CCH * 4 * 16;          // chunk weights (M <= 4)
-constexpr int EBUF = ((PE + WE) + 255) & ~255;   // 4 buffers (2 halves x 2 stages) = 160 KiB
-constexpr int SM_THREADS = 512;
-
-__device__ float g_zero_sm[64];
-typedef __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
+constexpr int SM_THREADS = 512;   // conv3x3_smallm_kernel: two halves of 256
 
 struct SmallMArgs {
     const float* x[2];
-    const float* w[2];   // ConvTranspose2d weights (C_s, M, 4, 4)
+    const float* w[2];   // Conv2d (M, C_s, 3, 3) weights (conv3x3_smallm_kernel)
+    const float* wpack;  // ConvTranspose2d weights packed [C0 + C1][16][4] (convt_smallm_kernel)
     int C[2];
     int nseg;
     const float* bias;
-    float* out;          // (B, M, 2IH, 2IW)
+    float* out;
     int B, IH, IW, M;
     int nty, ntx;
     int act;
     float act_param;
 };
 
-template <int MM>
-__global__ __launch_bounds__(SM_THREADS) void convt_smallm_kernel(SmallMArgs a) {
+// ---- ConvTranspose2d k4 s2 p1, M <= 4: 32x32 input tile (64x64 outputs) per workgroup.
+constexpr int CT_TT = 32;                    // input tile columns; a thread owns 2x2 input pixels
+#ifndef FFC_CT_TR
+#define FFC_CT_TR 16
+#endif
+#ifndef FFC_CT_CPQ
+#define FFC_CT_CPQ 2
+#endif
+constexpr int CT_TR = FFC_CT_TR;             // input tile rows
+constexpr int CT_QT = (CT_TT / 2) * (CT_TR / 2);   // threads per channel quarter
+constexpr int CT_PR = CT_TR + 2;             // patch rows: iy = y0-1 .. y0+TR
+constexpr int CT_PS = CT_TT + 8;             // patch row: ix = x0-4 .. x0+35 (10 aligned float4 groups)
+constexpr int CT_G = CT_PR * (CT_PS / 4);    // float4 groups per channel
+constexpr int CT_CPQ = FFC_CT_CPQ;           // channels per quarter per step
+constexpr int CT_GT = (CT_CPQ * CT_G + CT_QT - 1) / CT_QT;   // groups per thread per step
+constexpr int CT_PB = CT_PR * CT_PS;         // floats per channel patch
+constexpr int CT_NQ = 4;                     // channel quarters
+constexpr int CT_THREADS = CT_QT * CT_NQ;
+constexpr int CT_CMAX = 256;                 // channels (both segments) whose weights fit in LDS
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// MM output channels: pairs (m, m+1) run as v_pk_fma_f32, one input value against the two
+// channels' weights (LDS weight layout [channel][tap][m 0..3]); an odd last channel is scalar.
+template <int MM, bool VEC>   // VEC: IW % 4 == 0, every float4 group wholly inside or outside a row
+__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void convt_smallm_kernel(SmallMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int half = threadIdx.x >> 8, tid = threadIdx.x & 255, wave = tid >> 6;
+    const int q = __builtin_amdgcn_readfirstlane(threadIdx.x / CT_QT), tid = threadIdx.x % CT_QT;
     int bid = blockIdx.x;
     const int tx = bid % a.ntx;
     bid /= a.ntx;
     const int ty = bid % a.nty;
     const int b = bid / a.nty;
-    const int y0 = ty * TT, x0 = tx * TT;
-    const int qy = 2 * (tid >> 4), qx = 2 * (tid & 15);   // top-left of this thread's 2x2 pixels
-    const int M = a.M;
+    const int y0 = ty * CT_TR, x0 = tx * CT_TT;
+    const int qy = 2 * (tid >> 4), qx = 2 * (tid & 15);   // top-left of this thread's 2x2 input pixels
+    const int M = a.M, C0 = a.C[0];
+    const int Ct = C0 + (a.nseg > 1 ? a.C[1] : 0);
+    float* pbuf = lds;   // [2 stages][NQ][CPQ][PB]
+    // packed weights [Ct][16 taps][4 m] (ffc_convt_smallm_pack), read through the scalar cache:
+    // a channel's 64 values are wave-uniform and sit in SGPRs, so the FMAs need no LDS traffic
+    typedef float fx4 __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(4))) fx4* cf4;
+    const cf4 wpk = (cf4)a.wpack;
 
-    const int nch0 = (a.C[0] + CCH - 1) / CCH;
-    const int nchunks = nch0 + (a.nseg > 1 ? (a.C[1] + CCH - 1) / CCH : 0);
-
-    auto stage = [&](int ci, float* dst) {
-        const int s = ci < nch0 ? 0 : 1;
-        const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
-        const float* x = a.x[s];
-        const float* w = a.w[s];
-        const int C = a.C[s];
-        const int wn = min(CCH, C - c0) * M * 16;
-        for (int e = 0; e * 256 < PE + WE; ++e) {
-            const int n = e * 256 + tid;
-            const float* src = g_zero_sm;
-            if (n < PE) {
-                const int pc = n % PP, r = n / PP;
-                const int pr = r % PP, ch = r / PP;
-                const int iy = y0 - 1 + pr, ix = x0 - 1 + pc, c = c0 + ch;
-                if (c < C && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
-                    src = x + (((size_t)b * C + c) * a.IH + iy) * a.IW + ix;
-            } else if (n - PE < wn) {
-                src = w + (size_t)c0 * M * 16 + (n - PE);
+    // step k of quarter q: channels CPQ (NQ k + q) + {0 .. CPQ-1}
+    auto load = [&](int k, float4 (&r)[CT_GT]) {
+#pragma unroll
+        for (int j = 0; j < CT_GT; ++j) {
+            const int n = j * CT_QT + tid;
+            const int cl = n / CT_G, nn = n - cl * CT_G;
+            const int ci = CT_CPQ * (CT_NQ * k + q) + cl;
+            const int g = nn % (CT_PS / 4), pr = nn / (CT_PS / 4);
+            const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
+            r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (n >= CT_CPQ * CT_G || ci >= Ct || (unsigned)iy >= (unsigned)a.IH) continue;
+            const int s = ci < C0 ? 0 : 1;
+            const int c = s == 0 ? ci : ci - C0;
+            const float* x = a.x[s] + ((size_t)b * a.C[s] + c) * a.IH * a.IW;
+            const float* row = x + (size_t)iy * a.IW;
+            if (VEC) {
+                if ((unsigned)ix < (unsigned)a.IW) r[j] = *reinterpret_cast<const float4*>(row + ix);
+            } else {
+                if ((unsigned)ix < (unsigned)a.IW) r[j].x = row[ix];
+                if ((unsigned)(ix + 1) < (unsigned)a.IW) r[j].y = row[ix + 1];
+                if ((unsigned)(ix + 2) < (unsigned)a.IW) r[j].z = row[ix + 2];
+                if ((unsigned)(ix + 3) < (unsigned)a.IW) r[j].w = row[ix + 3];
             }
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + e * 256 + wave * 64), 4, 0, 0);
+        }
+    };
+    auto put = [&](float* dst, const float4 (&r)[CT_GT]) {
+#pragma unroll
+        for (int j = 0; j < CT_GT; ++j) {
+            const int n = j * CT_QT + tid;
+            if (n < CT_CPQ * CT_G) reinterpret_cast<float4*>(dst)[n] = r[j];
+        }
+    };
+    auto buf = [&](int k) { return pbuf + ((k & 1) * CT_NQ + q) * CT_CPQ * CT_PB; };
+
+    constexpr int NPR = MM / 2, NSG = MM % 2;
+    // [output row * 4 + output col] of the thread's 4x4 block: channel pairs, odd last channel
+    f2 accp[16][NPR > 0 ? NPR : 1];
+    float accs[16][NSG > 0 ? NSG : 1];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+#pragma unroll
+        for (int mp = 0; mp < NPR; ++mp) accp[o][mp] = f2{0.0f, 0.0f};
+        if (NSG) accs[o][0] = 0.0f;
+    }
+    auto get = [&](int o, int m) -> float {
+        if (m < 2 * NPR) return (m & 1) ? accp[o][m >> 1].y : accp[o][m >> 1].x;
+        return accs[o][0];
+    };
+    auto add = [&](int o, int m, float v) {
+        if (m < 2 * NPR) {
+            if (m & 1) accp[o][m >> 1].y += v;
+            else accp[o][m >> 1].x += v;
+        } else {
+            accs[o][0] += v;
         }
     };
 
-    float acc[MM][4][4];   // [m][output row 0..3][output col 0..3] of the thread's 4x4 output block
+    // out[oy] += x[iy] w[ky] with oy = 2 iy - 1 + ky: output row 2(qy+aa)+py takes input row
+    // qy+aa+dy through ky = py + 1 - 2 dy (same for columns)
+    auto compute = [&](int k, int cl) {
+        const int ci = CT_CPQ * (CT_NQ * k + q) + cl;
+        if (ci >= Ct) return;
+        const float* p = buf(k) + cl * CT_PB + qy * CT_PS + qx + 3;   // input row qy-1, col qx-1
+        float v[4][4];
 #pragma unroll
-    for (int m = 0; m < MM; ++m)
+        for (int i = 0; i < 4; ++i) {
+            const f2 mid = *reinterpret_cast<const f2*>(p + i * CT_PS + 1);
+            v[i][0] = p[i * CT_PS];
+            v[i][1] = mid.x;
+            v[i][2] = mid.y;
+            v[i][3] = p[i * CT_PS + 3];
+        }
+        const cf4 wc = wpk + ci * 16;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int ky = 0; ky < 4; ++ky) {
+            const int py = (ky & 1) ? 0 : 1, dy = ky == 0 ? 1 : (ky == 3 ? -1 : 0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[m][i][j] = 0.0f;
-
-    const int nsteps = (nchunks + 1) / 2;   // half h takes chunks 2k + h
-    if (half < nchunks) stage(half, lds + half * EBUF);
-    for (int k = 0; k < nsteps; ++k) {
-        __syncthreads();
-        const int ci = 2 * k + half;
-        if (ci + 2 < nchunks) stage(ci + 2, lds + (((k + 1) & 1) * 2 + half) * EBUF);
-        if (ci >= nchunks) continue;
-        const float* cur = lds + ((k & 1) * 2 + half) * EBUF;
-        const int s = ci < nch0 ? 0 : 1;
-        const int c0 = (s == 0 ? ci : ci - nch0) * CCH;
-        const int cn = min(CCH, a.C[s] - c0);
-        for (int cc = 0; cc < cn; ++cc) {
-            // 4x4 neighbourhood: input rows qy-1..qy+2, cols qx-1..qx+2 (patch has a +1 halo)
-            float v[4][4];
-            const float* p = cur + (cc * PP + qy) * PP + qx;
+            for (int kx = 0; kx < 4; ++kx) {
+                const fx4 wk = wc[ky * 4 + kx];
+                const int px = (kx & 1) ? 0 : 1, dx = kx == 0 ? 1 : (kx == 3 ? -1 : 0);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+                for (int aa = 0; aa < 2; ++aa)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[i][j] = p[i * PP + j];
-            const float* wl = cur + PE + cc * M * 16;
-#pragma unroll
-            for (int m = 0; m < MM; ++m) {
-                if (m < M) {
-                    float k[16];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 t = reinterpret_cast<const float4*>(wl + m * 16)[q];
-                        k[4 * q] = t.x; k[4 * q + 1] = t.y; k[4 * q + 2] = t.z; k[4 * q + 3] = t.w;
+                    for (int cb = 0; cb < 2; ++cb) {
+                        const float xv = v[aa + dy + 1][cb + dx + 1];
+                        const int o = (2 * aa + py) * 4 + 2 * cb + px;
+                        const f2 xx = f2{xv, xv};
+                        if (NPR > 0) accp[o][0] = __builtin_elementwise_fma(xx, f2{wk.x, wk.y}, accp[o][0]);
+                        if (NPR > 1) accp[o][1] = __builtin_elementwise_fma(xx, f2{wk.z, wk.w}, accp[o][1]);
+                        if (NSG) accs[o][0] = fmaf(xv, MM == 1 ? wk.x : wk.z, accs[o][0]);
                     }
-                    // input pixel (qy+aa, qx+cb); output row 2aa+py, col 2cb+px
-#pragma unroll
-                    for (int aa = 0; aa < 2; ++aa)
-#pragma unroll
-                        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-                            for (int py = 0; py < 2; ++py)
-#pragma unroll
-                                for (int px = 0; px < 2; ++px) {
-                                    float s2 = acc[m][2 * aa + py][2 * cb + px];
-#pragma unroll
-                                    for (int ta = 0; ta < 2; ++ta)
-#pragma unroll
-                                        for (int tb = 0; tb < 2; ++tb) {
-                                            const int ky = py == 0 ? (ta == 0 ? 1 : 3) : (ta == 0 ? 0 : 2);
-                                            const int dy = py == 0 ? (ta == 0 ? 0 : -1) : (ta == 0 ? 1 : 0);
-                                            const int kx = px == 0 ? (tb == 0 ? 1 : 3) : (tb == 0 ? 0 : 2);
-                                            const int dx = px == 0 ? (tb == 0 ? 0 : -1) : (tb == 0 ? 1 : 0);
-                                            s2 = fmaf(v[aa + dy + 1][cb + dx + 1], k[ky * 4 + kx], s2);
-                                        }
-                                    acc[m][2 * aa + py][2 * cb + px] = s2;
-                                }
-                }
             }
         }
-    }
-    // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
+    };
+    // one step of prefetch per quarter in registers: step k+1's loads are in flight under step k's
+    // FMAs (LDS-DMA would not overlap: the compiler drains it before any LDS read)
+    float4 r[CT_GT];
+    const int nsteps = (Ct + CT_NQ * CT_CPQ - 1) / (CT_NQ * CT_CPQ);
+    load(0, r);
+    put(buf(0), r);
     __syncthreads();
-    float* part = lds;   // 256 threads x MM x 16 (the stage buffers are free now)
-    if (half == 1) {
+    for (int k = 0; k < nsteps; ++k) {
+        const bool more = k + 1 < nsteps;
+        if (more) load(k + 1, r);
 #pragma unroll
-        for (int m = 0; m < MM; ++m)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * 256 + tid] = acc[m][i][j];
+        for (int cl = 0; cl < CT_CPQ; ++cl) {
+            compute(k, cl);
+            __builtin_amdgcn_sched_barrier(0);   // one channel's neighbourhood live at a time
+        }
+        if (more) put(buf(k + 1), r);
+        __syncthreads();
     }
-    __syncthreads();
-    if (half == 1) return;
+    // fixed-order combine of the quarters' partial sums: ((q0 + q1) + q2) + q3
+    float* part = lds;   // QT threads x 16 MM floats
+    for (int rq = 1; rq < CT_NQ; ++rq) {
+        if (q == rq) {
 #pragma unroll
-    for (int m = 0; m < MM; ++m)
+            for (int o = 0; o < 16; ++o)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+                for (int m = 0; m < MM; ++m) part[(o * MM + m) * CT_QT + tid] = get(o, m);
+        }
+        __syncthreads();
+        if (q == 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[m][i][j] += part[((m * 4 + i) * 4 + j) * 256 + tid];
+            for (int o = 0; o < 16; ++o)
+#pragma unroll
+                for (int m = 0; m < MM; ++m) add(o, m, part[(o * MM + m) * CT_QT + tid]);
+        }
+        __syncthreads();
+    }
+    if (q != 0) return;
     const int OH = 2 * a.IH, OW = 2 * a.IW;
     const int oy0 = 2 * (y0 + qy), ox0 = 2 * (x0 + qx);
     const bool xin = x0 + qx + 1 < a.IW;   // both input columns in range
     auto store = [&](auto actf) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            if (m >= M) break;
             const float bv = a.bias ? a.bias[m] : 0.0f;
+            auto val = [&](int i, int j) { return actf(get(i * 4 + j, m) + bv); };
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int oy = oy0 + i;
                 if (oy >= OH) continue;
                 float* row = a.out + (((size_t)b * M + m) * OH + oy) * OW + ox0;
                 if (xin) {
-                    *reinterpret_cast<float4*>(row) = make_float4(actf(acc[m][i][0] + bv), actf(acc[m][i][1] + bv),
-                                                                  actf(acc[m][i][2] + bv), actf(acc[m][i][3] + bv));
+                    *reinterpret_cast<float4*>(row) = make_float4(val(i, 0), val(i, 1), val(i, 2), val(i, 3));
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (ox0 + j < OW) row[j] = actf(acc[m][i][j] + bv);
+                        if (ox0 + j < OW) row[j] = val(i, j);
                 }
             }
         }
@@ -392,44 +436,82 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
 
 }  // namespace
 
-extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
-                                     const float* w1, const float* bias, int B, int IH, int IW, int M,
-                                     float* out, int act, float act_param, void* stream) {
-    FFC_CHECK_ARG(x0 && w0 && out && B > 0 && IH > 0 && IW > 0 && C0 > 0, "ffc_convt_k4s2_smallm: bad args");
+static __global__ void convt_smallm_pack_kernel(const float* __restrict__ w0, int C0, const float* __restrict__ w1,
+                                         int C1, int M, float* __restrict__ wp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (C0 + C1) * 64) return;
+    const int ci = i >> 6, tap = (i >> 2) & 15, m = i & 3;
+    const float* w = ci < C0 ? w0 : w1;
+    const int c = ci < C0 ? ci : ci - C0;
+    wp[i] = m < M ? w[((size_t)c * M + m) * 16 + tap] : 0.0f;
+}
+
+extern "C" size_t ffc_convt_smallm_pack_floats(int C0, int C1) {
+    return C0 > 0 && C1 >= 0 ? (size_t)(C0 + C1) * 64 : 0;
+}
+
+extern "C" int ffc_convt_smallm_pack(const float* w0, int C0, const float* w1, int C1, int M, float* wpack,
+                                     void* stream) {
+    FFC_CHECK_ARG(w0 && wpack && C0 > 0 && C1 >= 0 && (C1 == 0 || w1) && M >= 1 && M <= 4,
+                  "ffc_convt_smallm_pack: bad args");
+    const int n = (C0 + C1) * 64;
+    hipLaunchKernelGGL(convt_smallm_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w0, C0,
+                       w1, C1, M, wpack);
+    return ffc::launch_status("ffc_convt_smallm_pack");
+}
+
+extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, int C1, const float* wpack,
+                                     const float* bias, int B, int IH, int IW, int M, float* out, int act,
+                                     float act_param, void* stream) {
+    FFC_CHECK_ARG(x0 && wpack && out && B > 0 && IH > 0 && IW > 0 && C0 > 0, "ffc_convt_k4s2_smallm: bad args");
     FFC_CHECK_ARG(M >= 1 && M <= 4, "ffc_convt_k4s2_smallm: 1 <= M <= 4");
-    FFC_CHECK_ARG(!x1 || (w1 && C1 > 0), "ffc_convt_k4s2_smallm: second segment");
-    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "ffc_convt_k4s2_smallm: output not 16-B aligned");
+    FFC_CHECK_ARG(!x1 || C1 > 0, "ffc_convt_k4s2_smallm: second segment");
+    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(wpack) & 15) == 0,
+                  "ffc_convt_k4s2_smallm: output / packed weights not 16-B aligned");
+    FFC_CHECK_ARG(C0 + (x1 ? C1 : 0) <= CT_CMAX, "ffc_convt_k4s2_smallm: at most 256 input channels");
     SmallMArgs a;
     a.x[0] = x0;
-    a.w[0] = w0;
+    a.w[0] = nullptr;
     a.C[0] = C0;
     a.x[1] = x1;
-    a.w[1] = w1;
+    a.w[1] = nullptr;
     a.C[1] = x1 ? C1 : 0;
     a.nseg = x1 ? 2 : 1;
+    a.wpack = wpack;
     a.bias = bias;
     a.out = out;
     a.B = B;
     a.IH = IH;
     a.IW = IW;
     a.M = M;
-    a.nty = (IH + TT - 1) / TT;
-    a.ntx = (IW + TT - 1) / TT;
+    a.nty = (IH + CT_TR - 1) / CT_TR;
+    a.ntx = (IW + CT_TT - 1) / CT_TT;
     a.act = act;
     a.act_param = act_param;
-    const size_t lds = 4 * (size_t)EBUF * sizeof(float);
+
+    const size_t main_bytes = (size_t)2 * CT_NQ * CT_CPQ * CT_PB * sizeof(float);
+    const size_t comb_bytes = (size_t)CT_QT * 16 * M * sizeof(float);
+    const size_t lds = main_bytes > comb_bytes ? main_bytes : comb_bytes;
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
-    auto k = convt_smallm_kernel<4>;
-    static bool raised = false;
-    if (!raised) {
+    // M is a template parameter: no runtime m < M branches in the FMA body
+    typedef void (*CtKernel)(SmallMArgs);
+    static const CtKernel kernels[2][4] = {
+        {convt_smallm_kernel<1, false>, convt_smallm_kernel<2, false>, convt_smallm_kernel<3, false>,
+         convt_smallm_kernel<4, false>},
+        {convt_smallm_kernel<1, true>, convt_smallm_kernel<2, true>, convt_smallm_kernel<3, true>,
+         convt_smallm_kernel<4, true>}};
+    const int vec = IW % 4 == 0 ? 1 : 0;
+    auto k = kernels[vec][M - 1];
+    static bool raised[2][5] = {};
+    if (!raised[vec][M]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) {
             ffc::set_error("ffc_convt_k4s2_smallm: hipFuncSetAttribute failed");
             return FFC_E_LAUNCH;
         }
-        raised = true;
+        raised[vec][M] = true;
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(CT_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_convt_k4s2_smallm");
 }
 
@@ -449,6 +531,7 @@ extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, cons
     a.w[1] = w1;
     a.C[1] = x1 ? C1 : 0;
     a.nseg = x1 ? 2 : 1;
+    a.wpack = nullptr;
     a.bias = bias;
     a.out = out;
     a.B = B;

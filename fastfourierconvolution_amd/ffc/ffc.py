@@ -293,17 +293,33 @@ class _FFCExec:
         x1 = inp[1][0] if len(inp) > 1 else None
         w1 = w[1][0] if len(w) > 1 else None
         bias = next((x[4] for x in w if x[4] is not None), None)
+        C1 = segs[1].C if x1 is not None else 0
         if kind == "convT":
+            # weights packed [C0 + C1][16 taps][4] by a HIP kernel, cached per (pointer, version)
+            cache = self._ffc_cache()
+            key = ("ctpack", w[0][0].data_ptr(), w[0][0]._version,
+                   None if w1 is None else (w1.data_ptr(), w1._version))
+            wp = cache.get(key)
+            if wp is None:
+                for old in [kk for kk in cache if kk[0] == "ctpack" and kk[1] == key[1]]:
+                    del cache[old]
+                wp = cache[key] = torch.empty(rt.lib().ffc_convt_smallm_pack_floats(segs[0].C, C1), device=dev,
+                                              dtype=torch.float32)
+                rt.check(rt.lib().ffc_convt_smallm_pack(w[0][0].data_ptr(), segs[0].C, rt.ptr(w1), C1, M,
+                                                        wp.data_ptr(), stream), "ffc_convt_smallm_pack")
             out = torch.empty((B, M, 2 * IH, 2 * IW), device=dev, dtype=torch.float32)
-            fn, label, taps, OH, OW = rt.lib().ffc_convt_k4s2_smallm, "convt_smallm", 4, 2 * IH, 2 * IW
-        else:
-            out = torch.empty((B, M, IH, IW), device=dev, dtype=torch.float32)
-            fn, label, taps, OH, OW = rt.lib().ffc_conv3x3_smallm, "conv3_smallm", 9, IH, IW
-        flops = 2.0 * B * M * sum(sg.C for sg in segs) * taps * OH * OW
-        with rt.observe(label, flops=flops):
-            rt.check(fn(inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(), rt.ptr(x1),
-                        segs[1].C if x1 is not None else 0, rt.ptr(w1), rt.ptr(bias), B, IH, IW, M, out.data_ptr(),
-                        act[0], act[1], stream), f"ffc_{label}")
+            flops = 2.0 * B * M * sum(sg.C for sg in segs) * 4 * (2 * IH) * (2 * IW)
+            with rt.observe("convt_smallm", flops=flops):
+                rt.check(rt.lib().ffc_convt_k4s2_smallm(inp[0][0].data_ptr(), segs[0].C, rt.ptr(x1), C1,
+                                                        wp.data_ptr(), rt.ptr(bias), B, IH, IW, M, out.data_ptr(),
+                                                        act[0], act[1], stream), "ffc_convt_k4s2_smallm")
+            return out
+        out = torch.empty((B, M, IH, IW), device=dev, dtype=torch.float32)
+        flops = 2.0 * B * M * sum(sg.C for sg in segs) * 9 * IH * IW
+        with rt.observe("conv3_smallm", flops=flops):
+            rt.check(rt.lib().ffc_conv3x3_smallm(inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(), rt.ptr(x1), C1,
+                                                 rt.ptr(w1), rt.ptr(bias), B, IH, IW, M, out.data_ptr(),
+                                                 act[0], act[1], stream), "ffc_conv3x3_smallm")
         return out
 
     def _bn_from_tensor(self, bn, out, stream):

@@ -216,11 +216,16 @@ int ffc_pw_gate_conv(const float* x, const float* gate, const float* w, int B, i
 int ffc_pack_transpose(const float* w, int R, int K, float* wT, void* stream);
 
 /* Direct ConvTranspose2d(k=4, s=2, p=1) for M <= 4 output channels (the generator's last
- * layer, models/ffc_generator.py:28): out = act(conv_t(x0; w0) [+ conv_t(x1; w1)] + bias).
- * w*: raw ConvTranspose2d weights (C, M, 4, 4); x1/w1 may be NULL. */
-int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
-                          const float* w1, const float* bias, int B, int IH, int IW, int M,
-                          float* out, int act, float act_param, void* stream);
+ * layer, models/ffc_generator.py:28; ffc_transpose.py:96-100):
+ *   out = act(conv_t(x0; w0) [+ conv_t(x1; w1)] + bias).
+ * The weights are first packed by ffc_convt_smallm_pack from the raw ConvTranspose2d weights
+ * w0 (C0, M, 4, 4) and w1 (C1, M, 4, 4) (w1 NULL with C1 = 0) into wpack
+ * [ffc_convt_smallm_pack_floats(C0, C1)] = [C0 + C1][16 taps][4], 16-byte aligned; x1 may be NULL. */
+size_t ffc_convt_smallm_pack_floats(int C0, int C1);
+int ffc_convt_smallm_pack(const float* w0, int C0, const float* w1, int C1, int M, float* wpack, void* stream);
+int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, int C1, const float* wpack,
+                          const float* bias, int B, int IH, int IW, int M, float* out, int act,
+                          float act_param, void* stream);
 /* Direct Conv2d(k=3, s=1, p=1) for M <= 4 output channels (the fgan128 generator's head conv7,
  * fgan128_complete.py:484): out = act(conv(x0; w0) [+ conv(x1; w1)] + bias), (B, M, H, W).
  * w*: raw Conv2d weights (M, C, 3, 3); x1/w1 may be NULL. */
