@@ -121,6 +121,20 @@ SIGNATURES = [
     ("ffc_convt_smallm_pack", c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_convt_k4s2_smallm", c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                       c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
+    ("ffc_act_bwd", c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_int, c_float, c_void_p]),
+    ("ffc_reduce_splits", c_int, [c_int, c_int, c_int]),
+    ("ffc_channel_moments", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_bn_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p,
+                           c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_void_p]),
+    ("ffc_conv_wgrad", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    ("ffc_rfft2_planes", c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
+    ("ffc_irfft2_planes", c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
+    ("ffc_se_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("ffc_pool2", c_int, [c_void_p, c_longlong, c_int, c_int, c_float, c_void_p, c_void_p]),
+    ("ffc_up2", c_int, [c_void_p, c_longlong, c_int, c_int, c_float, c_void_p, c_void_p]),
 ]
 
 _lock = threading.Lock()

@@ -422,6 +422,18 @@ def sn_refresh(mod):
             setattr(mod, h.name, buf)
 
 
+def sn_refresh_train(mod):
+    """training path: run the spectral_norm pre-hooks so ``mod.weight`` = weight_orig / sigma is a
+    differentiable function of weight_orig (the reference calls the module, which does the same)"""
+    hooks = getattr(mod, "_forward_pre_hooks", None)
+    if not hooks:
+        return
+    from torch.nn.utils.spectral_norm import SpectralNorm
+    for h in hooks.values():
+        if isinstance(h, SpectralNorm):
+            h(mod, None)
+
+
 def conv_weight(mod):
     """(weight, layout, kh, kw, bias) for nn.Conv2d (layout 0) / nn.ConvTranspose2d (layout 1)."""
     w = mod.weight.detach()

@@ -1,0 +1,646 @@
+// Training path (BASELINE config 3: FFC-DCGAN generator + discriminator fwd+bwd) on gfx950.
+//
+// The inference forward fuses whole SpectralTransforms into a few launches and keeps nothing.
+// With autograd the path is split at the reference's own op boundaries (fourier_unity.py:32-56,
+// spectral_transform.py:77-110, ffc.py:84-99, ffc_transpose.py:91-110, ffc_bn_act.py:70-83),
+// each op a custom autograd function over the kernels below plus the inference conv GEMMs,
+// which also compute every data gradient (the adjoint of a conv is a transposed conv with the
+// same weight tensor and vice versa, so ffc_conv_forward / ffc_convp_forward run them):
+//
+//   ffc_conv_wgrad        weight gradients of conv / convT / 1x1 / Linear on f32 MFMA
+//                         (v_mfma_f32_32x32x2_f32), split-K over samples, deterministic
+//   ffc_rfft2_planes      rfftn(norm="ortho") per plane into the interleaved Re/Im channel
+//                         planes of fourier_unity.py:40-42 (interior bins x scale: with 2 it is
+//                         the adjoint of irfftn)
+//   ffc_irfft2_planes     irfftn(s=(H,W), norm="ortho") from interleaved planes (+ addend);
+//                         interior bins x scale (0.5 gives the adjoint of rfftn)
+//   ffc_channel_moments   {n, sum x, sum x^2} per channel in fp64 (BatchNorm2d batch stats)
+//   ffc_bn_bwd_*          BatchNorm2d (+ following activation) backward, fp64 reductions
+//   ffc_act_bwd           activation backward from the activation output
+//   ffc_se_bwd            SELayer backward, one workgroup per sample
+//   ffc_pool2 / ffc_up2   2x2 average pool / nearest x2 upsample (and each other's adjoint)
+#include <algorithm>
+
+#include "ffc_internal.h"
+
+namespace {
+
+__device__ __forceinline__ float act_grad_from_out(float y, float x_or_y, int act, float p) {
+    // derivative of the activation expressed through its output y (GELU: through its input)
+    switch (act) {
+        case FFC_ACT_RELU: return y > 0.0f ? 1.0f : 0.0f;
+        case FFC_ACT_LEAKY_RELU: return y > 0.0f ? 1.0f : p;
+        case FFC_ACT_TANH: return 1.0f - y * y;
+        case FFC_ACT_SIGMOID: return y * (1.0f - y);
+        case FFC_ACT_GELU: {
+            const float x = x_or_y;
+            const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+            const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+            return cdf + x * pdf;
+        }
+        default: return 1.0f;
+    }
+}
+
+// ------------------------------------------------------------------ activation backward
+__global__ void act_bwd_kernel(const float* __restrict__ t, const float* __restrict__ dy, float* __restrict__ dx,
+                               long long n, int act, float p) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float v = t[i];
+        float y = v;
+        if (act == FFC_ACT_GELU) y = 0.0f;
+        dx[i] = dy[i] * act_grad_from_out(y, v, act, p);
+    }
+}
+
+// ------------------------------------------------------------------ channel moments (fp64)
+// grid (C, S): workgroup (c, s) sums its share of the B*HW elements of channel c
+__global__ void moments_partial_kernel(const float* __restrict__ x, int B, int C, int HW, int S,
+                                       double* __restrict__ ws) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    const long long per = (long long)B * HW;
+    const long long lo = per * s / S, hi = per * (s + 1) / S;
+    double s1 = 0.0, s2 = 0.0;
+    for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const long long b = i / HW, q = i - b * HW;
+        const double v = x[((size_t)b * C + c) * HW + q];
+        s1 += v;
+        s2 += v * v;
+    }
+    __shared__ double r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ws[((size_t)s * C + c) * 2] = r1[0];
+        ws[((size_t)s * C + c) * 2 + 1] = r2[0];
+    }
+}
+
+__global__ void moments_final_kernel(const double* __restrict__ ws, int S, int C, double count, double* moments) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s1 = 0.0, s2 = 0.0;
+    for (int s = 0; s < S; ++s) {
+        s1 += ws[((size_t)s * C + c) * 2];
+        s2 += ws[((size_t)s * C + c) * 2 + 1];
+    }
+    moments[3 * c] = count;
+    moments[3 * c + 1] = s1;
+    moments[3 * c + 2] = s2;
+}
+
+// ------------------------------------------------------------------ BatchNorm2d (+act) backward
+// g = dy * act'(act(x*scale + shift)); partial sums of g and g*x per channel
+__global__ void bn_bwd_partial_kernel(const float* __restrict__ x, const float* __restrict__ dy, int B, int C, int HW,
+                                      int S, const float* __restrict__ scale, const float* __restrict__ shift, int act,
+                                      float p, double* __restrict__ ws) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    const long long per = (long long)B * HW;
+    const long long lo = per * s / S, hi = per * (s + 1) / S;
+    const float sc = scale[c], sh = shift[c];
+    double s1 = 0.0, s2 = 0.0;
+    for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const long long b = i / HW, q = i - b * HW;
+        const size_t off = ((size_t)b * C + c) * HW + q;
+        const float xv = x[off];
+        const float z = fmaf(xv, sc, sh);
+        const float g = dy[off] * act_grad_from_out(ffc::apply_act(z, act, p), z, act, p);
+        s1 += g;
+        s2 += (double)g * xv;
+    }
+    __shared__ double r1[256], r2[256];
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            r1[threadIdx.x] += r1[threadIdx.x + o];
+            r2[threadIdx.x] += r2[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ws[((size_t)s * C + c) * 2] = r1[0];
+        ws[((size_t)s * C + c) * 2 + 1] = r2[0];
+    }
+}
+
+// per channel: mean/invstd exactly as the forward finalize (bn_se_kernels.hip finalize_channel),
+// then dx = k0*g + k1*x + k2, dgamma = sum g*xhat, dbeta = sum g
+__global__ void bn_bwd_coeff_kernel(const double* __restrict__ ws, int S, int C, const double* __restrict__ moments,
+                                    const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
+                                    const float* __restrict__ gamma, float* __restrict__ coef,
+                                    float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double sg = 0.0, sgx = 0.0;
+    for (int s = 0; s < S; ++s) {
+        sg += ws[((size_t)s * C + c) * 2];
+        sgx += ws[((size_t)s * C + c) * 2 + 1];
+    }
+    float mean, var;
+    double n = 0.0;
+    if (moments) {
+        n = moments[3 * c];
+        const double mu = moments[3 * c + 1] / n;
+        double v = moments[3 * c + 2] / n - mu * mu;
+        if (v < 0.0) v = 0.0;
+        mean = (float)mu;
+        var = (float)v;
+    } else {
+        mean = rmean[c];
+        var = rvar[c];
+    }
+    const float inv = 1.0f / sqrtf(var + eps);
+    const float gm = gamma ? gamma[c] : 1.0f;
+    const double sgxh = (sgx - (double)mean * sg) * (double)inv;   // sum g * xhat
+    if (dgamma) dgamma[c] = (float)sgxh;
+    if (dbeta) dbeta[c] = (float)sg;
+    const float k0 = gm * inv;
+    float k1 = 0.0f, k2 = 0.0f;
+    if (moments) {
+        const double a = sgxh / n * (double)inv;   // coefficient of (x - mean) * inv
+        k1 = (float)(-(double)k0 * a);
+        k2 = (float)((double)k0 * (a * (double)mean - sg / n));
+    }
+    coef[3 * c] = k0;
+    coef[3 * c + 1] = k1;
+    coef[3 * c + 2] = k2;
+}
+
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy, int C, int HW,
+                                    long long total, const float* __restrict__ scale, const float* __restrict__ shift,
+                                    int act, float p, const float* __restrict__ coef, float* __restrict__ dx) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)((i / HW) % C);
+        const float xv = x[i];
+        const float z = fmaf(xv, scale[c], shift[c]);
+        const float g = dy[i] * act_grad_from_out(ffc::apply_act(z, act, p), z, act, p);
+        dx[i] = fmaf(coef[3 * c], g, fmaf(coef[3 * c + 1], xv, coef[3 * c + 2]));
+    }
+}
+
+// ------------------------------------------------------------------ weight gradient (MFMA)
+// G[m][n*T + t] = sum_b sum_q U[b][m][q] * V[b][n][qy*s - p + kh*d][qx*s - p + kw*d]
+// (zero outside V), t = kh*k + kw, q = qy*PW + qx.  K = (b, q) flattened, 16-deep chunks staged
+// in LDS; 64x64 tile per workgroup, 4 waves of one 32x32 v_mfma_f32_32x32x2_f32 tile each.
+// grid (tiles_n, tiles_m, S): split z reduces samples [B*z/S, B*(z+1)/S) into ws[z] (or into
+// G directly when S == 1).
+constexpr int WG_BK = 16;
+constexpr int WG_LD = WG_BK + 1;
+
+struct WgradArgs {
+    const float* U;
+    const float* V;
+    float* out;   // ws [S][Mu][NT] or G
+    int B, Mu, PH, PW, Nv, VH, VW, k, s, p, d, S;
+};
+
+__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+    __shared__ float As[64 * WG_LD];
+    __shared__ float Bs[64 * WG_LD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int T = a.k * a.k, NT = a.Nv * T, P = a.PH * a.PW;
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64, z = blockIdx.z;
+    const int b_lo = (int)((long long)a.B * z / a.S), b_hi = (int)((long long)a.B * (z + 1) / a.S);
+    const long long K0 = (long long)b_lo * P, K1 = (long long)b_hi * P;
+    const size_t VP = (size_t)a.VH * a.VW;
+    // this thread's k column and its 4 rows (A) / 4 columns (B) of every chunk
+    const int kc = tid & 15, rbase = tid >> 4;
+    int vn[4], vky[4], vkx[4];
+    bool vok[4], aok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int col = n0 + rbase + 16 * r;
+        vok[r] = col < NT;
+        const int n = vok[r] ? col / T : 0, t = vok[r] ? col - n * T : 0;
+        vn[r] = n;
+        vky[r] = (t / a.k) * a.d - a.p;
+        vkx[r] = (t % a.k) * a.d - a.p;
+        aok[r] = m0 + rbase + 16 * r < a.Mu;
+    }
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    const int h = lane >> 5, cl = lane & 31;
+    float av[4], bv[4];
+    auto load_chunk = [&](long long kk0) {
+        const long long kk = kk0 + kc;
+        if (kk < K1) {
+            const int b = (int)(kk / P), q = (int)(kk - (long long)b * P);
+            const int qy = q / a.PW, qx = q - qy * a.PW;
+            const float* Ub = a.U + ((size_t)b * a.Mu) * P + q;
+            const float* Vb = a.V + (size_t)b * a.Nv * VP;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                av[r] = aok[r] ? Ub[(size_t)(m0 + rbase + 16 * r) * P] : 0.0f;
+                const int iy = qy * a.s + vky[r], ix = qx * a.s + vkx[r];
+                bv[r] = (vok[r] && iy >= 0 && iy < a.VH && ix >= 0 && ix < a.VW)
+                            ? Vb[(size_t)vn[r] * VP + (size_t)iy * a.VW + ix] : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) av[r] = bv[r] = 0.0f;
+        }
+    };
+    if (K0 < K1) load_chunk(K0);
+    for (long long kk0 = K0; kk0 < K1; kk0 += WG_BK) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            As[(rbase + 16 * r) * WG_LD + kc] = av[r];
+            Bs[(rbase + 16 * r) * WG_LD + kc] = bv[r];
+        }
+        __syncthreads();
+        if (kk0 + WG_BK < K1) load_chunk(kk0 + WG_BK);   // next chunk's loads overlap this chunk's MFMAs
+#pragma unroll
+        for (int st = 0; st < WG_BK / 2; ++st) {
+            const float x = As[(wm + cl) * WG_LD + 2 * st + h];
+            const float y = Bs[(wn + cl) * WG_LD + 2 * st + h];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
+        }
+    }
+    float* out = a.out + (size_t)z * a.Mu * NT;
+    const int col = n0 + wn + cl;
+    if (col < NT) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (m < a.Mu) out[(size_t)m * NT + col] = acc[r];
+        }
+    }
+}
+
+__global__ void split_sum_kernel(const float* __restrict__ ws, int S, long long n, float* __restrict__ out,
+                                 int accumulate) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        float v = 0.0f;
+        for (int s = 0; s < S; ++s) v += ws[(size_t)s * n + i];
+        out[i] = accumulate ? out[i] + v : v;
+    }
+}
+
+// ------------------------------------------------------------------ planar 2-D real DFTs
+// One workgroup handles NPW planes.  Twiddles tw[j] = exp(-2 pi i j / N) in LDS (fp64 sincospi
+// rounded once).  Direct DFT sums: plane sizes on the training path are 4..64 per side.
+constexpr int DFT_MAXN = 64;
+
+__device__ __forceinline__ void make_twiddles(float2* tw, int N, int tid, int nt) {
+    for (int j = tid; j < N; j += nt) {
+        double sn, cs;
+        sincospi(2.0 * j / N, &sn, &cs);
+        tw[j] = make_float2((float)cs, (float)-sn);
+    }
+}
+
+__device__ __forceinline__ float interior_weight(int kw, int W) {
+    return (kw == 0 || 2 * kw == W) ? 0.0f : 1.0f;   // 1 where the bin has a Hermitian mirror
+}
+
+// x planes (P, H, W) -> Z: Re of plane p at Z + 2p*H*W', Im at Z + (2p+1)*H*W'
+__global__ __launch_bounds__(256) void rfft2_kernel(const float* __restrict__ x, int P, int H, int W, int NPW,
+                                                    float iscale, float* __restrict__ Z) {
+    extern __shared__ float smem[];
+    const int Wp = W / 2 + 1, HWp = H * Wp, HW = H * W;
+    float2* twW = reinterpret_cast<float2*>(smem);
+    float2* twH = twW + DFT_MAXN;
+    float* xs = reinterpret_cast<float*>(twH + DFT_MAXN);          // NPW * HW
+    float2* R = reinterpret_cast<float2*>(xs + NPW * HW);          // NPW * HWp
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.x * NPW;
+    const int np = min(NPW, P - p0);
+    make_twiddles(twW, W, tid, 256);
+    make_twiddles(twH, H, tid, 256);
+    for (int i = tid; i < np * HW; i += 256) xs[i] = x[(size_t)p0 * HW + i];
+    __syncthreads();
+    // rows: R[h][kw] = sum_w x[h][w] e^{-2 pi i kw w / W}
+    for (int i = tid; i < np * HWp; i += 256) {
+        const int pl = i / HWp, r = i - pl * HWp, hh = r / Wp, kw = r - hh * Wp;
+        const float* row = xs + pl * HW + hh * W;
+        float re = 0.0f, im = 0.0f;
+        int j = 0;
+        for (int w = 0; w < W; ++w) {
+            const float2 t = twW[j];
+            re = fmaf(row[w], t.x, re);
+            im = fmaf(row[w], t.y, im);
+            j += kw;
+            if (j >= W) j -= W;
+        }
+        R[i] = make_float2(re, im);
+    }
+    __syncthreads();
+    const float norm = rsqrtf((float)HW);
+    for (int i = tid; i < np * HWp; i += 256) {
+        const int pl = i / HWp, r = i - pl * HWp, kh = r / Wp, kw = r - kh * Wp;
+        const float2* col = R + pl * HWp + kw;
+        float re = 0.0f, im = 0.0f;
+        int j = 0;
+        for (int hh = 0; hh < H; ++hh) {
+            const float2 t = twH[j], v = col[hh * Wp];
+            re = fmaf(v.x, t.x, fmaf(-v.y, t.y, re));
+            im = fmaf(v.x, t.y, fmaf(v.y, t.x, im));
+            j += kh;
+            if (j >= H) j -= H;
+        }
+        const float sc = norm * (interior_weight(kw, W) > 0.0f ? iscale : 1.0f);
+        const size_t base = (size_t)(p0 + pl) * 2 * HWp + r;
+        Z[base] = re * sc;
+        Z[base + HWp] = im * sc;
+    }
+}
+
+// Z planes -> y (P, H, W) = irfftn(s=(H,W), ortho) [+ addend]; interior bins x iscale
+__global__ __launch_bounds__(256) void irfft2_kernel(const float* __restrict__ Z, int P, int H, int W, int NPW,
+                                                     float iscale, const float* __restrict__ addend,
+                                                     float* __restrict__ y) {
+    extern __shared__ float smem[];
+    const int Wp = W / 2 + 1, HWp = H * Wp, HW = H * W;
+    float2* twW = reinterpret_cast<float2*>(smem);
+    float2* twH = twW + DFT_MAXN;
+    float2* Xs = twH + DFT_MAXN;            // NPW * HWp
+    float2* R = Xs + NPW * HWp;             // NPW * HWp
+    const int tid = threadIdx.x;
+    const int p0 = blockIdx.x * NPW;
+    const int np = min(NPW, P - p0);
+    make_twiddles(twW, W, tid, 256);
+    make_twiddles(twH, H, tid, 256);
+    for (int i = tid; i < np * HWp; i += 256) {
+        const int pl = i / HWp, r = i - pl * HWp;
+        const size_t base = (size_t)(p0 + pl) * 2 * HWp + r;
+        Xs[i] = make_float2(Z[base], Z[base + HWp]);
+    }
+    __syncthreads();
+    // columns: R[h][kw] = sum_kh X[kh][kw] e^{+2 pi i kh h / H}
+    for (int i = tid; i < np * HWp; i += 256) {
+        const int pl = i / HWp, r = i - pl * HWp, hh = r / Wp, kw = r - hh * Wp;
+        const float2* col = Xs + pl * HWp + kw;
+        float re = 0.0f, im = 0.0f;
+        int j = 0;
+        for (int kh = 0; kh < H; ++kh) {
+            const float2 t = twH[j], v = col[kh * Wp];   // conj twiddle: (t.x, -t.y)
+            re = fmaf(v.x, t.x, fmaf(v.y, t.y, re));
+            im = fmaf(v.y, t.x, fmaf(-v.x, t.y, im));
+            j += hh;
+            if (j >= H) j -= H;
+        }
+        const float wgt = interior_weight(kw, W) > 0.0f ? 2.0f * iscale : 1.0f;
+        R[i] = make_float2(re * wgt, im * wgt);
+    }
+    __syncthreads();
+    // rows (C2R): y[h][w] = sum_kw Re(R[h][kw] e^{+2 pi i kw w / W}); Im of kw=0, W/2 drops out
+    const float norm = rsqrtf((float)HW);
+    for (int i = tid; i < np * HW; i += 256) {
+        const int pl = i / HW, r = i - pl * HW, hh = r / W, w = r - hh * W;
+        const float2* row = R + pl * HWp + hh * Wp;
+        float acc = 0.0f;
+        int j = 0;
+        for (int kw = 0; kw < Wp; ++kw) {
+            const float2 t = twW[j], v = row[kw];
+            acc = fmaf(v.x, t.x, fmaf(v.y, t.y, acc));   // Re(v * conj(t))
+            j += w;
+            if (j >= W) j -= W;
+        }
+        const size_t o = (size_t)(p0 + pl) * HW + r;
+        float outv = acc * norm;
+        if (addend) outv += addend[o];
+        y[o] = outv;
+    }
+}
+
+// ------------------------------------------------------------------ SELayer backward
+// One workgroup per sample.  Forward (spectral_transform.py:23-28): m = mean_HW x, h = relu(W1 m),
+// g = sigmoid(W2 h), out = x * g.  Writes dx, and the per-sample vectors the weight gradients
+// need: dpre2 (B, C) = d(W2 h), hact (B, hid), dpre1 (B, hid) = d(W1 m), mean (B, C).
+__global__ __launch_bounds__(256) void se_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dout,
+                                                     int C, int HW, const float* __restrict__ w1,
+                                                     const float* __restrict__ w2, int hid, float* __restrict__ dx,
+                                                     float* __restrict__ dpre2, float* __restrict__ hact_o,
+                                                     float* __restrict__ dpre1, float* __restrict__ mean_o) {
+    extern __shared__ float sm[];
+    float* mean = sm;            // C
+    float* dot = mean + C;       // C
+    float* gate = dot + C;       // C
+    float* dmean = gate + C;     // C
+    float* hpre = dmean + C;     // hid
+    float* dp1 = hpre + 32;      // hid
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* xb = x + (size_t)b * C * HW;
+    const float* db = dout + (size_t)b * C * HW;
+    for (int c = wave; c < C; c += 4) {
+        float s = 0.0f, q = 0.0f;
+        for (int i = lane; i < HW; i += 64) {
+            const float xv = xb[(size_t)c * HW + i];
+            s += xv;
+            q = fmaf(db[(size_t)c * HW + i], xv, q);
+        }
+        s = ffc::wave_sum(s);
+        q = ffc::wave_sum(q);
+        if (lane == 0) {
+            mean[c] = s / (float)HW;
+            dot[c] = q;
+        }
+    }
+    __syncthreads();
+    if (hid > 0) {
+        if (tid < hid) {
+            float s = 0.0f;
+            for (int c = 0; c < C; ++c) s = fmaf(w1[(size_t)tid * C + c], mean[c], s);
+            hpre[tid] = s;
+        }
+        __syncthreads();
+        for (int c = tid; c < C; c += 256) {
+            float s = 0.0f;
+            for (int j = 0; j < hid; ++j) s = fmaf(w2[(size_t)c * hid + j], fmaxf(hpre[j], 0.0f), s);
+            const float g = 1.0f / (1.0f + expf(-s));
+            gate[c] = g;
+            const float d2 = dot[c] * g * (1.0f - g);
+            dot[c] = d2;
+            dpre2[(size_t)b * C + c] = d2;
+            mean_o[(size_t)b * C + c] = mean[c];
+        }
+        __syncthreads();
+        if (tid < hid) {
+            float s = 0.0f;
+            for (int c = 0; c < C; ++c) s = fmaf(w2[(size_t)c * hid + tid], dot[c], s);
+            const float d1 = hpre[tid] > 0.0f ? s : 0.0f;
+            dp1[tid] = d1;
+            dpre1[(size_t)b * hid + tid] = d1;
+            hact_o[(size_t)b * hid + tid] = fmaxf(hpre[tid], 0.0f);
+        }
+        __syncthreads();
+        for (int c = tid; c < C; c += 256) {
+            float s = 0.0f;
+            for (int j = 0; j < hid; ++j) s = fmaf(w1[(size_t)j * C + c], dp1[j], s);
+            dmean[c] = s / (float)HW;
+        }
+    } else {
+        for (int c = tid; c < C; c += 256) {
+            gate[c] = 0.5f;   // Linear(C, 0) -> zeros -> sigmoid(0)
+            dmean[c] = 0.0f;
+        }
+    }
+    __syncthreads();
+    float* dxb = dx + (size_t)b * C * HW;
+    for (size_t i = tid; i < (size_t)C * HW; i += 256) {
+        const int c = (int)(i / HW);
+        dxb[i] = fmaf(db[i], gate[c], dmean[c]);
+    }
+}
+
+// ------------------------------------------------------------------ 2x2 pool / x2 nearest upsample
+__global__ void pool2_kernel(const float* __restrict__ x, long long P, int H, int W, float scale,
+                             float* __restrict__ y) {
+    const int h = H / 2, w = W / 2;
+    const long long n = P * h * w;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const long long pl = i / ((long long)h * w);
+        const int r = (int)(i - pl * h * w), yy = r / w, xx = r - yy * w;
+        const float* s = x + (size_t)pl * H * W + (size_t)(2 * yy) * W + 2 * xx;
+        y[i] = (s[0] + s[1] + s[W] + s[W + 1]) * scale;
+    }
+}
+
+__global__ void up2_kernel(const float* __restrict__ x, long long P, int h, int w, float scale,
+                           float* __restrict__ y) {
+    const int H = 2 * h, W = 2 * w;
+    const long long n = P * H * W;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const long long pl = i / ((long long)H * W);
+        const int r = (int)(i - pl * H * W), yy = r / W, xx = r - yy * W;
+        y[i] = x[(size_t)pl * h * w + (size_t)(yy >> 1) * w + (xx >> 1)] * scale;
+    }
+}
+
+int grid_for(long long n) { return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
+
+int dft_npw(int H, int W) { return std::max(1, std::min(64, 1024 / (H * W))); }
+
+size_t dft_lds(int H, int W, int npw, bool inverse) {
+    const size_t Wp = W / 2 + 1;
+    size_t b = 2 * DFT_MAXN * sizeof(float2);
+    if (inverse) b += 2 * (size_t)npw * H * Wp * sizeof(float2);
+    else b += (size_t)npw * H * W * sizeof(float) + (size_t)npw * H * Wp * sizeof(float2);
+    return b;
+}
+
+}  // namespace
+
+extern "C" int ffc_act_bwd(const float* t, const float* dy, float* dx, long long n, int act, float act_param,
+                           void* stream) {
+    FFC_CHECK_ARG(t && dy && dx && n > 0 && act >= 0 && act <= FFC_ACT_GELU, "ffc_act_bwd: bad args");
+    hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, t, dy, dx, n, act,
+                       act_param);
+    return ffc::launch_status("ffc_act_bwd");
+}
+
+extern "C" int ffc_reduce_splits(int B, int C, int HW) {
+    // splits per channel so that C * S workgroups fill the chip, each with >= 1024 elements
+    const long long per = (long long)B * HW;
+    int S = (int)std::max<long long>(1, std::min<long long>(per / 1024, (1024 + C - 1) / C));
+    return std::min(S, 256);
+}
+
+extern "C" int ffc_channel_moments(const float* x, int B, int C, int HW, double* ws, int S, double* moments,
+                                   void* stream) {
+    FFC_CHECK_ARG(x && ws && moments && B > 0 && C > 0 && HW > 0 && S > 0, "ffc_channel_moments: bad args");
+    hipLaunchKernelGGL(moments_partial_kernel, dim3(C, S), dim3(256), 0, (hipStream_t)stream, x, B, C, HW, S, ws);
+    hipLaunchKernelGGL(moments_final_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws, S, C,
+                       (double)B * HW, moments);
+    return ffc::launch_status("ffc_channel_moments");
+}
+
+extern "C" int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW, const float* scale,
+                          const float* shift, int act, float act_param, const double* moments, const float* rmean,
+                          const float* rvar, float eps, const float* gamma, double* ws, int S, float* coef,
+                          float* dgamma, float* dbeta, float* dx, void* stream) {
+    FFC_CHECK_ARG(x && dy && scale && shift && ws && coef && B > 0 && C > 0 && HW > 0 && S > 0,
+                  "ffc_bn_bwd: bad args");
+    FFC_CHECK_ARG(moments || (rmean && rvar), "ffc_bn_bwd: need batch moments or running stats");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(C, S), dim3(256), 0, s, x, dy, B, C, HW, S, scale, shift, act,
+                       act_param, ws);
+    hipLaunchKernelGGL(bn_bwd_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, moments, rmean, rvar,
+                       eps, gamma, coef, dgamma, dbeta);
+    if (dx) {
+        const long long total = (long long)B * C * HW;
+        hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, s, x, dy, C, HW, total, scale,
+                           shift, act, act_param, coef, dx);
+    }
+    return ffc::launch_status("ffc_bn_bwd");
+}
+
+extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const float* V, int Nv, int VH, int VW, int B,
+                              int k, int stride, int pad, int dil, int S, float* ws, float* dW, int accumulate,
+                              void* stream) {
+    FFC_CHECK_ARG(U && V && dW && Mu > 0 && Nv > 0 && PH > 0 && PW > 0 && VH > 0 && VW > 0 && B > 0 && k > 0 &&
+                      stride > 0 && dil > 0 && S >= 1 && S <= B,
+                  "ffc_conv_wgrad: bad args");
+    FFC_CHECK_ARG(S == 1 || ws, "ffc_conv_wgrad: split-K needs a workspace");
+    const int NT = Nv * k * k;
+    WgradArgs a{U, V, (S == 1 && !accumulate) ? dW : ws, B, Mu, PH, PW, Nv, VH, VW, k, stride, pad, dil, S};
+    FFC_CHECK_ARG(a.out, "ffc_conv_wgrad: accumulate needs a workspace");
+    dim3 grid((NT + 63) / 64, (Mu + 63) / 64, S);
+    hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+    if (a.out != dW) {
+        const long long n = (long long)Mu * NT;
+        hipLaunchKernelGGL(split_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, S, n, dW,
+                           accumulate);
+    }
+    return ffc::launch_status("ffc_conv_wgrad");
+}
+
+extern "C" int ffc_rfft2_planes(const float* x, int P, int H, int W, float interior_scale, float* Z, void* stream) {
+    FFC_CHECK_ARG(x && Z && P > 0 && H >= 1 && W >= 2 && H <= DFT_MAXN && W <= DFT_MAXN,
+                  "ffc_rfft2_planes: planes up to 64x64");
+    const int npw = dft_npw(H, W);
+    hipLaunchKernelGGL(rfft2_kernel, dim3((P + npw - 1) / npw), dim3(256), dft_lds(H, W, npw, false),
+                       (hipStream_t)stream, x, P, H, W, npw, interior_scale, Z);
+    return ffc::launch_status("ffc_rfft2_planes");
+}
+
+extern "C" int ffc_irfft2_planes(const float* Z, int P, int H, int W, float interior_scale, const float* addend,
+                                 float* y, void* stream) {
+    FFC_CHECK_ARG(Z && y && P > 0 && H >= 1 && W >= 2 && H <= DFT_MAXN && W <= DFT_MAXN,
+                  "ffc_irfft2_planes: planes up to 64x64");
+    const int npw = dft_npw(H, W);
+    hipLaunchKernelGGL(irfft2_kernel, dim3((P + npw - 1) / npw), dim3(256), dft_lds(H, W, npw, true),
+                       (hipStream_t)stream, Z, P, H, W, npw, interior_scale, addend, y);
+    return ffc::launch_status("ffc_irfft2_planes");
+}
+
+extern "C" int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H, int W, const float* w1,
+                          const float* w2, int hidden, float* dx, float* dpre2, float* hact, float* dpre1, float* mean,
+                          void* stream) {
+    FFC_CHECK_ARG(x && dout && dx && B > 0 && C > 0 && H > 0 && W > 0 && hidden >= 0 && hidden <= 32,
+                  "ffc_se_bwd: bad args");
+    FFC_CHECK_ARG(hidden == 0 || (w1 && w2 && dpre2 && hact && dpre1 && mean), "ffc_se_bwd: missing buffers");
+    const size_t lds = (4 * (size_t)C + 64) * sizeof(float);
+    FFC_CHECK_ARG(lds <= 64 * 1024, "ffc_se_bwd: too many channels");
+    hipLaunchKernelGGL(se_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, x, dout, C, H * W, w1, w2, hidden,
+                       dx, dpre2, hact, dpre1, mean);
+    return ffc::launch_status("ffc_se_bwd");
+}
+
+extern "C" int ffc_pool2(const float* x, long long P, int H, int W, float scale, float* y, void* stream) {
+    FFC_CHECK_ARG(x && y && P > 0 && H >= 2 && W >= 2 && H % 2 == 0 && W % 2 == 0, "ffc_pool2: bad args");
+    hipLaunchKernelGGL(pool2_kernel, dim3(grid_for(P * H * W / 4)), dim3(256), 0, (hipStream_t)stream, x, P, H, W,
+                       scale, y);
+    return ffc::launch_status("ffc_pool2");
+}
+
+extern "C" int ffc_up2(const float* x, long long P, int h, int w, float scale, float* y, void* stream) {
+    FFC_CHECK_ARG(x && y && P > 0 && h > 0 && w > 0, "ffc_up2: bad args");
+    hipLaunchKernelGGL(up2_kernel, dim3(grid_for(P * h * w * 4)), dim3(256), 0, (hipStream_t)stream, x, P, h, w,
+                       scale, y);
+    return ffc::launch_status("ffc_up2");
+}

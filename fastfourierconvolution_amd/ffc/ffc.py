@@ -11,6 +11,7 @@ reference semantics: they return their input (usually the int 0 of the tuple pro
 import torch
 import torch.nn as nn
 
+from .. import _autograd as ag
 from .. import _plan
 from .. import _runtime as rt
 from .spectral_transform import SpectralTransform
@@ -47,6 +48,8 @@ class _FFCExec:
         """noise: optional {"l"|"g": (NoiseInjection, noise tensor or None)} applied after the branch's
         BN + activation in the same pass (FFC_BN_ACT followed by the fgan128 NoiseInjection)"""
         x_l, x_g = x if type(x) is tuple else (x, 0)
+        if ag.wants_grad(self, x_l, x_g):
+            return self._run_train(x_l, x_g, y, act_l, act_g, bn_l, bn_g, noise)
         if isinstance(x_l, torch.Tensor):
             x_l = rt.require(x_l, "x_l")
         if isinstance(x_g, torch.Tensor):
@@ -111,6 +114,71 @@ class _FFCExec:
                 self.convg2g.conv2.out_channels if isinstance(self.convg2g, SpectralTransform) else None)
             branches.append(("g", segs, w, inp, add, act_g, bn_g, M))
         return self._launch_branches(branches, B, dev, stream, noise)
+
+    def _run_train(self, x_l, x_g, y, act_l, act_g, bn_l, bn_g, noise):
+        """training path (autograd recording): the layer's local convs and ST conv2 as one
+        _ConvLayerFn (both output branches; their data gradients w.r.t. x_l in one adjoint launch),
+        SpectralTransform through its per-op Functions, BN + activation as _BNActFn
+        (include/ffc_amd.h "training path")."""
+        if y is not None:
+            raise TypeError("FFC: the conditional (y) path is not supported (the reference raises in "
+                            "FourierUnitSN, fourier_unity.py:46-47)")
+        if noise:
+            raise NotImplementedError("NoiseInjection on the training path")
+        for t, n in ((x_l, "x_l"), (x_g, "x_g")):
+            if isinstance(t, torch.Tensor):
+                rt.require(t, n)
+        ref = x_l if isinstance(x_l, torch.Tensor) else x_g
+        if not isinstance(ref, torch.Tensor):
+            raise TypeError("FFC input has no tensor branch")
+        B = ref.shape[0]
+        inputs, idx, outs, edges, names = [], {}, [], [], []
+
+        def inp(t):
+            if id(t) not in idx:
+                idx[id(t)] = len(inputs)
+                inputs.append(t.contiguous())
+            return idx[id(t)]
+
+        def branch(parts, extra=None):
+            convs = []
+            for mod, t in parts:
+                if isinstance(mod, (nn.Conv2d, nn.ConvTranspose2d)):
+                    if not isinstance(t, torch.Tensor):
+                        raise TypeError(f"{type(mod).__name__} got {type(t).__name__} input")
+                    convs.append((mod, t))
+                elif isinstance(t, torch.Tensor):
+                    raise NotImplementedError("identity pass-through of a tensor on the training path")
+            return convs + ([extra] if extra else [])
+
+        for name, parts, extra, act, bn in (
+                ("l", [(self.convl2l, x_l), (self.convg2l, x_g)], None, act_l, bn_l),
+                ("g", [(self.convl2g, x_l)], "st", act_g, bn_g)):
+            if (name == "l" and self.ratio_gout == 1) or (name == "g" and self.ratio_gout == 0):
+                continue
+            ex = None
+            if extra and isinstance(self.convg2g, SpectralTransform) and isinstance(x_g, torch.Tensor):
+                v = ag.spectral_v(self.convg2g, x_g)
+                ex = (self.convg2g.conv2, v, _plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]))
+            elif extra and not isinstance(self.convg2g, nn.Identity):
+                raise NotImplementedError(type(self.convg2g).__name__)
+            convs = branch(parts)
+            if not convs and ex is None:
+                continue
+            j = len(outs)
+            M = (convs[0][0] if convs else ex[0]).out_channels
+            outs.append((M,) + (tuple(act) if bn is None else (0, 0.0)))
+            for mod, t in convs:
+                edges.append((j, inp(t), rt.conv_seg(mod, t), mod))
+            if ex is not None:
+                edges.append((j, inp(ex[1]), ex[2], ex[0]))
+            names.append((name, act, bn))
+        res = {"l": 0, "g": 0}
+        if outs:
+            ys = ag.conv_layer(self._ffc_cache(), B, outs, edges, inputs)
+            for (name, act, bn), yv in zip(names, ys):
+                res[name] = ag.bn_act(bn, yv, act) if bn is not None else yv
+        return res["l"], res["g"]
 
     def _launch_branches(self, branches, B, dev, stream, noise=None):
         """plan / pack / launch the GEMM(s) of the given branches (one launch per kernel kind),

@@ -7,6 +7,7 @@ rfftn -> 1x1 conv -> BatchNorm2d -> ReLU -> irfftn.
 import torch
 import torch.nn as nn
 
+from .. import _autograd as ag
 from .. import _runtime as rt
 from .._lib import check, ptr
 
@@ -144,4 +145,7 @@ class FourierUnitSN(nn.Module):
         if y is not None:
             # reference: self.bn(ffted, y) -> BatchNorm2d.forward() takes 1 input (fourier_unity.py:46-47)
             raise TypeError("FourierUnitSN: the conditional (y) path is not supported (the reference raises here)")
-        return self._run(rt.require(x, "x"))
+        x = rt.require(x, "x")
+        if ag.wants_grad(self, x):
+            return ag.fourier_unit(self, x, residual=False)
+        return self._run(x)

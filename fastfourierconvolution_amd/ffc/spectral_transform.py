@@ -18,6 +18,7 @@ resolution; the running-var unbiasing uses the upsampled count (count_mult = 4).
 import torch
 import torch.nn as nn
 
+from .. import _autograd as ag
 from .. import _plan
 from .. import _runtime as rt
 from .._lib import check, ptr
@@ -51,6 +52,8 @@ class SELayer(nn.Module):
     def forward(self, x):
         """x * sigmoid(fc(avg_pool(x))) as one per-(b, c) scale launch."""
         x = rt.require(x, "x")
+        if ag.wants_grad(self, x):
+            return ag.se_layer(self, x)
         g = self.gate(x, False)
         B, C, H, W = x.shape
         zeros = torch.zeros(B * C, device=x.device, dtype=torch.float32)
@@ -164,6 +167,12 @@ class SpectralTransform(nn.Module):
         if y is not None:
             raise TypeError("SpectralTransform: the conditional (y) path is not supported (the reference raises "
                             "in FourierUnitSN, fourier_unity.py:46-47)")
+        if ag.wants_grad(self, x):
+            v = ag.spectral_v(self, rt.require(x, "x"))
+            cache = self.__dict__.setdefault("_train_cache", {})
+            (out,) = ag.conv_layer(cache, v.shape[0], [(self.conv2.out_channels, 0, 0.0)],
+                                   [(0, 0, _plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]), self.conv2)], [v])
+            return out
         v = self.spectral(x)
         rt.sn_refresh(self.conv2)
         B, c, H, W = v.shape

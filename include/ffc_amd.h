@@ -298,6 +298,60 @@ int ffc_noise_inject(const float* x, const float* weight, const float* noise, fl
  * (the reference's clamp to the tensor's own min/max is the identity); n % 4 == 0 */
 int ffc_quantize_u8(const float* x, unsigned char* out, long long n, void* stream);
 
+
+/* ------------------------------------------------------------------ training path (config 3)
+ * Backward of the FFC operator surface for custom-op autograd (torch.autograd.Function per
+ * reference op; the reference differentiates through ATen).  Data gradients of every conv /
+ * convT / 1x1 run on ffc_conv_forward / ffc_convp_forward with the adjoint segment and the
+ * same weight tensor under the other layout; the entry points below cover the rest.
+ * Workspaces (ws) are caller-owned scratch; S = number of splits (see ffc_reduce_splits). */
+
+/* dx = dy * act'(.) for FFC_BN_ACT's activation (ffc_bn_act.py:63-67, ST act1, FU relu).
+ * t is the activation OUTPUT for ReLU/LeakyReLU/Tanh/Sigmoid and its INPUT for GELU. */
+int ffc_act_bwd(const float* t, const float* dy, float* dx, long long n, int act, float act_param, void* stream);
+/* splits per channel for the per-channel reductions below (grid C x S) */
+int ffc_reduce_splits(int B, int C, int HW);
+/* BatchNorm2d batch moments (nn.BatchNorm2d train forward): moments[C][3] = {n, sum x, sum x^2}
+ * in fp64, the input of ffc_bn_finalize; ws: S*C*2 doubles */
+int ffc_channel_moments(const float* x, int B, int C, int HW, double* ws, int S, double* moments, void* stream);
+/* BatchNorm2d (+ following activation) backward: y = act(x*scale + shift) with scale/shift from
+ * ffc_bn_finalize.  Train (moments != NULL): dx = gamma*inv*(g - mean(g) - xhat*mean(g*xhat));
+ * eval (rmean, rvar: running stats the forward used): dx = gamma*inv*g.  dgamma = sum g*xhat,
+ * dbeta = sum g (either may be NULL), dx may be NULL.  ws: S*C*2 doubles, coef: C*3 floats. */
+int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW, const float* scale, const float* shift,
+               int act, float act_param, const double* moments, const float* rmean, const float* rvar, float eps,
+               const float* gamma, double* ws, int S, float* coef, float* dgamma, float* dbeta, float* dx,
+               void* stream);
+/* Weight gradient of nn.Conv2d / nn.ConvTranspose2d / 1x1 conv / nn.Linear (ffc.py:45-70,
+ * ffc_transpose.py:48-86, spectral_transform.py:23-28,52-71, fourier_unity.py:20-23):
+ *   dW[m][n][kh][kw] = sum_b sum_q U[b][m][q] * V[b][n][qy*stride - pad + kh*dil][qx*stride - pad + kw*dil]
+ * U (B, Mu, PH, PW), V (B, Nv, VH, VW), zero outside V.  Conv2d: U = dy, V = x -> (Cout, Cin, k, k);
+ * ConvTranspose2d: U = x, V = dy -> (Cin, Cout, k, k).  Split-K over samples into ws
+ * (S * Mu * Nv*k*k floats; unused when S == 1 and accumulate == 0); accumulate adds into dW. */
+int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const float* V, int Nv, int VH, int VW, int B, int k,
+                   int stride, int pad, int dil, int S, float* ws, float* dW, int accumulate, void* stream);
+/* rfftn(x, dim=(-2,-1), norm="ortho") of P planes (P, H, W) into the interleaved Re/Im planes of
+ * fourier_unity.py:38-42: Re of plane p at Z[2p], Im at Z[2p+1], each H x (W/2+1).  Bins with a
+ * Hermitian mirror (0 < kw, 2kw != W) are multiplied by interior_scale (2: the adjoint of irfftn).
+ * H, W <= 64. */
+int ffc_rfft2_planes(const float* x, int P, int H, int W, float interior_scale, float* Z, void* stream);
+/* irfftn(X, s=(H,W), dim=(-2,-1), norm="ortho") (fourier_unity.py:51-56) from interleaved planes,
+ * Im of the kw = 0 and kw = W/2 bins ignored, mirrored bins x interior_scale (0.5: the adjoint of
+ * rfftn), + addend (P, H, W) when not NULL (SpectralTransform's x + fu(x), :108). H, W <= 64. */
+int ffc_irfft2_planes(const float* Z, int P, int H, int W, float interior_scale, const float* addend, float* y,
+                      void* stream);
+/* SELayer backward (spectral_transform.py:23-28), one workgroup per sample: dx, plus the
+ * per-sample vectors of the two Linear weight gradients: dpre2 (B, C), hact (B, hidden),
+ * dpre1 (B, hidden), mean (B, C).  hidden = C // 16 may be 0 (gate 0.5). */
+int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H, int W, const float* w1, const float* w2,
+               int hidden, float* dx, float* dpre2, float* hact, float* dpre1, float* mean, void* stream);
+/* y = scale * (2x2 window sum) of P planes (H, W even): AvgPool2d(2,2) with scale 0.25
+ * (spectral_transform.py:46-47), the adjoint of nearest Upsample(x2) with scale 1 */
+int ffc_pool2(const float* x, long long P, int H, int W, float scale, float* y, void* stream);
+/* y = scale * nearest x2 upsample of P planes (h, w): Upsample(scale_factor=2) with scale 1
+ * (spectral_transform.py:44-45), the adjoint of AvgPool2d(2,2) with scale 0.25 */
+int ffc_up2(const float* x, long long P, int h, int w, float scale, float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

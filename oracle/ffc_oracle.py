@@ -309,6 +309,43 @@ def sn_materialize(sd, dims, training, n_power_iterations=1, eps=1e-12):
 
 
 # ----------------------------------------------------------------------------- fixture driver
+def forward_case(case: dict, sd: dict, tin: dict, training: bool, fft="numpy") -> dict:
+    """the forward of one golden-manifest case -> {"out" | "out_l" | "out_g": tensor}"""
+    kind, ctor = case["kind"], case["ctor"]
+    if kind == "FourierUnitSN":
+        out = {"out": fourier_unit(tin["x"], sd, "", training, fft)}
+    elif kind == "SpectralTransform":
+        out = {"out": spectral_transform(tin["x"], sd, "", ctor.get("stride", 1),
+                                         ctor.get("upsample", False), training, fft)}
+    elif kind == "FFC_BN_ACT":
+        x = (tin["x_l"], tin["x_g"]) if "x_l" in tin else tin["x"]
+        ol, og = ffc_bn_act(x, sd, "", ctor, training, fft)
+        out = {}
+        if not isinstance(ol, int):
+            out["out_l"] = ol
+        if not isinstance(og, int):
+            out["out_g"] = og
+    elif kind == "FFCGenerator":
+        out = {"out": ffc_generator(tin["z"], sd, ctor["nz"], ctor["nc"], ctor["ngf"], training, fft)}
+    elif kind == "FFCDiscriminator":
+        out = {"out": ffc_discriminator(tin["x"], sd, ctor["nc"], ctor["ndf"], training, fft)}
+    elif kind == "SNFFC":
+        sn_materialize(sd, {}, training)
+        x = (tin["x_l"], tin["x_g"]) if "x_l" in tin else tin["x"]
+        ol, og = ffc(x, sd, "", ctor, training, fft)
+        out = {}
+        if not isinstance(ol, int):
+            out["out_l"] = ol
+        if not isinstance(og, int):
+            out["out_g"] = og
+    elif kind == "FGenerator":
+        noises = [(tin.get(f"noise{n}_l"), tin.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
+        out = {"out": fgan128_generator(tin["z"], sd, training, noises, fft=fft)}
+    else:
+        raise ValueError(kind)
+    return out
+
+
 def run_fixture_case(case: dict, state: dict, inputs: dict, dtype=torch.float64, fft="numpy"):
     """Run one golden-manifest case (tests/golden/manifest.json) through the oracle.
     ``state`` maps key -> numpy array (it is converted and updated in place via the
@@ -317,45 +354,39 @@ def run_fixture_case(case: dict, state: dict, inputs: dict, dtype=torch.float64,
               else torch.from_numpy(np.array(v))) for k, v in state.items()}
     tin = {k: torch.from_numpy(v).to(dtype) for k, v in inputs.items()}
     training = case["mode"] == "train"
-    kind, ctor = case["kind"], case["ctor"]
     with torch.no_grad():
-        if kind == "FourierUnitSN":
-            out = {"out": fourier_unit(tin["x"], sd, "", training, fft)}
-        elif kind == "SpectralTransform":
-            out = {"out": spectral_transform(tin["x"], sd, "", ctor.get("stride", 1),
-                                             ctor.get("upsample", False), training, fft)}
-        elif kind == "FFC_BN_ACT":
-            x = (tin["x_l"], tin["x_g"]) if "x_l" in tin else tin["x"]
-            ol, og = ffc_bn_act(x, sd, "", ctor, training, fft)
-            out = {}
-            if not isinstance(ol, int):
-                out["out_l"] = ol
-            if not isinstance(og, int):
-                out["out_g"] = og
-        elif kind == "FFCGenerator":
-            out = {"out": ffc_generator(tin["z"], sd, ctor["nz"], ctor["nc"], ctor["ngf"], training, fft)}
-        elif kind == "FFCDiscriminator":
-            out = {"out": ffc_discriminator(tin["x"], sd, ctor["nc"], ctor["ndf"], training, fft)}
-        elif kind == "SNFFC":
-            sn_materialize(sd, {}, training)
-            x = (tin["x_l"], tin["x_g"]) if "x_l" in tin else tin["x"]
-            ol, og = ffc(x, sd, "", ctor, training, fft)
-            out = {}
-            if not isinstance(ol, int):
-                out["out_l"] = ol
-            if not isinstance(og, int):
-                out["out_g"] = og
-        elif kind == "FGenerator":
-            noises = [(tin.get(f"noise{n}_l"), tin.get(f"noise{n}_g")) for n in (2, 3, 4, 5, 6)]
-            out = {"out": fgan128_generator(tin["z"], sd, training, noises, fft=fft)}
-        else:
-            raise ValueError(kind)
+        out = forward_case(case, sd, tin, training, fft)
     return out, sd
+
+
+PARAM_SUFFIXES = ("running_mean", "running_var", "num_batches_tracked", "weight_u", "weight_v")
+
+
+def grad_case(case: dict, state: dict, inputs: dict, cots: dict, dtype=torch.float64):
+    """Gradients of  loss = sum_k <out_k, cot_k>  for one case, by torch autograd through the
+    op-for-op restatement (torch.fft, fp64): the reference differentiates the same ops through
+    ATen (config 3, fwd+bwd).  -> (grads of inputs {name: t}, grads of parameters {key: t})."""
+    sd = {k: (torch.from_numpy(np.array(v)).to(dtype) if np.asarray(v).dtype.kind == "f"
+              else torch.from_numpy(np.array(v))) for k, v in state.items()}
+    params = [k for k, v in sd.items() if v.is_floating_point() and not k.endswith(PARAM_SUFFIXES)]
+    for k in params:
+        sd[k].requires_grad_(True)
+    tin = {k: torch.from_numpy(v).to(dtype).requires_grad_(True) for k, v in inputs.items()}
+    with torch.enable_grad():
+        out = forward_case(case, sd, tin, case["mode"] == "train", fft="torch")
+        loss = sum((out[k] * torch.from_numpy(cots[k]).to(dtype)).sum() for k in out)
+        names = list(tin) + params
+        gs = torch.autograd.grad(loss, [tin[k] for k in tin] + [sd[k] for k in params], allow_unused=True)
+    gin = {k: g for k, g in zip(names[:len(tin)], gs[:len(tin)]) if g is not None}
+    gpar = {k: g for k, g in zip(params, gs[len(tin):]) if g is not None}
+    return gin, gpar
 
 
 def normwise_err(a, ref) -> float:
     """max|a-ref| / max|ref| — the parity metric of SURVEY.md §8c."""
     a = a.detach().double() if isinstance(a, torch.Tensor) else torch.as_tensor(a).double()
     ref = ref.detach().double() if isinstance(ref, torch.Tensor) else torch.as_tensor(ref).double()
+    if ref.numel() == 0:
+        return 0.0 if a.numel() == 0 else float("inf")
     den = ref.abs().max().item()
     return (a - ref).abs().max().item() / (den if den > 0 else 1.0)

@@ -82,3 +82,13 @@ def call_dropin(case, mod, inputs):
                 res["out_g"] = og
             return res
         return {"out": mod(next(iter(t.values())))}
+
+
+def grad_cases():
+    """gradient fixtures (tests/golden/gen_golden_grad.py, BASELINE config 3 fwd + bwd)"""
+    with open(os.path.join(GOLDEN, "manifest_grad.json")) as f:
+        return json.load(f)["cases"]
+
+
+def grad_arrays(data, prefix):
+    return {k[len(prefix):]: data[k] for k in data.files if k.startswith(prefix)}
