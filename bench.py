@@ -43,10 +43,11 @@ PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn"], default="gen64",
+    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn", "gan64train"], default="gen64",
                    help="gen64: FFCGenerator 64x64 (BASELINE metric, configs[1]/[2]); "
                         "fgan128: fgan128 FGenerator 128x128x3 (configs[3], 64 per GPU = B 512 / 8); "
-                        "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4], 128 per GPU)")
+                        "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4], 128 per GPU); "
+                        "gan64train: generator + discriminator 64x64x3 fwd+bwd + Adam (configs[2], B=256)")
     p.add_argument("--mix", choices=["fp32", "fp16"], default=None,
                    help="spectral mix arithmetic (default: fp16 for fgan128sn, fp32 otherwise)")
     p.add_argument("--gpus", type=int, default=1)
@@ -148,8 +149,123 @@ def weights_init(m):
         nn.init.constant_(m.bias.data, 0)
 
 
+def train_main(args):
+    """BASELINE configs[2]: FFCGenerator(100, 3, 64) + FFCDiscriminator(3, 64), 64x64x3, B=256, one
+    step = z -> G -> D -> loss = mean(D(G(z))) -> backward through D and G (custom-op autograd, every
+    forward and backward op a HIP kernel of libffc_amd.so) -> Adam on both parameter sets (the
+    reference's fgan64 optimizer, lr 2e-4, betas (0.5, 0.999); torch's foreach Adam).  Train-mode
+    BN.  Single GPU (config 3 is 1x MI355X)."""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import _runtime as rt
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("gan64train is the single-GPU configs[2] workload")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G = F.FFCGenerator(args.nz, args.nc, args.ngf)
+        D = F.FFCDiscriminator(args.nc, args.ngf)
+    G.apply(weights_init)
+    D.apply(weights_init)
+    cpu_state = ({k: v.clone() for k, v in G.state_dict().items()}, {k: v.clone() for k, v in D.state_dict().items()})
+    G, D = G.to(dev).train(), D.to(dev).train()
+    opt = torch.optim.Adam(list(G.parameters()) + list(D.parameters()), lr=2e-4, betas=(0.5, 0.999), foreach=True)
+    gen = torch.Generator(device="cpu").manual_seed(100)
+    z_cpu = torch.randn((args.batch, args.nz, 1, 1), generator=gen)
+    z = z_cpu.to(dev)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = D(G(z)).mean()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    value = args.batch * args.steps / elapsed
+    obs = rt.LaunchObserver()
+    rt.set_observer(obs)
+    for _ in range(max(1, args.profile_steps)):
+        step()
+    rt.set_observer(None)
+    summ = obs.summary()
+    nprof = max(1, args.profile_steps)
+    kernels = {k: {"launches_per_step": v["launches"] / nprof, "ms_per_step": v["ms"] / nprof,
+                   "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
+    mm = {k: v for k, v in summ.items() if v["flops"] > 0}
+    dom = max(mm, key=lambda k: mm[k]["ms"])
+    d = summ[dom]
+    achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4)}
+    tr = pmc_traffic(dom, args.workload)
+    roof["traffic"] = tr["bytes_per_launch"] if tr else None
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        from oracle.ffc_oracle import ffc_discriminator, ffc_generator
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        nb = min(args.batch, 16)
+        zs = z_cpu[:nb]
+
+        def cpu_step(dt, sdg, sdd):
+            p = [v for sd in (sdg, sdd) for k, v in sd.items() if v.is_floating_point() and
+                 not k.endswith(("running_mean", "running_var"))]
+            for t in p:
+                t.grad = None
+                t.requires_grad_(True)
+            loss = ffc_discriminator(ffc_generator(zs.to(dt), sdg, args.nz, args.nc, args.ngf, True, fft="torch"),
+                                     sdd, args.nc, args.ngf, True, fft="torch").mean()
+            loss.backward()
+            return loss.item()
+        sdg = {k: v.clone() for k, v in cpu_state[0].items()}
+        sdd = {k: v.clone() for k, v in cpu_state[1].items()}
+        iters, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds or iters == 0:
+            cpu_step(torch.float32, sdg, sdd)
+            iters += 1
+        el = time.perf_counter() - t0
+        cpu = {"value": round(nb * iters / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
+               "sample": f"oracle fp32 torch-CPU G+D fwd+bwd (torch autograd through the op-for-op reference "
+                         f"path, no optimizer), B={nb}, {iters} iterations in {el:.1f}s, train-mode BN"}
+        sd64 = [{k: (v.double() if v.is_floating_point() else v.clone()) for k, v in st.items()} for st in cpu_state]
+        ref = cpu_step(torch.float64, *sd64)
+        with contextlib.redirect_stdout(io.StringIO()):
+            G2 = F.FFCGenerator(args.nz, args.nc, args.ngf)
+            D2 = F.FFCDiscriminator(args.nc, args.ngf)
+        G2.load_state_dict(cpu_state[0])
+        D2.load_state_dict(cpu_state[1])
+        got = D2.to(dev).train()(G2.to(dev).train()(zs.to(dev))).mean().item()
+        parity = {"loss_rel_err_vs_fp64_oracle": abs(got - ref) / abs(ref), "mode": f"train, B={nb}",
+                  "gradients": "layer-wise vs the fp64 oracle in tests/test_gpu_train.py (<= 1e-4 normwise)",
+                  "tolerance": 1e-4}
+    line = {
+        "metric": "FFC-DCGAN G+D fwd+bwd train step images/sec @ B=256 64x64x3 (BASELINE configs[2])",
+        "value": round(value, 1), "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
+        "config": {"workload": f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) + FFCDiscriminator("
+                               f"nc={args.nc},ndf={args.ngf}) fwd+bwd + Adam, loss = mean(D(G(z)))",
+                   "global_batch": args.batch, "per_gpu_batch": args.batch, "bn_mode": "train", "hipgraph": False,
+                   "parallelism": "dp1"},
+        "roofline": roof, "cpu_baseline": cpu, "parity": parity, "kernels": kernels,
+    }
+    print(json.dumps(line))
+
+
 def main():
     args = parse()
+    if args.workload == "gan64train":
+        if args.batch is None:
+            args.batch = 256
+        return train_main(args)
     if args.batch is None:
         args.batch = {"gen64": 256, "fgan128": 64, "fgan128sn": 128}[args.workload]
     fgan = args.workload in ("fgan128", "fgan128sn")

@@ -465,6 +465,9 @@ def fourier_unit(fu, x, residual: bool):
     """FourierUnitSN.forward (fourier_unity.py:32-56) [+ x] on the training path"""
     B, C, H, W = x.shape
     fu._check(C)
+    if fu.mix_precision != "fp32":
+        raise NotImplementedError("the training path computes the spectral mix in fp32 only (config 5's fp16 "
+                                  "mix is forward-only)")
     if H > 64 or W > 64:
         raise NotImplementedError("training-path Fourier unit: planes up to 64x64")
     Z = _RFFT2Fn.apply(x)

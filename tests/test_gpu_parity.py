@@ -146,10 +146,13 @@ def test_fu_sizes_vs_oracle(fu_path):
 def test_unsupported_plane_raises():
     import fastfourierconvolution_amd as F
     fu = F.FourierUnitSN(4, 4).cuda()
-    with pytest.raises(NotImplementedError):
-        fu(torch.randn(1, 4, 48, 48, device="cuda"))     # not a power of two
-    with pytest.raises(NotImplementedError):
-        fu(torch.randn(1, 4, 64, 128, device="cuda"))    # staged FU: square planes only
+    with torch.no_grad():                                 # the fused inference kernels
+        with pytest.raises(NotImplementedError):
+            fu(torch.randn(1, 4, 48, 48, device="cuda"))     # not a power of two
+        with pytest.raises(NotImplementedError):
+            fu(torch.randn(1, 4, 64, 128, device="cuda"))    # staged FU: square planes only
+    with pytest.raises(NotImplementedError):             # training path: direct DFTs up to 64 x 64
+        fu(torch.randn(1, 4, 128, 128, device="cuda"))
 
 
 def test_conditional_path_raises_like_reference():
