@@ -102,6 +102,61 @@ def run_conv(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0, 0.
     return out
 
 
+def smallm_route(segs, layouts, M):
+    """<= 4 output channels: 'full' (Conv2d onto a 1x1 output, ffc_conv_full_smallm), 'convT'
+    (ConvTranspose2d k4 s2 p1, ffc_convt_k4s2_smallm), else None (implicit-GEMM kernels)"""
+    if M > 4 or not 1 <= len(segs) <= 2 or not rt.USE_SMALLM:
+        return None
+    if all(sg.kind == "conv" and sg.k == sg.IH == sg.IW and sg.p == 0 and sg.d == 1 and not sg.pool and not sg.gate
+           for sg in segs) and all(lay == 0 for lay in layouts):
+        return "full"
+    if all(sg.kind == "convT" and (sg.k, sg.s, sg.p, sg.d, sg.op) == (4, 2, 1, 1, 0) for sg in segs) and \
+            all((sg.IH, sg.IW) == (segs[0].IH, segs[0].IW) for sg in segs) and sum(sg.C for sg in segs) <= 256 and \
+            all(lay == 1 for lay in layouts):
+        return "convT"
+    return None
+
+
+def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0, 0.0), addend=None):
+    """out = act(sum_s conv_s(x_s) [+ addend]) on the best kernel for the job: the small-M direct
+    kernels for <= 4 output channels, the implicit-GEMM kernels otherwise"""
+    route = None
+    if addend is None and sum(1 for w in weights if w[4] is not None) <= 1:
+        route = smallm_route(segs, [w[1] for w in weights], M)
+    if route is None:
+        return run_conv(cache, key, B, M, segs, weights, inputs, out_shape, act, addend)
+    L = rt.lib()
+    bias = next((w[4] for w in weights if w[4] is not None), None)
+    x1 = inputs[1] if len(inputs) > 1 else None
+    w1 = weights[1][0] if len(weights) > 1 else None
+    dev = inputs[0].device
+    stream = _stream(inputs[0])
+    if route == "full":
+        sg = segs[0]
+        out = torch.empty((B, M, 1, 1), device=dev, dtype=torch.float32)
+        K0 = sg.C * sg.k * sg.k
+        K1 = segs[1].C * segs[1].k * segs[1].k if x1 is not None else 0
+        with rt.observe("conv_full_smallm", flops=2.0 * B * M * (K0 + K1)):
+            check(L.ffc_conv_full_smallm(ptr(inputs[0]), K0, ptr(weights[0][0]), ptr(x1), K1, ptr(w1), ptr(bias), B, M,
+                                         ptr(out), act[0], float(act[1]), stream), "ffc_conv_full_smallm")
+        return out
+    C0, C1 = segs[0].C, (segs[1].C if x1 is not None else 0)
+    pkey = ("ctpack", key, weights[0][0].data_ptr(), weights[0][0]._version,
+            None if w1 is None else (w1.data_ptr(), w1._version))
+    wp = cache.get(pkey)
+    if wp is None:
+        for old in [k for k in cache if k[:2] == ("ctpack", key)]:
+            del cache[old]
+        wp = cache[pkey] = torch.empty(L.ffc_convt_smallm_pack_floats(C0, C1), device=dev, dtype=torch.float32)
+        check(L.ffc_convt_smallm_pack(ptr(weights[0][0]), C0, ptr(w1), C1, M, ptr(wp), stream), "ffc_convt_smallm_pack")
+    IH, IW = segs[0].IH, segs[0].IW
+    out = torch.empty((B, M, 2 * IH, 2 * IW), device=dev, dtype=torch.float32)
+    with rt.observe("convt_smallm", flops=2.0 * B * M * (C0 + C1) * 4 * (2 * IH) * (2 * IW)):
+        check(L.ffc_convt_k4s2_smallm(ptr(inputs[0]), C0, ptr(x1), C1, ptr(wp), ptr(bias), B, IH, IW, M, ptr(out),
+                                      act[0], float(act[1]), stream), "ffc_convt_k4s2_smallm")
+    return out
+
+
 def wgrad_splits(B, Mu, NT, P):
     tiles = -(-Mu // 64) * -(-NT // 64)
     S = max(1, min(B, 1024 // max(1, tiles)))
@@ -157,8 +212,8 @@ class _ConvLayerFn(torch.autograd.Function):
             segs = tuple(ed[2] for _, ed in es)
             wts = [(ws[e], ed[3], ed[2].k, ed[2].k, bs[e]) for e, ed in es]
             fused = act if act != 5 else 0
-            y = run_conv(spec.cache, ("fwd", j, spec.B, segs, tuple(ed[3] for _, ed in es)), spec.B, M, segs, wts,
-                         [xs[ed[1]] for _, ed in es], act=(fused, param))
+            y = conv_forward(spec.cache, ("fwd", j, spec.B, segs, tuple(ed[3] for _, ed in es)), spec.B, M, segs, wts,
+                             [xs[ed[1]] for _, ed in es], act=(fused, param))
             if act == 5:
                 pre = y
                 y = _act_out(pre, act, param, _stream(pre))
@@ -205,8 +260,8 @@ class _ConvLayerFn(torch.autograd.Function):
                 segs = tuple(a[1] for a in grp)
                 wts = [(ws[a[0]], 1 - a[2], a[1].k, a[1].k, None) for a in grp]
                 key = ("adj", i, tuple(a[0] for a in grp), spec.B, segs)
-                dx = run_conv(spec.cache, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
-                              addend=dx)
+                dx = conv_forward(spec.cache, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
+                                  addend=dx)
             grads[i] = dx
         for e, (j, i, sg, lay) in enumerate(spec.edges):
             g = gs[j]

@@ -521,6 +521,57 @@ __global__ void up2_kernel(const float* __restrict__ x, long long P, int h, int 
     }
 }
 
+// ------------------------------------------------------------------ conv onto a 1x1 output, M <= 4
+// out[b][m] = act(sum_seg sum_k x_seg[b][k] * w_seg[m][k] + bias[m]): a Conv2d whose kernel covers
+// the whole input plane (k == H == W, p = 0), e.g. FFCDiscriminator's last layer (4x4 -> 1x1,
+// models/ffc_discriminator.py:31).  One workgroup per sample; a per-sample dot product of K floats.
+constexpr int FS_MMAX = 4;
+
+__global__ __launch_bounds__(256) void conv_full_smallm_kernel(const float* __restrict__ x0, int K0,
+                                                               const float* __restrict__ w0,
+                                                               const float* __restrict__ x1, int K1,
+                                                               const float* __restrict__ w1,
+                                                               const float* __restrict__ bias, int M,
+                                                               float* __restrict__ out, int act, float p) {
+    const int b = blockIdx.x, tid = threadIdx.x;
+    float acc[FS_MMAX] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int sgi = 0; sgi < 2; ++sgi) {
+        const float* x = sgi ? x1 : x0;
+        const float* w = sgi ? w1 : w0;
+        const int K = sgi ? K1 : K0;
+        if (!x) continue;
+        const float* xb = x + (size_t)b * K;
+        if ((K & 3) == 0) {
+            const float4* x4 = reinterpret_cast<const float4*>(xb);
+            for (int i = tid; i < K / 4; i += 256) {
+                const float4 v = x4[i];
+#pragma unroll
+                for (int m = 0; m < FS_MMAX; ++m) {
+                    if (m >= M) break;
+                    const float4 ww = reinterpret_cast<const float4*>(w + (size_t)m * K)[i];
+                    acc[m] = fmaf(v.x, ww.x, fmaf(v.y, ww.y, fmaf(v.z, ww.z, fmaf(v.w, ww.w, acc[m]))));
+                }
+            }
+        } else {
+            for (int i = tid; i < K; i += 256) {
+                const float v = xb[i];
+                for (int m = 0; m < M; ++m) acc[m] = fmaf(v, w[(size_t)m * K + i], acc[m]);
+            }
+        }
+    }
+    __shared__ float red[4][FS_MMAX];
+#pragma unroll
+    for (int m = 0; m < FS_MMAX; ++m) {
+        const float v = ffc::wave_sum(acc[m]);
+        if ((tid & 63) == 0) red[tid >> 6][m] = v;
+    }
+    __syncthreads();
+    if (tid < M) {
+        const float v = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid] + (bias ? bias[tid] : 0.0f);
+        out[(size_t)b * M + tid] = ffc::apply_act(v, act, p);
+    }
+}
+
 int grid_for(long long n) { return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192)); }
 
 int dft_npw(int H, int W) { return std::max(1, std::min(64, 1024 / (H * W))); }
@@ -629,6 +680,19 @@ extern "C" int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H
     hipLaunchKernelGGL(se_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, x, dout, C, H * W, w1, w2, hidden,
                        dx, dpre2, hact, dpre1, mean);
     return ffc::launch_status("ffc_se_bwd");
+}
+
+extern "C" int ffc_conv_full_smallm(const float* x0, int K0, const float* w0, const float* x1, int K1,
+                                    const float* w1, const float* bias, int B, int M, float* out, int act,
+                                    float act_param, void* stream) {
+    FFC_CHECK_ARG(x0 && w0 && out && B > 0 && K0 > 0 && M >= 1 && M <= FS_MMAX, "ffc_conv_full_smallm: bad args");
+    FFC_CHECK_ARG(!x1 || (w1 && K1 > 0), "ffc_conv_full_smallm: second segment");
+    const bool al = ((reinterpret_cast<uintptr_t>(x0) | reinterpret_cast<uintptr_t>(w0)) & 15) == 0 &&
+                    (!x1 || ((reinterpret_cast<uintptr_t>(x1) | reinterpret_cast<uintptr_t>(w1)) & 15) == 0);
+    FFC_CHECK_ARG(al, "ffc_conv_full_smallm: 16-byte aligned operands");
+    hipLaunchKernelGGL(conv_full_smallm_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, x0, K0, w0, x1, K1, w1,
+                       bias, M, out, act, act_param);
+    return ffc::launch_status("ffc_conv_full_smallm");
 }
 
 extern "C" int ffc_pool2(const float* x, long long P, int H, int W, float scale, float* y, void* stream) {

@@ -352,6 +352,9 @@ class _FFCExec:
             return None
         if all(sg.kind == "convT" and (sg.k, sg.s, sg.p, sg.d, sg.op) == (4, 2, 1, 1, 0) for sg in segs):
             return "convT"
+        if all(sg.kind == "conv" and sg.k == sg.IH == sg.IW and sg.p == 0 and sg.d == 1 and not sg.pool
+               for sg in segs) and all(x[1] == 0 for x in w):
+            return "full"   # Conv2d onto a 1x1 output (FFCDiscriminator's last layer)
         if segs[0].IW % 4 == 0 and all(sg.kind == "conv" and (sg.k, sg.s, sg.p, sg.d) == (3, 1, 1, 1) for sg in segs):
             return "conv3"
         return None
@@ -382,6 +385,9 @@ class _FFCExec:
                                                         wp.data_ptr(), rt.ptr(bias), B, IH, IW, M, out.data_ptr(),
                                                         act[0], act[1], stream), "ffc_convt_k4s2_smallm")
             return out
+        if kind == "full":
+            return ag.conv_forward(self._ffc_cache(), ("inf_full",), B, M, tuple(segs), w,
+                                   [x for x, _ in inp], act=act)
         out = torch.empty((B, M, IH, IW), device=dev, dtype=torch.float32)
         flops = 2.0 * B * M * sum(sg.C for sg in segs) * 9 * IH * IW
         with rt.observe("conv3_smallm", flops=flops):

@@ -345,6 +345,12 @@ int ffc_irfft2_planes(const float* Z, int P, int H, int W, float interior_scale,
  * dpre1 (B, hidden), mean (B, C).  hidden = C // 16 may be 0 (gate 0.5). */
 int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H, int W, const float* w1, const float* w2,
                int hidden, float* dx, float* dpre2, float* hact, float* dpre1, float* mean, void* stream);
+/* Conv2d whose kernel covers the whole input plane (k == H == W, padding 0 -> 1x1 output) with
+ * M <= 4 outputs, up to two summed segments (FFCDiscriminator's last FFC_BN_ACT, 4x4 -> 1x1 + Sigmoid,
+ * models/ffc_discriminator.py:31; ffc.py:89-97): out[b][m] = act(sum x_s[b][k] w_s[m][k] + bias[m]),
+ * K_s = C_s*k*k, weights in nn.Conv2d layout; 16-byte aligned operands */
+int ffc_conv_full_smallm(const float* x0, int K0, const float* w0, const float* x1, int K1, const float* w1,
+                         const float* bias, int B, int M, float* out, int act, float act_param, void* stream);
 /* y = scale * (2x2 window sum) of P planes (H, W even): AvgPool2d(2,2) with scale 0.25
  * (spectral_transform.py:46-47), the adjoint of nearest Upsample(x2) with scale 1 */
 int ffc_pool2(const float* x, long long P, int H, int W, float scale, float* y, void* stream);
