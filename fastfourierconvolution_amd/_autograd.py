@@ -157,10 +157,10 @@ def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0
     return out
 
 
-def wgrad_splits(B, Mu, NT, P):
-    tiles = -(-Mu // 64) * -(-NT // 64)
-    S = max(1, min(B, 1024 // max(1, tiles)))
-    S = max(1, min(S, (B * P) // 256 or 1))
+def wgrad_splits(B, Mu, NT, P, bt=64):
+    tiles = -(-Mu // bt) * -(-NT // bt)
+    S = max(1, min(B, 1024 // max(1, tiles), 64))      # the fixed-order split sum reads S partials per weight
+    S = max(1, min(S, (B * P) // 512 or 1))
     return S
 
 
@@ -169,7 +169,7 @@ def conv_wgrad(U, V, k, s, p, d, dW_shape):
     B, Mu, PH, PW = U.shape
     _, Nv, VH, VW = V.shape
     NT = Nv * k * k
-    S = wgrad_splits(B, Mu, NT, PH * PW)
+    S = wgrad_splits(B, Mu, NT, PH * PW, rt.lib().ffc_conv_wgrad_tile(Mu, NT))
     dW = torch.empty(dW_shape, device=U.device, dtype=torch.float32)
     if dW.numel() != Mu * NT:
         raise FFCError(f"weight gradient shape {dW_shape} != ({Mu}, {Nv}, {k}, {k})")

@@ -127,6 +127,7 @@ SIGNATURES = [
     ("ffc_bn_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p,
                            c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p]),
+    ("ffc_conv_wgrad_tile", c_int, [c_int, c_int]),
     ("ffc_conv_wgrad", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     ("ffc_rfft2_planes", c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),

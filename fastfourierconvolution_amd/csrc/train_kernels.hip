@@ -195,9 +195,6 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __
 // in LDS; 64x64 tile per workgroup, 4 waves of one 32x32 v_mfma_f32_32x32x2_f32 tile each.
 // grid (tiles_n, tiles_m, S): split z reduces samples [B*z/S, B*(z+1)/S) into ws[z] (or into
 // G directly when S == 1).
-constexpr int WG_BK = 16;
-constexpr int WG_LD = WG_BK + 1;
-
 struct WgradArgs {
     const float* U;
     const float* V;
@@ -205,35 +202,48 @@ struct WgradArgs {
     int B, Mu, PH, PW, Nv, VH, VW, k, s, p, d, S;
 };
 
+// BT x BT tile (64 or 128), each wave a (BT/2) x (BT/2) quadrant of TT x TT MFMA tiles; K in
+// BK-deep chunks (64 for the small tile: its chunk carries only 8 MFMAs per wave, so the loads of
+// four 16-deep chunks are issued together to pay the global-load latency once)
+template <int BT, int BK>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
-    __shared__ float As[64 * WG_LD];
-    __shared__ float Bs[64 * WG_LD];
+    constexpr int WG_BK = BK;
+    constexpr int WG_LD = BK + 1;
+    constexpr int RS = 256 / BK;       // row stride between a thread's staged rows
+    constexpr int R = BT / RS;         // rows of A / columns of B each thread stages per chunk
+    constexpr int TT = BT / 64;        // 32x32 MFMA tiles per wave per dimension
+    __shared__ float As[BT * WG_LD];
+    __shared__ float Bs[BT * WG_LD];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int T = a.k * a.k, NT = a.Nv * T, P = a.PH * a.PW;
-    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64, z = blockIdx.z;
+    const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT, z = blockIdx.z;
     const int b_lo = (int)((long long)a.B * z / a.S), b_hi = (int)((long long)a.B * (z + 1) / a.S);
     const long long K0 = (long long)b_lo * P, K1 = (long long)b_hi * P;
     const size_t VP = (size_t)a.VH * a.VW;
-    // this thread's k column and its 4 rows (A) / 4 columns (B) of every chunk
-    const int kc = tid & 15, rbase = tid >> 4;
-    int vn[4], vky[4], vkx[4];
-    bool vok[4], aok[4];
+    // this thread's k column and its R rows (A) / R columns (B) of every chunk
+    const int kc = tid % BK, rbase = tid / BK;
+    int vn[R], vky[R], vkx[R];
+    bool vok[R], aok[R];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int col = n0 + rbase + 16 * r;
+    for (int r = 0; r < R; ++r) {
+        const int col = n0 + rbase + RS * r;
         vok[r] = col < NT;
         const int n = vok[r] ? col / T : 0, t = vok[r] ? col - n * T : 0;
         vn[r] = n;
         vky[r] = (t / a.k) * a.d - a.p;
         vkx[r] = (t % a.k) * a.d - a.p;
-        aok[r] = m0 + rbase + 16 * r < a.Mu;
+        aok[r] = m0 + rbase + RS * r < a.Mu;
     }
-    floatx16 acc;
+    floatx16 acc[TT][TT];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    for (int i = 0; i < TT; ++i)
+#pragma unroll
+        for (int j = 0; j < TT; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+    const int wm = (wave >> 1) * (BT / 2), wn = (wave & 1) * (BT / 2);
     const int h = lane >> 5, cl = lane & 31;
-    float av[4], bv[4];
+    float av[R], bv[R];
     auto load_chunk = [&](long long kk0) {
         const long long kk = kk0 + kc;
         if (kk < K1) {
@@ -242,44 +252,58 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
             const float* Ub = a.U + ((size_t)b * a.Mu) * P + q;
             const float* Vb = a.V + (size_t)b * a.Nv * VP;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                av[r] = aok[r] ? Ub[(size_t)(m0 + rbase + 16 * r) * P] : 0.0f;
+            for (int r = 0; r < R; ++r) {
+                av[r] = aok[r] ? Ub[(size_t)(m0 + rbase + RS * r) * P] : 0.0f;
                 const int iy = qy * a.s + vky[r], ix = qx * a.s + vkx[r];
                 bv[r] = (vok[r] && iy >= 0 && iy < a.VH && ix >= 0 && ix < a.VW)
                             ? Vb[(size_t)vn[r] * VP + (size_t)iy * a.VW + ix] : 0.0f;
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) av[r] = bv[r] = 0.0f;
+            for (int r = 0; r < R; ++r) av[r] = bv[r] = 0.0f;
         }
     };
     if (K0 < K1) load_chunk(K0);
     for (long long kk0 = K0; kk0 < K1; kk0 += WG_BK) {
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            As[(rbase + 16 * r) * WG_LD + kc] = av[r];
-            Bs[(rbase + 16 * r) * WG_LD + kc] = bv[r];
+        for (int r = 0; r < R; ++r) {
+            As[(rbase + RS * r) * WG_LD + kc] = av[r];
+            Bs[(rbase + RS * r) * WG_LD + kc] = bv[r];
         }
         __syncthreads();
         if (kk0 + WG_BK < K1) load_chunk(kk0 + WG_BK);   // next chunk's loads overlap this chunk's MFMAs
 #pragma unroll
         for (int st = 0; st < WG_BK / 2; ++st) {
-            const float x = As[(wm + cl) * WG_LD + 2 * st + h];
-            const float y = Bs[(wn + cl) * WG_LD + 2 * st + h];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
+            float x[TT], y[TT];
+#pragma unroll
+            for (int i = 0; i < TT; ++i) {
+                x[i] = As[(wm + 32 * i + cl) * WG_LD + 2 * st + h];
+                y[i] = Bs[(wn + 32 * i + cl) * WG_LD + 2 * st + h];
+            }
+#pragma unroll
+            for (int i = 0; i < TT; ++i)
+#pragma unroll
+                for (int j = 0; j < TT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[i], y[j], acc[i][j], 0, 0, 0);
         }
     }
     float* out = a.out + (size_t)z * a.Mu * NT;
-    const int col = n0 + wn + cl;
-    if (col < NT) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (m < a.Mu) out[(size_t)m * NT + col] = acc[r];
-        }
+    for (int j = 0; j < TT; ++j) {
+        const int col = n0 + wn + 32 * j + cl;
+        if (col >= NT) continue;
+#pragma unroll
+        for (int i = 0; i < TT; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < a.Mu) out[(size_t)m * NT + col] = acc[i][j][r];
+            }
     }
 }
+
+int wgrad_tile(int Mu, int NT) { return (Mu >= 128 && NT >= 128) ? 128 : 64; }
 
 __global__ void split_sum_kernel(const float* __restrict__ ws, int S, long long n, float* __restrict__ out,
                                  int accumulate) {
@@ -630,6 +654,8 @@ extern "C" int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW,
     return ffc::launch_status("ffc_bn_bwd");
 }
 
+extern "C" int ffc_conv_wgrad_tile(int Mu, int NT) { return wgrad_tile(Mu, NT); }
+
 extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const float* V, int Nv, int VH, int VW, int B,
                               int k, int stride, int pad, int dil, int S, float* ws, float* dW, int accumulate,
                               void* stream) {
@@ -640,8 +666,12 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
     const int NT = Nv * k * k;
     WgradArgs a{U, V, (S == 1 && !accumulate) ? dW : ws, B, Mu, PH, PW, Nv, VH, VW, k, stride, pad, dil, S};
     FFC_CHECK_ARG(a.out, "ffc_conv_wgrad: accumulate needs a workspace");
-    dim3 grid((NT + 63) / 64, (Mu + 63) / 64, S);
-    hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+    const int bt = wgrad_tile(Mu, NT);
+    dim3 grid((NT + bt - 1) / bt, (Mu + bt - 1) / bt, S);
+    if (bt == 128)
+        hipLaunchKernelGGL((wgrad_kernel<128, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(256), 0, (hipStream_t)stream, a);
     if (a.out != dW) {
         const long long n = (long long)Mu * NT;
         hipLaunchKernelGGL(split_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, S, n, dW,

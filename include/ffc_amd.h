@@ -328,6 +328,8 @@ int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW, const floa
  * U (B, Mu, PH, PW), V (B, Nv, VH, VW), zero outside V.  Conv2d: U = dy, V = x -> (Cout, Cin, k, k);
  * ConvTranspose2d: U = x, V = dy -> (Cin, Cout, k, k).  Split-K over samples into ws
  * (S * Mu * Nv*k*k floats; unused when S == 1 and accumulate == 0); accumulate adds into dW. */
+/* output tile edge ffc_conv_wgrad uses for (Mu, NT = Nv*k*k): grid = ceil(NT/t) x ceil(Mu/t) x S */
+int ffc_conv_wgrad_tile(int Mu, int NT);
 int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const float* V, int Nv, int VH, int VW, int B, int k,
                    int stride, int pad, int dil, int S, float* ws, float* dW, int accumulate, void* stream);
 /* rfftn(x, dim=(-2,-1), norm="ortho") of P planes (P, H, W) into the interleaved Re/Im planes of
