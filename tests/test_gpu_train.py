@@ -230,3 +230,46 @@ def test_train_step_optimizer_repacks_weights():
     for k, v in G.state_dict().items():
         if v.is_floating_point():
             assert normwise_err(v.cpu(), sd[k]) < 1e-4, k
+
+
+def test_train_step_graph_capture_bit_identical():
+    """the whole training step (forward, custom-op backward, optimizer) captured into one hipGraph
+    and replayed gives bit-identical weights and BN buffers to eager steps (deterministic kernels;
+    re-packs of the optimizer-updated weights are captured with the step)"""
+    import fastfourierconvolution_amd as F
+
+    def make():
+        torch.manual_seed(0)
+        with contextlib.redirect_stdout(io.StringIO()):
+            G, D = F.FFCGenerator(100, 3, 64), F.FFCDiscriminator(3, 64)
+        return G.cuda().train(), D.cuda().train()
+
+    z = torch.randn(16, 100, 1, 1, generator=torch.Generator().manual_seed(1)).cuda()
+    res = []
+    for graph in (False, True):
+        G, D = make()
+        opt = torch.optim.SGD(list(G.parameters()) + list(D.parameters()), lr=0.05)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            D(G(z)).mean().backward()
+            opt.step()
+        if graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            for _ in range(2):
+                g.replay()
+        else:
+            for _ in range(4):
+                step()
+        torch.cuda.synchronize()
+        res.append({k: v.detach().cpu().clone() for m in (G, D) for k, v in m.state_dict().items()})
+    for k in res[0]:
+        assert torch.equal(res[0][k], res[1][k]), k
