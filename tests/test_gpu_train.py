@@ -270,6 +270,7 @@ def test_train_step_graph_capture_bit_identical():
             for _ in range(4):
                 step()
         torch.cuda.synchronize()
-        res.append({k: v.detach().cpu().clone() for m in (G, D) for k, v in m.state_dict().items()})
+        res.append({n + k: v.detach().cpu().clone() for n, m in (("G.", G), ("D.", D))
+                    for k, v in m.state_dict().items()})
     for k in res[0]:
         assert torch.equal(res[0][k], res[1][k]), k
