@@ -158,10 +158,13 @@ def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0
 
 
 def wgrad_splits(B, Mu, NT, P, bt=64):
+    """split-K count for ffc_conv_wgrad: ~512 workgroups (2 per CU) with >= 1024 k per split
+    (measured on MI355X at the config-3 shapes: fewer splits leave CUs idle, more pay for the
+    partial-sum traffic), partial sums capped at 32 M floats"""
     tiles = -(-Mu // bt) * -(-NT // bt)
-    S = max(1, min(B, 1024 // max(1, tiles), 64))      # the fixed-order split sum reads S partials per weight
-    S = max(1, min(S, (B * P) // 512 or 1))
-    return S
+    S = -(-512 // max(1, tiles))
+    S = min(S, max(1, (B * P) // 1024), max(1, (32 << 20) // max(1, Mu * NT)))
+    return max(1, S)
 
 
 def conv_wgrad(U, V, k, s, p, d, dW_shape):

@@ -217,8 +217,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int T = a.k * a.k, NT = a.Nv * T, P = a.PH * a.PW;
     const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT, z = blockIdx.z;
-    const int b_lo = (int)((long long)a.B * z / a.S), b_hi = (int)((long long)a.B * (z + 1) / a.S);
-    const long long K0 = (long long)b_lo * P, K1 = (long long)b_hi * P;
+    // split z reduces k = (sample, pixel) in [K0, K1): an even share of the flattened K
+    const long long Ktot = (long long)a.B * P;
+    const long long K0 = Ktot * z / a.S, K1 = Ktot * (z + 1) / a.S;
     const size_t VP = (size_t)a.VH * a.VW;
     // this thread's k column and its R rows (A) / R columns (B) of every chunk
     const int kc = tid % BK, rbase = tid / BK;
@@ -304,6 +305,25 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
 }
 
 int wgrad_tile(int Mu, int NT) { return (Mu >= 128 && NT >= 128) ? 128 : 64; }
+
+// few weights, many splits: 16 weights x 16 split groups per workgroup, fixed-order LDS combine
+__global__ __launch_bounds__(256) void split_sum_grouped_kernel(const float* __restrict__ ws, int S, long long n,
+                                                                float* __restrict__ out, int accumulate) {
+    __shared__ float part[16][17];
+    const int e = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const long long i = (long long)blockIdx.x * 16 + e;
+    float v = 0.0f;
+    if (i < n)
+        for (int s = g; s < S; s += 16) v += ws[(size_t)s * n + i];
+    part[g][e] = v;
+    __syncthreads();
+    if (g == 0 && i < n) {
+        float t = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t += part[q][e];
+        out[i] = accumulate ? out[i] + t : t;
+    }
+}
 
 __global__ void split_sum_kernel(const float* __restrict__ ws, int S, long long n, float* __restrict__ out,
                                  int accumulate) {
@@ -660,7 +680,7 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
                               int k, int stride, int pad, int dil, int S, float* ws, float* dW, int accumulate,
                               void* stream) {
     FFC_CHECK_ARG(U && V && dW && Mu > 0 && Nv > 0 && PH > 0 && PW > 0 && VH > 0 && VW > 0 && B > 0 && k > 0 &&
-                      stride > 0 && dil > 0 && S >= 1 && S <= B,
+                      stride > 0 && dil > 0 && S >= 1 && (long long)S <= (long long)B * PH * PW,
                   "ffc_conv_wgrad: bad args");
     FFC_CHECK_ARG(S == 1 || ws, "ffc_conv_wgrad: split-K needs a workspace");
     const int NT = Nv * k * k;
@@ -674,8 +694,12 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
         hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(256), 0, (hipStream_t)stream, a);
     if (a.out != dW) {
         const long long n = (long long)Mu * NT;
-        hipLaunchKernelGGL(split_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, S, n, dW,
-                           accumulate);
+        if (n >= 65536 || S < 32)
+            hipLaunchKernelGGL(split_sum_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, ws, S, n, dW,
+                               accumulate);
+        else
+            hipLaunchKernelGGL(split_sum_grouped_kernel, dim3((unsigned)((n + 15) / 16)), dim3(256), 0,
+                               (hipStream_t)stream, ws, S, n, dW, accumulate);
     }
     return ffc::launch_status("ffc_conv_wgrad");
 }

@@ -326,8 +326,9 @@ int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW, const floa
  * ffc_transpose.py:48-86, spectral_transform.py:23-28,52-71, fourier_unity.py:20-23):
  *   dW[m][n][kh][kw] = sum_b sum_q U[b][m][q] * V[b][n][qy*stride - pad + kh*dil][qx*stride - pad + kw*dil]
  * U (B, Mu, PH, PW), V (B, Nv, VH, VW), zero outside V.  Conv2d: U = dy, V = x -> (Cout, Cin, k, k);
- * ConvTranspose2d: U = x, V = dy -> (Cin, Cout, k, k).  Split-K over samples into ws
- * (S * Mu * Nv*k*k floats; unused when S == 1 and accumulate == 0); accumulate adds into dW. */
+ * ConvTranspose2d: U = x, V = dy -> (Cin, Cout, k, k).  Split-K: S even shares of the flattened
+ * (sample, pixel) K, 1 <= S <= B*PH*PW, partials in ws (S * Mu * Nv*k*k floats; unused when S == 1
+ * and accumulate == 0) summed in a fixed order (deterministic); accumulate adds into dW. */
 /* output tile edge ffc_conv_wgrad uses for (Mu, NT = Nv*k*k): grid = ceil(NT/t) x ceil(Mu/t) x S */
 int ffc_conv_wgrad_tile(int Mu, int NT);
 int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const float* V, int Nv, int VH, int VW, int B, int k,
