@@ -43,12 +43,13 @@ class ConvJob(ctypes.Structure):
 class ConvPSeg(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("gate", c_void_p), ("C", c_int), ("Cpad", c_int), ("IH", c_int), ("IW", c_int),
                 ("mult_y", c_int), ("mult_x", c_int), ("org_y", c_int), ("org_x", c_int), ("PR", c_int),
-                ("PC", c_int), ("pool", c_int), ("vec4", c_int)]
+                ("PC", c_int), ("pool", c_int), ("vec4", c_int), ("cc", c_int), ("pad_", c_int)]
 
 
 class ConvPPhase(ctypes.Structure):
     _fields_ = [("py", c_int), ("px", c_int), ("PH", c_int), ("PW", c_int), ("Kpad", c_int),
-                ("T", c_int * MAX_SEG), ("kseg", c_int * MAX_SEG), ("tap", (c_int * 4) * MAX_SEG),
+                ("T", c_int * MAX_SEG), ("kseg", c_int * MAX_SEG), ("tap", (c_int * 8) * MAX_SEG),
+                ("tap_h", c_int * MAX_SEG),
                 ("a_off", c_longlong)]
 
 

@@ -258,7 +258,7 @@ class PatchPlan:
     prc: list            # per segment (PR, PC)
     vec4: list           # per segment: staged in 16-byte groups (IW % 4 == 0)
     rowlen: list         # per segment: LDS patch row length in floats (PC, or whole 4-float groups)
-    phases: list         # dicts: py, px, PH, PW, T[s], kseg[s], tap_base[s], Kpad, a_off, kt_off, K
+    phases: list         # dicts: py, px, PH, PW, T[s], kseg[s], tap_base[s], tap_h[s], Kpad, a_off, kt_off, K
     ktab: np.ndarray     # packing table (same format as JobPlan.ktab)
     taptab: np.ndarray   # int32 patch-relative tap offsets
     a_size: int
@@ -268,6 +268,7 @@ class PatchPlan:
     TC: int
     nrb: int
     ncb: int
+    cc: list = field(default_factory=list)   # per segment: channels per chunk (16, or 4 for 16 taps)
 
     @property
     def Mpad(self):
@@ -310,19 +311,23 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
     TR = min(PHm, max(1, npix // TC))
     NS = max(1, min(B, npix // (TR * TC)))
     nrb, ncb = -(-PHm // TR), -(-PWm // TC)
-    cpad = [-(-sg.C // PATCH_CC) * PATCH_CC for sg in segs]
-    # taps per (phase, segment)
+    # taps per (phase, segment): 1, 2 or 4 in 16-channel chunks; 16 (4 x 4, e.g. Conv2d k4 s2) in
+    # 4-channel chunks, one-phase jobs only
     taps = []
+    cc = [PATCH_CC] * len(segs)
     for ph in base.phases:
         row = []
         for si, sg in enumerate(segs):
             ty = _taps(sg, base.Sy, ph.py, sg.IH, ph.PH)
             tx = _taps(sg, base.Sx, ph.px, sg.IW, ph.PW)
             T = len(ty) * len(tx)
-            if T and 4 % T:
+            if T == 16 and NP == 1 and len(ty) == len(tx) == 4:
+                cc[si] = 4
+            elif T and 4 % T:
                 return None
             row.append((ty, tx))
         taps.append(row)
+    cpad = [-(-sg.C // cc[si]) * cc[si] for si, sg in enumerate(segs)]
     org, prc, vec4, rowlen = [], [], [], []
     for si, sg in enumerate(segs):
         oys = [o for row in taps for (k, o) in row[si][0]]
@@ -335,7 +340,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         PC = (TC - 1) * mx_ + (max(oxs) - ox0) + 1
         v4 = sg.IW % 4 == 0
         al = ox0 % 4 == 0 and (TC * mx_) % 4 == 0
-        if NS * PATCH_CC * PR * patch_units_per_row(PC, v4, al) > PATCH_MAX_UNITS:
+        if NS * cc[si] * PR * patch_units_per_row(PC, v4, al) > PATCH_MAX_UNITS:
             return None
         vec4.append(v4)
         rowlen.append(4 * patch_units_per_row(PC, True, al) if v4 else PC)
@@ -345,7 +350,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
     a_total = 0
     Mpad = -(-M // MPAD) * MPAD
     for pi, ph in enumerate(base.phases):
-        d = dict(py=ph.py, px=ph.px, PH=ph.PH, PW=ph.PW, T=[], kseg=[], tap_base=[])
+        d = dict(py=ph.py, px=ph.px, PH=ph.PH, PW=ph.PW, T=[], kseg=[], tap_base=[], tap_h=[])
         k = 0
         kt_off = len(ktab)
         for si, sg in enumerate(segs):
@@ -355,9 +360,19 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
             d["kseg"].append(k)
             d["tap_base"].append(len(taptab))
             PR, PC = prc[si]
+            base_t = len(taptab)
             for (ky, oy) in ty:
                 for (kx, ox) in tx:
                     taptab.append(((oy - org[si][0]) << 16) | (ox - org[si][1]))
+            th = 0
+            if T == 16:   # the kernel reads taps 8..15 as taps 0..7 shifted by one (dy, dx)
+                dyx = [(t >> 16, t & 0xFFFF) for t in taptab[base_t:]]
+                hy, hx = dyx[8][0] - dyx[0][0], dyx[8][1] - dyx[0][1]
+                if hx < 0 or any((dyx[j + 8][0] - dyx[j][0], dyx[j + 8][1] - dyx[j][1]) != (hy, hx)
+                                 for j in range(8)):
+                    return None
+                th = (hy << 16) | hx
+            d["tap_h"].append(th)
             for ch in range(cpad[si]):
                 for (ky, oy) in ty:
                     for (kx, ox) in tx:
@@ -373,7 +388,7 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         phases.append(d)
     return PatchPlan(B, M, base.OH, base.OW, base.Sy, base.Sx, segs, base.mults, cpad, org, prc, vec4, rowlen, phases,
                      np.asarray(ktab, dtype=np.int32).reshape(-1, 4), np.asarray(taptab or [0], dtype=np.int32),
-                     a_total, cfg, NS, TR, TC, nrb, ncb)
+                     a_total, cfg, NS, TR, TC, nrb, ncb, cc)
 
 
 def pick_patch_cfg(B, M, segs):
@@ -384,8 +399,8 @@ def pick_patch_cfg(B, M, segs):
         if q is not None:
             return q
     p = plan_patch_job(B, M, segs)
-    if p is None:
-        return plan_patch_job(B, M, segs, 1)   # a smaller pixel block may still fit the staging limits
+    if p is None:   # a smaller pixel block may still fit the staging limits
+        return plan_patch_job(B, M, segs, 1) or plan_patch_job(B, M, segs, 3)
     if p.cfg == 0:
         blocks = p.npb * (-(-M // 32))
         if blocks < 512:

@@ -317,12 +317,13 @@ class ConvExec:
             s.PR, s.PC = pl.prc[i][0], pl.rowlen[i]
             s.pool = int(sg.pool)
             s.vec4 = int(pl.vec4[i])
+            s.cc = pl.cc[i]
         for i, ph in enumerate(pl.phases):
             p = job.ph[i]
             p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]
             for si in range(len(pl.segs)):
-                p.T[si], p.kseg[si] = ph["T"][si], ph["kseg"][si]
-                for t in range(ph["T"][si]):
+                p.T[si], p.kseg[si], p.tap_h[si] = ph["T"][si], ph["kseg"][si], ph["tap_h"][si]
+                for t in range(min(ph["T"][si], 8)):
                     p.tap[si][t] = int(pl.taptab[ph["tap_base"][si] + t])
         job.A = self.A.data_ptr()
         job.bias = self.bias.data_ptr() if self.bias is not None else None

@@ -8,7 +8,8 @@
 //   * 32 output channels (M-tile) x a pixel block (NS samples x TR x TC pixels of the phase grid)
 //   * NP = 4 (stride-2 transposed conv): wave w computes phase w = (py, px) of every pixel of the
 //     block; NP = 1 (direct conv): the waves split the pixel block.
-//   * K runs over (segment, 16-channel chunk, tap).  Per chunk the input patch the block needs is
+//   * K runs over (segment, chunk, tap), a chunk being 16 channels (segments with 1, 2 or 4 taps
+//     per phase) or 4 channels x 16 taps (Conv2d k4 s2, one phase).  Per chunk the input patch the block needs is
 //     staged once in LDS (zero outside the input, 2x2 avg-pool / SE gate applied on the way in);
 //     every (phase, tap) B fragment is a conflict-free ds_read_b32 from it.  The next chunk's
 //     global loads are in flight (registers) while the current chunk's MFMAs run.
@@ -20,8 +21,6 @@
 #include <string>
 
 namespace {
-
-constexpr int CC = FFC_PATCH_CC;  // channels per chunk
 
 struct ConvPArgs {
     ffc_convp_job jobs[2];
@@ -54,14 +53,14 @@ constexpr int NEMAX = 8;   // staging units (4-float groups, or floats) per thre
 // x + off[e] + ch0 * IH*IW; off < 0 marks a unit outside the input / batch (zero fill).
 struct Stager {
     const float* x;
-    int C, Cpad, IHW, T, kseg, vec4, nunits;
+    int C, Cpad, IHW, T, kseg, vec4, nunits, cc, lcc;
     int off[NEMAX];
     unsigned chn;   // 4-bit channel-in-chunk of each of the thread's units
 };
 
 // A row pointer + patch geometry for the segment whose chunks are being multiplied.
 struct Computer {
-    int T, lt, PRC, gstep, Cpad;
+    int T, lt, PRC, gstep, Cpad, cc;
     int sb[8];      // per k-step s8: (s8 >> lt) * PRC + tap offset (s8 & (T-1))
 };
 
@@ -127,13 +126,15 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         st.T = P.T[s];
         st.kseg = P.kseg[s];
         st.vec4 = S.vec4;
+        st.cc = S.cc;
+        st.lcc = S.cc == 4 ? 2 : 4;
         const int PR = S.PR;
         const int iy0 = r0 * S.mult_y + S.org_y;
         const int ix0 = c0 * S.mult_x + S.org_x;
         const int xa = S.vec4 ? (ix0 & ~3) : ix0;
         const int PCu = S.vec4 ? S.PC / 4 : S.PC;   // units per patch row (4-float groups when vec4)
         const int step = S.vec4 ? 4 : 1;
-        st.nunits = NS * CC * PR * PCu;
+        st.nunits = NS * st.cc * PR * PCu;
         st.chn = 0;
         // n / d as umulhi(n, ceil(2^32 / d)): exact for n < 2^16 (n < 2048 units here); d = 1 special
         const unsigned mPC = PCu > 1 ? 0xFFFFFFFFu / (unsigned)PCu + 1u : 0u;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
             const int g = (int)(n - q1 * PCu);
             const unsigned q2 = PR > 1 ? __umulhi(q1, mPR) : q1;
             const int pr = (int)(q1 - q2 * PR);
-            const int ns = (int)(q2 >> 4), ch = (int)(q2 & 15);
+            const int ns = (int)(q2 >> st.lcc), ch = (int)(q2 & (st.cc - 1));
             const int b = b0 + ns, iy = iy0 + pr, ix = xa + g * step;
             const bool ok = (int)n < st.nunits && b < J.B && (unsigned)iy < (unsigned)S.IH &&
                             (unsigned)ix < (unsigned)S.IW;
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
             }
         }
     };
-    // A of one chunk (4 groups of 16 k; groups >= T are loaded but unused: the packed
+    // A of one chunk (4 groups of 16 k; groups >= min(T, 4) are loaded but unused: the packed
     // buffer carries tail padding) into registers, not waited for here
     auto load_A = [&](int ch0, floatx4 (&n0)[4], floatx4 (&n1)[4]) {
         const float* __restrict__ Ap =
@@ -198,29 +199,32 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         const int T = P.T[s];
         cp.T = T;
         cp.Cpad = S.Cpad;
+        cp.cc = S.cc;
         if (T == 0) return;
-        cp.lt = T == 4 ? 2 : (T == 2 ? 1 : 0);
+        cp.lt = T == 16 ? 4 : (T == 4 ? 2 : (T == 2 ? 1 : 0));   // k = (channel, tap): tap = k & (T - 1)
         const int PCa = S.PC;
         const int ix0 = c0 * S.mult_x + S.org_x;
         const int xoff = S.vec4 ? ix0 - (ix0 & ~3) : 0;
         cp.PRC = S.PR * PCa;
         cp.gstep = (16 >> cp.lt) * cp.PRC;
-        int tap[4];
+        int tap[8];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 8; ++t) {
             const int tt = P.tap[s][t & (T - 1)];
             tap[t] = (tt >> 16) * PCa + (tt & 0xFFFF);
         }
 #pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8) cp.sb[s8] = (s8 >> cp.lt) * cp.PRC + tap[s8 & 3 & (T - 1)];
-        const int hoff = ((8 * h) >> cp.lt) * cp.PRC;
+        for (int s8 = 0; s8 < 8; ++s8) cp.sb[s8] = (s8 >> cp.lt) * cp.PRC + tap[s8 & (T - 1)];
+        // lane half h carries k = 16g + 8h + s8: 8h / T channels further on (T <= 4), or taps 8..15 (T = 16)
+        const int th = P.tap_h[s];
+        const int hoff = ((8 * h) >> cp.lt) * cp.PRC + (T == 16 ? h * ((th >> 16) * PCa + (th & 0xFFFF)) : 0);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt)
-            lb[nt] = 4 * (pns[nt] * (CC * cp.PRC) + pr_[nt] * S.mult_y * PCa + pc_[nt] * S.mult_x + xoff + hoff);
+            lb[nt] = 4 * (pns[nt] * (cp.cc * cp.PRC) + pr_[nt] * S.mult_y * PCa + pc_[nt] * S.mult_x + xoff + hoff);
     };
 
     int nchunks = 0;
-    for (int s = 0; s < nseg; ++s) nchunks += J.seg[s].Cpad / CC;
+    for (int s = 0; s < nseg; ++s) nchunks += J.seg[s].Cpad / J.seg[s].cc;
 
 #ifdef FFC_TRACE
     unsigned long long tr_rt0 = __builtin_amdgcn_s_memrealtime(), tr_c0, tr_a, tr_b, tr_bar = 0, tr_stg = 0, tr_mf = 0;
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
     floatx4 a0[4], a1[4], n0[4], n1[4];
     stage_issue(0, patch);
     load_A(0, n0, n1);
-    sch = CC;
+    sch = st.cc;
     if (sch >= st.Cpad && nseg > 1) {
         ss = 1;
         sch = 0;
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #ifndef FFC_PROBE_NOSTAGE
             stage_issue(sch, patch + ((ci + 1) & 1) * ebuf);
 #endif
-            sch += CC;
+            sch += st.cc;
             if (sch >= st.Cpad && ss + 1 < nseg) {
                 ++ss;
                 sch = 0;
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
             const int base = ((ci & 1) * ebuf) * 4;   // byte offset of this chunk's buffer
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                if (g < T) {
+                if (g < T || T == 16) {
                     const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
                                          a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
                     const int gb = base + 4 * g * cp.gstep;
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         FFC_STAMP(tr_b);
         tr_mf += tr_b - tr_a;
 #endif
-        cch += CC;
+        cch += cp.cc;
         if (cch >= cp.Cpad && cs + 1 < nseg) {
             ++cs;
             cch = 0;
@@ -441,19 +445,21 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
         FFC_CHECK_ARG(J.NS > 0 && J.TR > 0 && J.TC > 0 && J.nrb > 0 && J.ncb > 0, "ffc_convp_forward: tiling");
         for (int s = 0; s < J.nseg; ++s) {
             const ffc_convp_seg& S = J.seg[s];
-            FFC_CHECK_ARG(S.x && S.Cpad % CC == 0 && S.Cpad >= S.C, "ffc_convp_forward: segment channels");
+            FFC_CHECK_ARG(S.cc == 16 || (S.cc == 4 && J.nphase == 1), "ffc_convp_forward: channels per chunk");
+            FFC_CHECK_ARG(S.x && S.Cpad % S.cc == 0 && S.Cpad >= S.C, "ffc_convp_forward: segment channels");
             FFC_CHECK_ARG(S.PC > 0 && S.PR > 0, "ffc_convp_forward: patch shape");
             FFC_CHECK_ARG(!S.pool && !S.gate, "ffc_convp_forward: pooled / gated segments use ffc_conv_forward");
             FFC_CHECK_ARG(!S.vec4 || (S.IW % 4 == 0 && S.PC % 4 == 0), "ffc_convp_forward: vec4 staging needs IW, PC % 4 == 0");
             FFC_CHECK_ARG(!S.vec4 || (reinterpret_cast<uintptr_t>(S.x) & 15) == 0,
                           "ffc_convp_forward: vec4 staging needs a 16-byte aligned input");
-            const size_t units = (size_t)J.NS * CC * S.PR * (S.vec4 ? S.PC / 4 : S.PC);
+            const size_t units = (size_t)J.NS * S.cc * S.PR * (S.vec4 ? S.PC / 4 : S.PC);
             FFC_CHECK_ARG(units <= (size_t)NEMAX * 256, "ffc_convp_forward: patch too large for the staging registers");
             const size_t E = (units + 255) / 256 * 256 * (S.vec4 ? 4 : 1);
             if (E > emax) emax = E;
             for (int p = 0; p < J.nphase; ++p) {
                 const int T = J.ph[p].T[s];
-                FFC_CHECK_ARG(T >= 0 && T <= 4 && (T == 0 || (4 % T) == 0), "ffc_convp_forward: taps must divide 4");
+                FFC_CHECK_ARG(S.cc == 4 ? T == 16 : (T >= 0 && T <= 4 && (T == 0 || (4 % T) == 0)),
+                              "ffc_convp_forward: taps must divide 4 (16-channel chunks) or be 16 (4-channel chunks)");
             }
         }
     }

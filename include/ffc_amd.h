@@ -101,8 +101,11 @@ int ffc_conv_stat_rows_per_tile(int tile_cfg);
  * the block needs (NS x 16 x PR x PC, zero outside the input) is staged once in LDS; every
  * (phase, tap) B fragment is then read from that patch, so an input element is fetched from
  * HBM/L2 once per block instead of once per (phase, tap).  Requires the taps per phase of each
- * segment to divide 4 (ConvT k4 s2: 4; 1x1: 1).  A is packed with every segment's channels
- * padded to a multiple of 16 (k = (seg, ch, tap)); the packed buffer needs >= 64 floats of tail padding
+ * segment to divide 4 (ConvT k4 s2: 4; 1x1: 1), or 16 in a one-phase job (Conv2d k4 s2: the
+ * discriminator's convs, FFCDiscriminator ffc1-3 (models/ffc_discriminator.py:27-30), and the
+ * data gradient of every ConvT k4 s2), whose chunks are then 4 channels x 16 taps.  A is packed
+ * with every segment's channels padded to a multiple of its chunk (k = (seg, ch, tap)); the
+ * packed buffer needs >= 64 floats of tail padding
  * (groups of taps a phase does not use are loaded, not multiplied).  Tap offsets travel in the
  * phase descriptor (kernel arguments, no table in memory).  Per-thread staging holds at most 2048
  * units (16-byte groups when vec4, else floats) of NS x 16 x PR x PC. */
@@ -117,14 +120,17 @@ typedef struct ffc_convp_seg {
                           * row start rounded down to a multiple of 4) */
     int pool;
     int vec4;            /* 1: stage the patch in 16-byte groups (IW % 4 == 0, x 16-byte aligned) */
+    int cc;              /* channels per chunk: 16 (taps 1, 2, 4) or 4 (16 taps) */
+    int pad_;
 } ffc_convp_seg;
 
 typedef struct ffc_convp_phase {
     int py, px, PH, PW;
     int Kpad;            /* sum over segments of Cpad * T[s] */
-    int T[FFC_MAX_SEG];  /* taps of each segment in this phase (1, 2 or 4, or 0) */
+    int T[FFC_MAX_SEG];  /* taps of each segment in this phase (1, 2, 4 or 16, or 0) */
     int kseg[FFC_MAX_SEG];   /* k offset of each segment inside the phase's packed rows */
-    int tap[FFC_MAX_SEG][4];    /* each segment's taps: (dy << 16) | dx from the patch origin */
+    int tap[FFC_MAX_SEG][8];    /* each segment's taps: (dy << 16) | dx from the patch origin (first 8) */
+    int tap_h[FFC_MAX_SEG];     /* 16 taps: tap j + 8 = tap j + tap_h for j < 8 (same encoding) */
     long long a_off;     /* float offset of the phase's packed weights [Mpad][Kpad] */
 } ffc_convp_phase;
 

@@ -177,6 +177,14 @@ def emulate_patch(plan, xs, ws, layouts):
                 assert sx == (s | (ch << 4))
                 tt = plan.taptab[ph["tap_base"][s] + t]
                 dy, dx = int(tt) >> 16, int(tt) & 0xFFFF
+                if T == 16:   # kernel view: lane half 1 reads taps 8..15 as taps 0..7 shifted by tap_h
+                    assert plan.cc[s] == 4 and plan.cpad[s] % 4 == 0
+                    if t >= 8:
+                        t0 = int(plan.taptab[ph["tap_base"][s] + t - 8])
+                        th = ph["tap_h"][s]
+                        assert (dy, dx) == ((t0 >> 16) + (th >> 16), (t0 & 0xFFFF) + (th & 0xFFFF))
+                else:
+                    assert plan.cc[s] == 16 and plan.cpad[s] % 16 == 0
                 assert (dy, dx) == (oy - plan.org[s][0], ox - plan.org[s][1])
                 # every in-block pixel stays inside the patch, also shifted by the 16-byte row alignment
                 PCa = plan.rowlen[s]
@@ -200,6 +208,9 @@ PATCH_CASES = {
     "gen_ffc4": [_plan.Seg("convT", 6, 32, 32, 4, 2, 1)],
     "odd_sizes": [_plan.Seg("convT", 3, 5, 7, 4, 2, 1)],
     "conv_k4s1p0": [_plan.Seg("conv", 5, 4, 4, 4, 1, 0)],
+    "conv_k4s2p1": [_plan.Seg("conv", 5, 8, 8, 4, 2, 1), _plan.Seg("conv", 3, 8, 8, 4, 2, 1)],
+    "conv_k4s2p1_pw": [_plan.Seg("conv", 6, 16, 16, 4, 2, 1), _plan.Seg("pw", 5, 8, 8)],
+    "conv_k4s2p1_odd": [_plan.Seg("conv", 3, 9, 7, 4, 2, 1)],
 }
 
 
@@ -230,3 +241,17 @@ def test_generator_layers_use_patch_kernel():
                     (64, [_plan.Seg("convT", 128, 8, 8, 4, 2, 1), _plan.Seg("pw", 32, 16, 16)]),
                     (32, [_plan.Seg("convT", 64, 16, 16, 4, 2, 1), _plan.Seg("pw", 16, 32, 32)])]:
         assert _plan.pick_patch_cfg(256, M, segs) is not None
+
+
+def test_strided_conv_layers_use_patch_kernel():
+    """FFCDiscriminator ffc0-3 convs (models/ffc_discriminator.py:26-30) and the generator's ConvT
+    data gradients (Conv2d k4 s2 p1) run on the LDS-patch kernel in 4-channel x 16-tap chunks"""
+    for M, segs in [(64, [_plan.Seg("conv", 3, 64, 64, 4, 2, 1)]),
+                    (128, [_plan.Seg("conv", 64, 32, 32, 4, 2, 1)] * 2),
+                    (128, [_plan.Seg("conv", 64, 32, 32, 4, 2, 1), _plan.Seg("pw", 64, 16, 16)]),
+                    (256, [_plan.Seg("conv", 128, 16, 16, 4, 2, 1)] * 2),
+                    (512, [_plan.Seg("conv", 256, 8, 8, 4, 2, 1)] * 2),
+                    (256, [_plan.Seg("conv", 128, 8, 8, 4, 2, 1)] * 2),
+                    (32, [_plan.Seg("conv", 3, 64, 64, 4, 2, 1)])]:
+        p = _plan.pick_patch_cfg(256, M, segs)
+        assert p is not None and 4 in p.cc, segs
