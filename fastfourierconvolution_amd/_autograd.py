@@ -158,12 +158,14 @@ def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0
 
 
 def wgrad_splits(B, Mu, NT, P, bt=64):
-    """split-K count for ffc_conv_wgrad: ~512 workgroups (2 per CU) with >= 1024 k per split
-    (measured on MI355X at the config-3 shapes: fewer splits leave CUs idle, more pay for the
-    partial-sum traffic), partial sums capped at 32 M floats"""
+    """split-K count for ffc_conv_wgrad: ~512 workgroups (2 per CU), >= 256 k per split (>= 64 when
+    K < 4096), partial sums capped at 32 M floats.  Measured on MI355X over every config-3 weight
+    gradient (tools/wgrad_probe.py, profiles/r01g/wgrad_probe*.log): the workgroup count decides;
+    the former >= 1024-k floor left 1x1 and 8x8-plane gradients on 8-128 workgroups at 2-8x the time"""
     tiles = -(-Mu // bt) * -(-NT // bt)
+    K = B * P
     S = -(-512 // max(1, tiles))
-    S = min(S, max(1, (B * P) // 1024), max(1, (32 << 20) // max(1, Mu * NT)))
+    S = min(S, max(1, K // (256 if K >= 4096 else 64)), max(1, (32 << 20) // max(1, Mu * NT)))
     return max(1, S)
 
 

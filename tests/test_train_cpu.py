@@ -44,7 +44,8 @@ def test_wgrad_splits_bounded():
     for B in (1, 2, 8, 256):
         for Mu, NT, P in ((128, 1024, 16), (3, 512, 1024), (512, 512, 12), (16, 256, 1)):
             S = wgrad_splits(B, Mu, NT, P)
-            assert 1 <= S <= max(1, B * P // 1024) and S * Mu * NT <= max(Mu * NT, 32 << 20)
+            K = B * P
+            assert 1 <= S <= max(1, K // (256 if K >= 4096 else 64)) and S * Mu * NT <= max(Mu * NT, 32 << 20)
 
 
 def _tw(N):
