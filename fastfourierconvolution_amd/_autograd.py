@@ -91,7 +91,7 @@ def run_conv(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0, 0.
     dev = inputs[0].device
     hit = cache.get(key)
     if hit is None:
-        ex = rt.ConvExec(B, M, list(segs), weights, dev)
+        ex = rt.ConvExec(B, M, list(segs), weights, dev, pw_ok=True)
         hit = cache[key] = (ex, rt.LaunchPlan([ex], dev))
     ex, lp = hit
     ex.ensure_packed(weights)
@@ -123,6 +123,18 @@ def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0
     route = None
     if addend is None and sum(1 for w in weights if w[4] is not None) <= 1:
         route = smallm_route(segs, [w[1] for w in weights], M)
+    if route is None and addend is None and len(segs) == 1 and weights[0][4] is None and weights[0][1] == 1:
+        sg = segs[0]
+        if sg.kind == "convT" and (sg.IH, sg.IW, sg.s, sg.p, sg.d, sg.op) == (1, 1, 1, 0, 1, 0) and sg.C <= 256:
+            # ConvTranspose2d on a 1x1 input (FFCGenerator ffc0, models/ffc_generator.py:24): a plain GEMM
+            # out (B, M*k*k) = x (B, C) . W (C, M*k*k) on the dense kernel; W needs no packing
+            Wt = weights[0][0]
+            N = M * sg.k * sg.k
+            out = torch.empty((B, M, sg.k, sg.k), device=inputs[0].device, dtype=torch.float32)
+            with rt.observe("dense", flops=2.0 * B * sg.C * N):
+                check(rt.lib().ffc_dense_forward(ptr(inputs[0]), ptr(Wt), None, B, sg.C, N, N, ptr(out), None,
+                                                 act[0], float(act[1]), _stream(out)), "ffc_dense_forward")
+            return out
     if route is None:
         return run_conv(cache, key, B, M, segs, weights, inputs, out_shape, act, addend)
     L = rt.lib()

@@ -71,6 +71,8 @@ SIGNATURES = [
     ("ffc_conv_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p, c_int, c_int, c_void_p]),
     ("ffc_conv_stat_rows_per_tile", c_int, [c_int]),
     ("ffc_convp_forward", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_int, c_void_p]),
+    ("ffc_pw_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p]),
+    ("ffc_pw_tiles", c_int, [c_int, c_int, c_int, c_int]),
     ("ffc_conv_pack", c_int, [ctypes.POINTER(ConvJob), ctypes.POINTER(c_void_p), ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_void_p),
                               c_void_p, c_void_p, c_void_p]),

@@ -223,6 +223,18 @@ def algorithmic_flops(plan) -> float:
 
 
 USE_PATCH = True   # LDS-patch kernel where it applies (tests flip this to cover the generic kernel)
+# 1x1-only jobs of the training path: "pw" = ffc_pw_forward (tiled GEMM), "patch" / "gemm" = the
+# conv kernels (A/B measurements, tests)
+PW_KERNEL = __import__("os").environ.get("FFC_PW_KERNEL", "pw")
+
+
+def pick_pw_cfg(B, M, Q):
+    """largest ffc_pw_forward tile that still gives >= 512 workgroups (2 per CU), else the smallest"""
+    cands = (0, 1, 2) if M > 64 else (1, 2)
+    for c in cands:
+        if lib().ffc_pw_tiles(M, B, Q, c) >= 512:
+            return c
+    return 2
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
@@ -259,9 +271,13 @@ class ConvExec:
     kind 'patch' -> ffc_convp_forward (LDS input patch, all phases per workgroup),
     kind 'gemm'  -> ffc_conv_forward (generic phase GEMM with gathered B)."""
 
-    def __init__(self, B, M, segs, weights, device):
-        pp = _plan.pick_patch_cfg(B, M, segs) if USE_PATCH else None
-        if pp is not None:
+    def __init__(self, B, M, segs, weights, device, pw_ok=False):
+        pw_only = all(sg.kind == "pw" and not sg.pool and not sg.gate for sg in segs)
+        pp = _plan.pick_patch_cfg(B, M, segs) if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None
+        if pw_ok and pw_only and PW_KERNEL == "pw":
+            self.kind, self.plan = "pw", _plan.plan_job(B, M, segs)
+            self.launch_key = ("pw", pick_pw_cfg(B, M, self.plan.OH * self.plan.OW))
+        elif pp is not None:
             self.kind, self.plan = "patch", pp
             self.launch_key = ("patch", pp.cfg)
         else:
@@ -301,7 +317,7 @@ class ConvExec:
         return job
 
     def base_job(self):
-        if self.kind == "gemm":
+        if self.kind in ("gemm", "pw"):
             return self.pack_job()
         pl = self.plan
         job = _lib.ConvPJob()
@@ -368,6 +384,12 @@ class LaunchPlan:
         if len(kinds) != 1:
             raise ValueError("jobs of one launch must share a kernel configuration")
         self.key = kinds.pop()
+        if self.key[0] == "pw":
+            self.cfg = self.key[1]
+            self._rows = [0 for _ in execs]
+            self.ntiles = sum(lib().ffc_pw_tiles(e.plan.M, e.plan.B, e.plan.OH * e.plan.OW, self.cfg) for e in execs)
+            self.tiles = None
+            return
         if self.key[0] == "patch":
             self.cfg = self.key[1]
             tiles = _plan.build_patch_tiles([e.plan for e in execs])
@@ -389,7 +411,10 @@ class LaunchPlan:
     def launch(self, jobs, stream, flops=0.0):
         L = lib()
         with observe("conv_gemm", flops=flops):
-            if self.key[0] == "patch":
+            if self.key[0] == "pw":
+                for jb in jobs:
+                    check(L.ffc_pw_forward(ctypes.byref(jb), self.cfg, stream), "ffc_pw_forward")
+            elif self.key[0] == "patch":
                 arr = (_lib.ConvPJob * len(jobs))(*jobs)
                 check(L.ffc_convp_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
                       "ffc_convp_forward")

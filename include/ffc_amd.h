@@ -95,6 +95,16 @@ int ffc_conv_forward(const ffc_conv_job* jobs, int njobs, const int* tiles, int 
 /* number of BN slab rows each tile writes (waves along N) for a tile_cfg */
 int ffc_conv_stat_rows_per_tile(int tile_cfg);
 
+/* 1x1-only job (every segment kind 'pw' at the output resolution, no pool / gate, one phase,
+ * stats == NULL) as a plain tiled GEMM: SpectralTransform conv1 / conv2
+ * (layers/ffc/spectral_transform.py:52-53,70-71), the FU spectral mix conv_layer
+ * (layers/ffc/fourier_unity.py:25,45) and their data gradients on the training path.  A is the
+ * job's ffc_conv_pack output ([Mpad][Kpad], k = segment-major channel).  cfg selects the tile:
+ * 0 = 128 x 128, 1 = 64 x 128, 2 = 64 x 64 (output channels x pixels);  ffc_pw_tiles returns the
+ * workgroup count of a cfg (or -1). */
+int ffc_pw_forward(const ffc_conv_job* job, int cfg, void* stream);
+int ffc_pw_tiles(int M, int B, int Q, int cfg);
+
 /* ---- LDS-patch variant (the hot path for FFCTranspose k4 s2 and strided convs) ----
  * A workgroup owns one M-tile of 32 output channels x a pixel block (NS samples x TR x TC
  * phase-grid pixels) x all phases.  For each 16-channel chunk of each segment the input patch
