@@ -23,6 +23,8 @@
 
 #include "ffc_internal.h"
 
+#include <cstdlib>
+
 namespace {
 
 __device__ __forceinline__ float act_grad_from_out(float y, float x_or_y, int act, float p) {
@@ -191,8 +193,8 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __
 
 // ------------------------------------------------------------------ weight gradient (MFMA)
 // G[m][n*T + t] = sum_b sum_q U[b][m][q] * V[b][n][qy*s - p + kh*d][qx*s - p + kw*d]
-// (zero outside V), t = kh*k + kw, q = qy*PW + qx.  K = (b, q) flattened, 16-deep chunks staged
-// in LDS; 64x64 tile per workgroup, 4 waves of one 32x32 v_mfma_f32_32x32x2_f32 tile each.
+// (zero outside V), t = kh*k + kw, q = qy*PW + qx.  K = (b, q) flattened, chunks staged in LDS;
+// 128x128 or 64x64 tile per workgroup, 4 waves of v_mfma_f32_32x32x2_f32 tiles.
 // grid (tiles_n, tiles_m, S): split z reduces samples [B*z/S, B*(z+1)/S) into ws[z] (or into
 // G directly when S == 1).
 struct WgradArgs {
@@ -204,7 +206,8 @@ struct WgradArgs {
 
 // BT x BT tile (64 or 128), each wave a (BT/2) x (BT/2) quadrant of TT x TT MFMA tiles; K in
 // BK-deep chunks (64 for the small tile: its chunk carries only 8 MFMAs per wave, so the loads of
-// four 16-deep chunks are issued together to pay the global-load latency once)
+// four 16-deep chunks are issued together to pay the global-load latency once; 32 for the large
+// tile: 64 MFMAs per wave between barriers)
 template <int BT, int BK>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     constexpr int WG_BK = BK;
@@ -688,10 +691,21 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
     FFC_CHECK_ARG(a.out, "ffc_conv_wgrad: accumulate needs a workspace");
     const int bt = wgrad_tile(Mu, NT);
     dim3 grid((NT + bt - 1) / bt, (Mu + bt - 1) / bt, S);
-    if (bt == 128)
-        hipLaunchKernelGGL((wgrad_kernel<128, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    static const int bk_knob = [] {   // A/B measurement knob (tools/wgrad_probe.py): K chunk depth
+        const char* e = getenv("FFC_WGRAD_BK");
+        return e ? atoi(e) : 0;
+    }();
+    if (bt == 128) {   // 32-deep chunks: 64 MFMAs per wave between barriers (measured 18 % faster than 16)
+        if (bk_knob == 16)
+            hipLaunchKernelGGL((wgrad_kernel<128, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL((wgrad_kernel<128, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    } else {   // 64-deep chunks (32 measured slower: the small tile needs the deeper load batch)
+        if (bk_knob == 32)
+            hipLaunchKernelGGL((wgrad_kernel<64, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    }
     if (a.out != dW) {
         const long long n = (long long)Mu * NT;
         if (n >= 65536 || S < 32)
