@@ -17,6 +17,7 @@ c_int, c_float, c_void_p, c_longlong, c_size_t, c_double = (
 
 MAX_SEG = 3
 MAX_PHASE = 16
+CONVP_EXACT_F32 = 8   # include/ffc_amd.h FFC_CONVP_EXACT_F32 (ffc_convp_forward cfg flag)
 
 ACT = {"Identity": 0, "ReLU": 1, "LeakyReLU": 2, "Tanh": 3, "Sigmoid": 4, "GELU": 5}
 

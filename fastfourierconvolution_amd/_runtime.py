@@ -235,6 +235,9 @@ def pick_pw_cfg(B, M, Q):
         if lib().ffc_pw_tiles(M, B, Q, c) >= 512:
             return c
     return 2
+# LDS-patch conv products: "split" = fp32-accurate split-bf16 MFMA (three exact bf16 pieces per
+# operand, six piece products), "f32" = v_mfma_f32_32x32x2_f32 (A/B measurements, tests)
+CONV_ARITH = __import__("os").environ.get("FFC_CONV_ARITH", "split")
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
@@ -416,7 +419,8 @@ class LaunchPlan:
                     check(L.ffc_pw_forward(ctypes.byref(jb), self.cfg, stream), "ffc_pw_forward")
             elif self.key[0] == "patch":
                 arr = (_lib.ConvPJob * len(jobs))(*jobs)
-                check(L.ffc_convp_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
+                cfg = self.cfg | (_lib.CONVP_EXACT_F32 if CONV_ARITH == "f32" else 0)
+                check(L.ffc_convp_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, cfg, stream),
                       "ffc_convp_forward")
             else:
                 arr = (_lib.ConvJob * len(jobs))(*jobs)

@@ -1,4 +1,4 @@
-// LDS-patch implicit-GEMM convolution for gfx950 (f32 MFMA) — the local-branch hot path.
+// LDS-patch implicit-GEMM convolution for gfx950 (MFMA, fp32-accurate) — the local-branch hot path.
 //
 // Replaces nn.ConvTranspose2d / nn.Conv2d of FFCTranspose / FFC (layers/ffc/ffc_transpose.py:79-86,
 // layers/ffc/ffc.py:45-70) together with SpectralTransform.conv2 (spectral_transform.py:70-71,108),
@@ -15,7 +15,9 @@
 //     global loads are in flight (registers) while the current chunk's MFMAs run.
 //   * A (packed weights, k = (seg, ch, tap), each 16-k group of one lane half contiguous) is read
 //     straight from L2 as 2 x dwordx4 per lane per 16 k and shared by the wave's N-tiles.
-//   * v_mfma_f32_32x32x2_f32: exact fp32.  Lane half h of k-step s carries k = 16g + 8h + s.
+//   * Products: by default fp32-accurate split-bf16 MFMA (split3 / mfma_split3 below: 6 x
+//     v_mfma_f32_32x32x16_bf16 per 16 k); cfg | FFC_CONVP_EXACT_F32 runs v_mfma_f32_32x32x2_f32
+//     (bitwise fp32 fma chains).  Lane half h of k-step s carries k = 16g + 8h + s in both.
 #include "ffc_internal.h"
 
 #include <string>
@@ -48,6 +50,59 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 
 constexpr int NEMAX = 8;   // staging units (4-float groups, or floats) per thread per chunk
 
+// ---- fp32-accurate products on the bf16 MFMA (SPLIT instantiations)
+// An fp32 value a splits EXACTLY into three bf16 pieces by truncation: hi = top 8 significand bits,
+// mid = the next 8 of a - hi, lo = a - hi - mid (<= 8 significant bits left, so exact in bf16; bf16
+// has fp32's exponent range).  a*b = sum of the 9 piece products; the 6 with piece order <= 2 are
+// kept (dropped terms < 2^-21 |a b|, the order of fp32 accumulation rounding), each product of two
+// bf16 pieces is exact in the fp32 accumulator.  6 x v_mfma_f32_32x32x16_bf16 (32 cycles each) per
+// 16 k replace 8 x v_mfma_f32_32x32x2_f32 (64 cycles each): 192 vs 512 MFMA cycles.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+    bf16x8 hi, mid, lo;
+};
+
+__device__ __forceinline__ unsigned pack_hi16(unsigned lo_elem, unsigned hi_elem) {
+    return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);   // {lo_elem[31:16], hi_elem[31:16]}
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ Split3 split3(const float (&v)[8]) {
+    u32x4 hv, mv, lv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // element pairs: the subtractions as v_pk_add_f32
+        const f32x2 a = {v[2 * q], v[2 * q + 1]};
+        const u32x2 ua = __builtin_bit_cast(u32x2, a);
+        const f32x2 r1 = a - __builtin_bit_cast(f32x2, ua & 0xFFFF0000u);
+        const u32x2 u1 = __builtin_bit_cast(u32x2, r1);
+        const f32x2 r2 = r1 - __builtin_bit_cast(f32x2, u1 & 0xFFFF0000u);
+        const u32x2 u2 = __builtin_bit_cast(u32x2, r2);
+        hv[q] = pack_hi16(ua[0], ua[1]);
+        mv[q] = pack_hi16(u1[0], u1[1]);
+        lv[q] = pack_hi16(u2[0], u2[1]);
+    }
+    Split3 s;
+    s.hi = __builtin_bit_cast(bf16x8, hv);
+    s.mid = __builtin_bit_cast(bf16x8, mv);
+    s.lo = __builtin_bit_cast(bf16x8, lv);
+    return s;
+}
+
+__device__ __forceinline__ floatx16 mfma_split3(const Split3& a, const Split3& b, floatx16 acc) {
+    // smallest terms first
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, acc, 0, 0, 0);
+    return acc;
+}
+
 // Per-segment staging state: the chunk-invariant part of every unit this thread moves.
 // Unit n of the patch image [ns][ch][pr][col] (col in 4-float groups when vec4) maps to
 // x + off[e] + ch0 * IH*IW; off < 0 marks a unit outside the input / batch (zero fill).
@@ -64,7 +119,7 @@ struct Computer {
     int sb[8];      // per k-step s8: (s8 >> lt) * PRC + tap offset (s8 & (T-1))
 };
 
-template <int NP, int NTW>
+template <int NP, int NTW, bool SPLIT>
 __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const ConvPArgs& args = *(const ConvPArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -284,20 +339,60 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #ifndef FFC_PROBE_NOMFMA
         if (T > 0) {
             const int base = ((ci & 1) * ebuf) * 4;   // byte offset of this chunk's buffer
+            if constexpr (SPLIT) {
+                // one 32x32x16 k-step per (group, N-tile): element j of lane half h is k = 16g + 8h + j,
+                // the same k order as the f32 path's k-steps (bf16 A/B lane maps).  The B reads of
+                // the next (group, N-tile) are issued before this one's split + MFMAs.
+                const int ng = T == 16 ? 4 : T;
+                auto rd = [&](int g, int nt, float (&b)[8]) {
+                    const int gb = base + 4 * g * cp.gstep + lb[nt];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                if (g < T || T == 16) {
-                    const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
-                                         a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
-                    const int gb = base + 4 * g * cp.gstep;
+                    for (int s8 = 0; s8 < 8; ++s8)
+                        b[s8] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(patch) +
+                                                                (gb + 4 * cp.sb[s8]));
+                };
+#ifdef FFC_CONVP_NO_PREFETCH   // A/B measurement builds
+                constexpr bool PF = false;
+#else
+                constexpr bool PF = true;
+#endif
+                float bq[2][8];
+                if (PF) rd(0, 0, bq[0]);
 #pragma unroll
-                    for (int s8 = 0; s8 < 8; ++s8) {
-                        const int sb = gb + 4 * cp.sb[s8];
+                for (int g = 0; g < 4; ++g) {
+                    if (g < ng) {
+                        const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
+                                             a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
+                        const Split3 as = split3(av);
 #pragma unroll
                         for (int nt = 0; nt < NTW; ++nt) {
-                            const float bv = *reinterpret_cast<const float*>(
-                                reinterpret_cast<const char*>(patch) + (lb[nt] + sb));
-                            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
+                            const int cur = PF ? (g * NTW + nt) & 1 : 0;
+                            if (!PF)
+                                rd(g, nt, bq[cur]);
+                            else if (nt + 1 < NTW)
+                                rd(g, nt + 1, bq[cur ^ 1]);
+                            else if (g + 1 < ng)
+                                rd(g + 1, 0, bq[cur ^ 1]);
+                            acc[nt] = mfma_split3(as, split3(bq[cur]), acc[nt]);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    if (g < T || T == 16) {
+                        const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
+                                             a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
+                        const int gb = base + 4 * g * cp.gstep;
+#pragma unroll
+                        for (int s8 = 0; s8 < 8; ++s8) {
+                            const int sb = gb + 4 * cp.sb[s8];
+#pragma unroll
+                            for (int nt = 0; nt < NTW; ++nt) {
+                                const float bv = *reinterpret_cast<const float*>(
+                                    reinterpret_cast<const char*>(patch) + (lb[nt] + sb));
+                                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s8], bv, acc[nt], 0, 0, 0);
+                            }
                         }
                     }
                 }
@@ -404,9 +499,9 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #endif
 }
 
-template <int NP, int NTW>
+template <int NP, int NTW, bool SPLIT>
 int launch(const ConvPArgs& a, int ntiles, size_t lds, hipStream_t s) {
-    auto k = convp_kernel<NP, NTW>;
+    auto k = convp_kernel<NP, NTW, SPLIT>;
     if (lds > 64 * 1024) {
         static bool raised = false;  // per instantiation
         if (!raised) {
@@ -434,6 +529,8 @@ extern "C" int ffc_debug_trace_read(void* dst, size_t bytes) {
 extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                                  void* stream) {
     FFC_CHECK_ARG(jobs && tiles && njobs >= 1 && njobs <= 2 && ntiles > 0, "ffc_convp_forward: bad args");
+    const bool exact = (cfg & FFC_CONVP_EXACT_F32) != 0;
+    cfg &= ~FFC_CONVP_EXACT_F32;
     size_t emax = 0;
     const int np = (cfg <= 1) ? 4 : 1;
     for (int j = 0; j < njobs; ++j) {
@@ -472,11 +569,20 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
     a.jobs[1] = jobs[njobs > 1 ? 1 : 0];
     a.tiles = reinterpret_cast<const int4*>(tiles);
     hipStream_t s = (hipStream_t)stream;
-    switch (cfg) {
-        case 0: return launch<4, 4>(a, ntiles, lds, s);
-        case 1: return launch<4, 2>(a, ntiles, lds, s);
-        case 2: return launch<1, 2>(a, ntiles, lds, s);
-        case 3: return launch<1, 1>(a, ntiles, lds, s);
+    if (exact) {
+        switch (cfg) {
+            case 0: return launch<4, 4, false>(a, ntiles, lds, s);
+            case 1: return launch<4, 2, false>(a, ntiles, lds, s);
+            case 2: return launch<1, 2, false>(a, ntiles, lds, s);
+            case 3: return launch<1, 1, false>(a, ntiles, lds, s);
+        }
+    } else {
+        switch (cfg) {
+            case 0: return launch<4, 4, true>(a, ntiles, lds, s);
+            case 1: return launch<4, 2, true>(a, ntiles, lds, s);
+            case 2: return launch<1, 2, true>(a, ntiles, lds, s);
+            case 3: return launch<1, 1, true>(a, ntiles, lds, s);
+        }
     }
     ffc::set_error("ffc_convp_forward: unknown cfg");
     return FFC_E_INVALID;

@@ -160,7 +160,9 @@ typedef struct ffc_convp_job {
 } ffc_convp_job;
 
 /* tiles: int4 {job, m0, pixel block, 0}; cfg: 0 = 4 phases x 4 N-tiles/wave, 1 = 4 x 2,
- * 2 = 1 phase x 2 N-tiles/wave, 3 = 1 x 1 */
+ * 2 = 1 phase x 2 N-tiles/wave, 3 = 1 x 1; | FFC_CONVP_EXACT_F32 selects the f32-input MFMA
+ * (bitwise fp32 fma chains) instead of the default fp32-accurate split-bf16 MFMA products */
+#define FFC_CONVP_EXACT_F32 8
 int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                       void* stream);
 
