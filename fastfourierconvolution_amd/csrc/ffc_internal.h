@@ -9,6 +9,60 @@
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// ---- fp32-accurate products on the bf16 MFMA (the SPLIT kernel instantiations)
+// An fp32 value a splits EXACTLY into three bf16 pieces by truncation: hi = top 8 significand bits,
+// mid = the next 8 of a - hi, lo = a - hi - mid (<= 8 significant bits left, so exact in bf16; bf16
+// has fp32's exponent range).  a*b = sum of the 9 piece products; the 6 with piece order <= 2 are
+// kept (dropped terms < 2^-21 |a b|, the order of fp32 accumulation rounding), each product of two
+// bf16 pieces is exact in the fp32 accumulator.  6 x v_mfma_f32_32x32x16_bf16 (32 cycles each) per
+// 16 k replace 8 x v_mfma_f32_32x32x2_f32 (64 cycles each): 192 vs 512 MFMA cycles.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+    bf16x8 hi, mid, lo;
+};
+
+static __device__ __forceinline__ unsigned pack_hi16(unsigned lo_elem, unsigned hi_elem) {
+    return __builtin_amdgcn_perm(hi_elem, lo_elem, 0x07060302u);   // {lo_elem[31:16], hi_elem[31:16]}
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+static __device__ __forceinline__ Split3 split3(const float (&v)[8]) {
+    u32x4 hv, mv, lv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // element pairs: the subtractions as v_pk_add_f32
+        const f32x2 a = {v[2 * q], v[2 * q + 1]};
+        const u32x2 ua = __builtin_bit_cast(u32x2, a);
+        const f32x2 r1 = a - __builtin_bit_cast(f32x2, ua & 0xFFFF0000u);
+        const u32x2 u1 = __builtin_bit_cast(u32x2, r1);
+        const f32x2 r2 = r1 - __builtin_bit_cast(f32x2, u1 & 0xFFFF0000u);
+        const u32x2 u2 = __builtin_bit_cast(u32x2, r2);
+        hv[q] = pack_hi16(ua[0], ua[1]);
+        mv[q] = pack_hi16(u1[0], u1[1]);
+        lv[q] = pack_hi16(u2[0], u2[1]);
+    }
+    Split3 s;
+    s.hi = __builtin_bit_cast(bf16x8, hv);
+    s.mid = __builtin_bit_cast(bf16x8, mv);
+    s.lo = __builtin_bit_cast(bf16x8, lv);
+    return s;
+}
+
+static __device__ __forceinline__ floatx16 mfma_split3(const Split3& a, const Split3& b, floatx16 acc) {
+    // smallest terms first
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, acc, 0, 0, 0);
+    return acc;
+}
+
+
 namespace ffc {
 
 void set_error(const std::string& msg);

@@ -208,8 +208,8 @@ struct WgradArgs {
 // BK-deep chunks (64 for the small tile: its chunk carries only 8 MFMAs per wave, so the loads of
 // four 16-deep chunks are issued together to pay the global-load latency once; 32 for the large
 // tile: 64 MFMAs per wave between barriers)
-template <int BT, int BK>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
+template <int BT, int BK, bool SPLIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_kernel(WgradArgs a) {
     constexpr int WG_BK = BK;
     constexpr int WG_LD = BK + 1;
     constexpr int RS = 256 / BK;       // row stride between a thread's staged rows
@@ -277,6 +277,31 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
         }
         __syncthreads();
         if (kk0 + WG_BK < K1) load_chunk(kk0 + WG_BK);   // next chunk's loads overlap this chunk's MFMAs
+        if constexpr (SPLIT) {
+            // fp32-accurate split-bf16 MFMA (ffc_internal.h split3): per 16-deep k-step, element j
+            // of lane half h is k = 2j + h for both operands (k-steps not unrolled: register budget)
+#pragma unroll 1
+            for (int q = 0; q < WG_BK / 16; ++q) {
+                Split3 ys[TT];
+#pragma unroll
+                for (int j = 0; j < TT; ++j) {
+                    float yv[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) yv[e] = Bs[(wn + 32 * j + cl) * WG_LD + 16 * q + 2 * e + h];
+                    ys[j] = split3(yv);
+                }
+#pragma unroll
+                for (int i = 0; i < TT; ++i) {
+                    float xv[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) xv[e] = As[(wm + 32 * i + cl) * WG_LD + 16 * q + 2 * e + h];
+                    const Split3 xs = split3(xv);
+#pragma unroll
+                    for (int j = 0; j < TT; ++j) acc[i][j] = mfma_split3(xs, ys[j], acc[i][j]);
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int st = 0; st < WG_BK / 2; ++st) {
             float x[TT], y[TT];
@@ -695,16 +720,21 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
         const char* e = getenv("FFC_WGRAD_BK");
         return e ? atoi(e) : 0;
     }();
+    static const bool exact = [] {    // A/B knob: f32-input MFMA instead of the split-bf16 products
+        const char* e = getenv("FFC_WGRAD_ARITH");
+        return e && std::string(e) == "f32";
+    }();
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, a); };
     if (bt == 128) {   // 32-deep chunks: 64 MFMAs per wave between barriers (measured 18 % faster than 16)
         if (bk_knob == 16)
-            hipLaunchKernelGGL((wgrad_kernel<128, 16>), grid, dim3(256), 0, (hipStream_t)stream, a);
+            exact ? go(wgrad_kernel<128, 16, false>) : go(wgrad_kernel<128, 16, true>);
         else
-            hipLaunchKernelGGL((wgrad_kernel<128, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+            exact ? go(wgrad_kernel<128, 32, false>) : go(wgrad_kernel<128, 32, true>);
     } else {   // 64-deep chunks (32 measured slower: the small tile needs the deeper load batch)
         if (bk_knob == 32)
-            hipLaunchKernelGGL((wgrad_kernel<64, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+            exact ? go(wgrad_kernel<64, 32, false>) : go(wgrad_kernel<64, 32, true>);
         else
-            hipLaunchKernelGGL((wgrad_kernel<64, 64>), grid, dim3(256), 0, (hipStream_t)stream, a);
+            exact ? go(wgrad_kernel<64, 64, false>) : go(wgrad_kernel<64, 64, true>);
     }
     if (a.out != dW) {
         const long long n = (long long)Mu * NT;
