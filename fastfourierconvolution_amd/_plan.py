@@ -391,8 +391,11 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
                      a_total, cfg, NS, TR, TC, nrb, ncb, cc)
 
 
-def pick_patch_cfg(B, M, segs):
-    """4-phase jobs: NTW=4 unless that leaves fewer than ~2 workgroups per CU."""
+def pick_patch_cfg(B, M, segs, min_blocks=512):
+    """4-phase jobs: NTW=4 unless that leaves fewer than `min_blocks` workgroups.  512 (2 per CU)
+    suits the f32-MFMA products; the split-bf16 products pay a per-group A split that 4 N-tiles
+    amortise better than 2, so the runtime passes 128 for them (gen64 on MI355X: 459K -> 478K
+    img/s; fgan128 and the training step unchanged, profiles/r01i)."""
     force = os.environ.get("FFC_PATCH_CFG4")   # A/B measurements: force the 4-phase configuration
     if force is not None:
         q = plan_patch_job(B, M, segs, int(force))
@@ -403,7 +406,7 @@ def pick_patch_cfg(B, M, segs):
         return plan_patch_job(B, M, segs, 1) or plan_patch_job(B, M, segs, 3)
     if p.cfg == 0:
         blocks = p.npb * (-(-M // 32))
-        if blocks < 512:
+        if blocks < min_blocks:
             q = plan_patch_job(B, M, segs, 1)
             if q is not None:
                 return q

@@ -276,7 +276,7 @@ class ConvExec:
 
     def __init__(self, B, M, segs, weights, device, pw_ok=False):
         pw_only = all(sg.kind == "pw" and not sg.pool and not sg.gate for sg in segs)
-        pp = _plan.pick_patch_cfg(B, M, segs) if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None
+        pp = _plan.pick_patch_cfg(B, M, segs, 128 if CONV_ARITH == "split" else 512) if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None
         if pw_ok and pw_only and PW_KERNEL == "pw":
             self.kind, self.plan = "pw", _plan.plan_job(B, M, segs)
             self.launch_key = ("pw", pick_pw_cfg(B, M, self.plan.OH * self.plan.OW))

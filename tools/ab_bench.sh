@@ -2,6 +2,7 @@
 # A/B the in-tree library against variants, interleaved, in one GPU session.
 # usage: tools/ab_bench.sh <variant>...   variant = cur | <name> (libffc_amd_<name>.so)
 #        optionally suffixed +VAR=value (environment for that run), e.g. cur+FFC_TILE_ORDER=interleaved
+#        AB_ARGS: extra bench.py arguments (e.g. "--workload fgan128"), AB_STEPS: timed steps
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -11,7 +12,7 @@ for round in 1 2; do
     if [ "$name" != "$v" ]; then envs=${v#*+}; fi
     if [ "$name" = cur ]; then lib=""; else lib="fastfourierconvolution_amd/libffc_amd_$name.so"; fi
     tag=$(echo "$v" | tr '+=/' '___')
-    env FFC_LIB_PATH=$lib $envs timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline \
+    env FFC_LIB_PATH=$lib $envs timeout -k 10 300 python bench.py --steps ${AB_STEPS:-50} --warmup 5 --no-cpu-baseline ${AB_ARGS:-} \
       > gpurun_out/ab_$tag.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; tail -5 gpurun_out/ab_$tag.log; exit $rc; fi
