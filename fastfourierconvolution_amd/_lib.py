@@ -61,7 +61,7 @@ class ConvPJob(ctypes.Structure):
                 ("nseg", c_int), ("nphase", c_int), ("B", c_int), ("M", c_int), ("Mpad", c_int),
                 ("OH", c_int), ("OW", c_int), ("Sy", c_int), ("Sx", c_int),
                 ("NS", c_int), ("TR", c_int), ("TC", c_int), ("nrb", c_int), ("ncb", c_int),
-                ("act", c_int), ("act_param", c_float)]
+                ("act", c_int), ("act_param", c_float), ("A3", c_void_p), ("a3_stride", ctypes.c_longlong)]
 
 
 # (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
@@ -72,6 +72,7 @@ SIGNATURES = [
     ("ffc_conv_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p, c_int, c_int, c_void_p]),
     ("ffc_conv_stat_rows_per_tile", c_int, [c_int]),
     ("ffc_convp_forward", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_int, c_void_p]),
+    ("ffc_split_bf16", c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p]),
     ("ffc_pw_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p]),
     ("ffc_pw_tiles", c_int, [c_int, c_int, c_int, c_int]),
     ("ffc_conv_pack", c_int, [ctypes.POINTER(ConvJob), ctypes.POINTER(c_void_p), ctypes.POINTER(c_int),

@@ -238,6 +238,7 @@ def pick_pw_cfg(B, M, Q):
 # LDS-patch conv products: "split" = fp32-accurate split-bf16 MFMA (three exact bf16 pieces per
 # operand, six piece products), "f32" = v_mfma_f32_32x32x2_f32 (A/B measurements, tests)
 CONV_ARITH = __import__("os").environ.get("FFC_CONV_ARITH", "split")
+PRESPLIT_A = __import__("os").environ.get("FFC_CONVP_PRESPLIT", "1") != "0"   # A/B knob: A3 planes
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
@@ -290,6 +291,11 @@ class ConvExec:
         self.ktab = torch.from_numpy(self.plan.ktab.copy()).to(device)
         # + tail padding: the patch kernel loads all 4 tap groups of a chunk, used or not
         self.A = torch.zeros(max(1, self.plan.a_size) + 256, device=device, dtype=torch.float32)
+        # split-bf16 patch conv: A pre-split into three exact bf16 planes (ffc_split_bf16) after every
+        # pack, so the kernel loads the pieces instead of splitting each chunk's A in registers
+        self.a3_stride = -(-self.A.numel() // 8) * 8
+        self.A3 = (torch.zeros(3 * self.a3_stride, device=device, dtype=torch.int16)
+                   if self.kind == "patch" and CONV_ARITH == "split" and PRESPLIT_A else None)
         self.has_bias = any(w[4] is not None for w in weights)
         self.bias = torch.empty(M, device=device, dtype=torch.float32) if self.has_bias else None
         self._packed = None
@@ -346,6 +352,8 @@ class ConvExec:
                     p.tap[si][t] = int(pl.taptab[ph["tap_base"][si] + t])
         job.A = self.A.data_ptr()
         job.bias = self.bias.data_ptr() if self.bias is not None else None
+        if self.A3 is not None:
+            job.A3, job.a3_stride = self.A3.data_ptr(), self.a3_stride
         return job
 
     def ensure_packed(self, weights):
@@ -362,6 +370,9 @@ class ConvExec:
         check(lib().ffc_conv_pack(ctypes.byref(job), wp, lay, kh, kw, bp, self.A.data_ptr(),
                                   ptr(self.bias), torch.cuda.current_stream(self.device).cuda_stream),
               "ffc_conv_pack")
+        if self.A3 is not None:
+            check(lib().ffc_split_bf16(self.A.data_ptr(), self.A.numel(), self.A3.data_ptr(), self.a3_stride,
+                                       torch.cuda.current_stream(self.device).cuda_stream), "ffc_split_bf16")
         self._packed = key
 
     def job(self, inputs, out, act=0, act_param=0.0, addend=None, stats=None):

@@ -68,13 +68,16 @@ struct Computer {
     int sb[8];      // per k-step s8: (s8 >> lt) * PRC + tap offset (s8 & (T-1))
 };
 
-template <int NP, int NTW, bool SPLIT>
+// AR: 0 = f32-input MFMA, 1 = split-bf16 (A split in registers), 2 = split-bf16 with A pre-split
+// (ffc_convp_job.A3 planes)
+template <int NP, int NTW, int AR>
 __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const ConvPArgs& args = *(const ConvPArgs*)__builtin_amdgcn_kernarg_segment_ptr();
 #else
     const ConvPArgs& args = args_byval;
 #endif
+    constexpr bool SPLIT = AR > 0;
     extern __shared__ __attribute__((aligned(16))) float patch[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -195,6 +198,17 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
         }
     };
 
+    // the same A rows from the three pre-split bf16 planes: 8 consecutive k per lane = one dwordx4
+    auto load_A3 = [&](int ch0, u32x4 (&n)[3][4]) {
+        const uint16_t* __restrict__ Ap =
+            J.A3 + P.a_off + (size_t)(m0 + cl) * P.Kpad + st.kseg + ch0 * st.T + 8 * h;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                n[q][g] = *reinterpret_cast<const u32x4*>(Ap + q * J.a3_stride + 16 * g);
+    };
+
     // ---- compute: per-segment LDS read offsets
     Computer cp;
     int lb[NTW];   // per N-tile byte offset of the lane's pixel inside a chunk buffer (+ lane-half channel)
@@ -240,8 +254,12 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
     stage_setup(0);
     compute_setup(0);
     floatx4 a0[4], a1[4], n0[4], n1[4];
+    u32x4 c3[3][4], n3[3][4];   // AR == 2: current / next chunk's A planes
     stage_issue(0, patch);
-    load_A(0, n0, n1);
+    if constexpr (AR == 2)
+        load_A3(0, n3);
+    else
+        load_A(0, n0, n1);
     sch = st.cc;
     if (sch >= st.Cpad && nseg > 1) {
         ss = 1;
@@ -263,12 +281,21 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #endif
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            a0[g] = n0[g];
-            a1[g] = n1[g];
+            if constexpr (AR == 2) {
+                c3[0][g] = n3[0][g];
+                c3[1][g] = n3[1][g];
+                c3[2][g] = n3[2][g];
+            } else {
+                a0[g] = n0[g];
+                a1[g] = n1[g];
+            }
         }
         if (ci + 1 < nchunks) {  // next chunk's A and patch stay in flight under this chunk's MFMAs
 #ifndef FFC_PROBE_NOA   // timing-probe builds only (wrong results): drop the A loads / patch staging
-            load_A(sch, n0, n1);
+            if constexpr (AR == 2)
+                load_A3(sch, n3);
+            else
+                load_A(sch, n0, n1);
 #endif
 #ifndef FFC_PROBE_NOSTAGE
             stage_issue(sch, patch + ((ci + 1) & 1) * ebuf);
@@ -310,9 +337,16 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     if (g < ng) {
-                        const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
-                                             a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
-                        const Split3 as = split3(av);
+                        Split3 as;
+                        if constexpr (AR == 2) {
+                            as.hi = __builtin_bit_cast(bf16x8, c3[0][g]);
+                            as.mid = __builtin_bit_cast(bf16x8, c3[1][g]);
+                            as.lo = __builtin_bit_cast(bf16x8, c3[2][g]);
+                        } else {
+                            const float av[8] = {a0[g][0], a0[g][1], a0[g][2], a0[g][3],
+                                                 a1[g][0], a1[g][1], a1[g][2], a1[g][3]};
+                            as = split3(av);
+                        }
 #pragma unroll
                         for (int nt = 0; nt < NTW; ++nt) {
                             const int cur = PF ? (g * NTW + nt) & 1 : 0;
@@ -448,9 +482,9 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #endif
 }
 
-template <int NP, int NTW, bool SPLIT>
+template <int NP, int NTW, int AR>
 int launch(const ConvPArgs& a, int ntiles, size_t lds, hipStream_t s) {
-    auto k = convp_kernel<NP, NTW, SPLIT>;
+    auto k = convp_kernel<NP, NTW, AR>;
     if (lds > 64 * 1024) {
         static bool raised = false;  // per instantiation
         if (!raised) {
@@ -518,21 +552,60 @@ extern "C" int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int
     a.jobs[1] = jobs[njobs > 1 ? 1 : 0];
     a.tiles = reinterpret_cast<const int4*>(tiles);
     hipStream_t s = (hipStream_t)stream;
+    bool pre = true;   // every job carries pre-split A planes
+    for (int j = 0; j < njobs; ++j) {
+        if (!jobs[j].A3) pre = false;
+        FFC_CHECK_ARG(!jobs[j].A3 || (jobs[j].a3_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(jobs[j].A3) & 15) == 0),
+                      "ffc_convp_forward: A3 planes need 16-byte alignment");
+    }
     if (exact) {
         switch (cfg) {
-            case 0: return launch<4, 4, false>(a, ntiles, lds, s);
-            case 1: return launch<4, 2, false>(a, ntiles, lds, s);
-            case 2: return launch<1, 2, false>(a, ntiles, lds, s);
-            case 3: return launch<1, 1, false>(a, ntiles, lds, s);
+            case 0: return launch<4, 4, 0>(a, ntiles, lds, s);
+            case 1: return launch<4, 2, 0>(a, ntiles, lds, s);
+            case 2: return launch<1, 2, 0>(a, ntiles, lds, s);
+            case 3: return launch<1, 1, 0>(a, ntiles, lds, s);
+        }
+    } else if (pre) {
+        switch (cfg) {
+            case 0: return launch<4, 4, 2>(a, ntiles, lds, s);
+            case 1: return launch<4, 2, 2>(a, ntiles, lds, s);
+            case 2: return launch<1, 2, 2>(a, ntiles, lds, s);
+            case 3: return launch<1, 1, 2>(a, ntiles, lds, s);
         }
     } else {
         switch (cfg) {
-            case 0: return launch<4, 4, true>(a, ntiles, lds, s);
-            case 1: return launch<4, 2, true>(a, ntiles, lds, s);
-            case 2: return launch<1, 2, true>(a, ntiles, lds, s);
-            case 3: return launch<1, 1, true>(a, ntiles, lds, s);
+            case 0: return launch<4, 4, 1>(a, ntiles, lds, s);
+            case 1: return launch<4, 2, 1>(a, ntiles, lds, s);
+            case 2: return launch<1, 2, 1>(a, ntiles, lds, s);
+            case 3: return launch<1, 1, 1>(a, ntiles, lds, s);
         }
     }
     ffc::set_error("ffc_convp_forward: unknown cfg");
     return FFC_E_INVALID;
+}
+
+// ---- ffc_split_bf16: the pre-split packed weights (split3 per element, planes hi / mid / lo)
+namespace {
+__global__ void split_bf16_kernel(const float* __restrict__ x, long long n, uint16_t* __restrict__ out,
+                                  long long stride) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const float a = x[i];
+        const unsigned u = __float_as_uint(a);
+        const float r1 = a - __uint_as_float(u & 0xFFFF0000u);
+        const unsigned u1 = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(u1 & 0xFFFF0000u);
+        out[i] = (uint16_t)(u >> 16);
+        out[stride + i] = (uint16_t)(u1 >> 16);
+        out[2 * stride + i] = (uint16_t)(__float_as_uint(r2) >> 16);
+    }
+}
+}  // namespace
+
+extern "C" int ffc_split_bf16(const float* x, long long n, uint16_t* planes, long long stride, void* stream) {
+    FFC_CHECK_ARG(x && planes && n > 0 && stride >= n && stride % 8 == 0, "ffc_split_bf16: bad args");
+    const long long blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(split_bf16_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                       (hipStream_t)stream, x, n, planes, stride);
+    return ffc::launch_status("ffc_split_bf16");
 }

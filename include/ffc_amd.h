@@ -157,12 +157,21 @@ typedef struct ffc_convp_job {
     int NS, TR, TC, nrb, ncb;   /* pixel block: NS samples x TR rows x TC cols; row/col blocks per sample */
     int act;
     float act_param;
+    /* optional: A pre-split into three exact bf16 planes (hi, mid, lo: ffc_split_bf16), plane p at
+     * A3 + p * a3_stride elements; NULL = split A in registers per chunk */
+    const uint16_t* A3;
+    long long a3_stride;
 } ffc_convp_job;
 
 /* tiles: int4 {job, m0, pixel block, 0}; cfg: 0 = 4 phases x 4 N-tiles/wave, 1 = 4 x 2,
  * 2 = 1 phase x 2 N-tiles/wave, 3 = 1 x 1; | FFC_CONVP_EXACT_F32 selects the f32-input MFMA
  * (bitwise fp32 fma chains) instead of the default fp32-accurate split-bf16 MFMA products */
 #define FFC_CONVP_EXACT_F32 8
+
+/* fp32 -> three exact bf16 planes by truncation (hi = top 8 significand bits, mid = the next 8 of
+ * x - hi, lo = the rest): planes[p * stride + i], p = 0, 1, 2; stride >= n, a multiple of 8.
+ * The pre-split packed weights of the split-bf16 patch conv (ffc_convp_job.A3). */
+int ffc_split_bf16(const float* x, long long n, uint16_t* planes, long long stride, void* stream);
 int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                       void* stream);
 
