@@ -1,5 +1,6 @@
 #!/bin/bash
-# r01i GPU session: smoke, every workload's bench line, rocprofv3 kernel stats of the gen64 bench.
+# One measurement session: smoke, every workload's bench line, rocprofv3 kernel stats of the gen64
+# bench, PMC HBM traffic (gen64, fgan128) into gpurun_out/ (copy to profiles/<round>/).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -19,3 +20,6 @@ run bench_fgan128sn 300 python bench.py --workload fgan128sn --steps 20 --warmup
 run bench_gan64train 300 python bench.py --workload gan64train --steps 20 --warmup 3 --cpu-seconds 10
 run rocprof_gen64 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gen64 -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline
 find gpurun_out/prof_gen64 -name "*stats*"
+ROUND=${ROUND:-pmc} bash tools/pmc_traffic.sh || exit $?
+ROUND=${ROUND:-pmc} WORKLOAD=fgan128 bash tools/pmc_traffic.sh || exit $?
+cp profiles/${ROUND:-pmc}/pmc_traffic*.json gpurun_out/
