@@ -238,7 +238,7 @@ def pick_pw_cfg(B, M, Q):
 # LDS-patch conv products: "split" = fp32-accurate split-bf16 MFMA (three exact bf16 pieces per
 # operand, six piece products), "f32" = v_mfma_f32_32x32x2_f32 (A/B measurements, tests)
 CONV_ARITH = __import__("os").environ.get("FFC_CONV_ARITH", "split")
-PRESPLIT_A = __import__("os").environ.get("FFC_CONVP_PRESPLIT", "1") != "0"   # A/B knob: A3 planes
+PRESPLIT_A = __import__("os").environ.get("FFC_CONVP_PRESPLIT", "0") == "1"   # A/B knob: A3 planes (off: measured neutral / -1 %)
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
