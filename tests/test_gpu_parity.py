@@ -182,6 +182,25 @@ def test_graph_capture_replays():
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("arith", ["f32", "split-presplit"])
+@pytest.mark.parametrize("case", [c for c in CASES if c["kind"] in ("FFC_BN_ACT", "FFCGenerator", "FFCDiscriminator")],
+                         ids=lambda c: c["name"])
+def test_golden_conv_arith_variants(case, arith):
+    """the LDS-patch conv's other product paths on the same cases (the default split-bf16 path with
+    A split in registers runs in test_golden): the exact f32-input MFMA (FFC_CONV_ARITH=f32) and the
+    split with pre-split A planes (FFC_CONVP_PRESPLIT=1, ffc_split_bf16 + ffc_convp_job.A3)"""
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.CONV_ARITH, rt.PRESPLIT_A
+    rt.CONV_ARITH, rt.PRESPLIT_A = ("f32", False) if arith == "f32" else ("split", True)
+    try:
+        state, inputs, data = load_case(case)
+        out = call_dropin(case, build_dropin(case, state), inputs)
+        for k, v in out.items():
+            assert normwise_err(v.cpu(), torch.from_numpy(data["ref." + k])) <= TOL, k
+    finally:
+        rt.CONV_ARITH, rt.PRESPLIT_A = old
+
+
 @pytest.mark.parametrize("case", [c for c in CASES if c["kind"] in ("FFC_BN_ACT", "FFCGenerator")],
                          ids=lambda c: c["name"])
 def test_golden_generic_conv_kernel(case):
