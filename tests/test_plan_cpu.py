@@ -255,3 +255,13 @@ def test_strided_conv_layers_use_patch_kernel():
                     (32, [_plan.Seg("conv", 3, 64, 64, 4, 2, 1)])]:
         p = _plan.pick_patch_cfg(256, M, segs)
         assert p is not None and 4 in p.cc, segs
+
+
+def test_patch_cfg_policy_min_blocks():
+    """4-phase jobs keep NTW = 4 (cfg 0) down to `min_blocks` workgroups: the split-bf16 products use
+    128 (the runtime's choice, _runtime.CONV_ARITH == "split"), the f32 products 512"""
+    segs = [_plan.Seg("convT", 128, 8, 8, 4, 2, 1), _plan.Seg("pw", 32, 16, 16)]   # gen64 ffc2 global, M = 64
+    p512 = _plan.pick_patch_cfg(256, 64, segs)
+    p128 = _plan.pick_patch_cfg(256, 64, segs, 128)
+    assert p512.cfg == 1 and p128.cfg == 0
+    assert 128 <= p128.npb * 2 < 512   # cfg 0: pixel blocks x 2 M-tiles, between the two thresholds
