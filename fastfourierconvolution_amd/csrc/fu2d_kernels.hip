@@ -442,10 +442,21 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 // The wave's A operand: fp32 fragments in registers (compile-time C, C*MT <= 64), fp16 fragments in
 // registers (F16), or read from the LDS copy Wm per k-step.
-template <int MT, int CC, bool F16, bool NOAREG = false>
+#ifdef FFC_MIX_F32   // A/B measurement builds: the register-resident fp32 mix on the f32-input MFMA
+constexpr bool MIX_SPLIT = false;
+#else
+constexpr bool MIX_SPLIT = true;
+#endif
+
+template <int MT, int CC, bool F16, bool NOAREG = false, bool SPLITOK = true>
 struct MixA {
     static constexpr bool AREG = !NOAREG && !F16 && CC > 0 && CC * MT <= 64;
+    // fp32 mix with register-resident weights: fp32-accurate split-bf16 products (ffc_internal.h
+    // split3), the weights split once per workgroup; element j of lane half hh in k-block q is
+    // k = 2 (8q + j) + hh, i.e. channel 8q + j, Re (hh = 0) or Im (hh = 1)
+    static constexpr bool SPLIT = AREG && MIX_SPLIT && SPLITOK && CC % 8 == 0;
     float areg[AREG ? CC : 1][MT];
+    Split3 as3[SPLIT ? CC / 8 : 1][SPLIT ? MT : 1];
     half8 a16[F16 ? MT : 1][F16 ? CC / 8 : 1];
     const float* Wm;
     int Mpad;
@@ -466,12 +477,23 @@ struct MixA {
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) areg[s][mt] = Wm[(2 * s + hh) * Mpad + mt * 32 + col];
         }
+        if constexpr (SPLIT) {
+#pragma unroll
+            for (int q = 0; q < CC / 8; ++q)
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    float av[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) av[j] = areg[8 * q + j][mt];
+                    as3[q][mt] = split3(av);
+                }
+        }
     }
 };
 
 // acc[mt] = Wmix[mt rows] . Z[:, bin n of this lane] (Z rebuilt from T on the fly)
-template <int MT, int CC, bool F16, bool NOAREG = false>
-__device__ __forceinline__ void mix_tile(floatx16 (&acc)[MT], const MixGeom& g, const MixA<MT, CC, F16, NOAREG>& A, int n,
+template <int MT, int CC, bool F16, bool NOAREG = false, bool SPLITOK = true>
+__device__ __forceinline__ void mix_tile(floatx16 (&acc)[MT], const MixGeom& g, const MixA<MT, CC, F16, NOAREG, SPLITOK>& A, int n,
                                          int C, int hh, int col) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -501,6 +523,23 @@ __device__ __forceinline__ void mix_tile(floatx16 (&acc)[MT], const MixGeom& g, 
             for (int mt = 0; mt < MT; ++mt)
                 acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A.a16[mt][kb], bz, acc[mt], 0, 0, 0);
         }
+    } else if constexpr (MixA<MT, CC, F16, NOAREG, SPLITOK>::SPLIT) {
+        float2 tv[CC];
+#pragma unroll
+        for (int s = 0; s < CC; ++s) tv[s] = g.Tb[idx + (size_t)s * g.planeT];
+#pragma unroll
+        for (int q = 0; q < CC / 8; ++q) {
+            float zb[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float2 t2 = tv[8 * q + j];
+                if (cj) t2.y = -t2.y;
+                zb[j] = hh ? (t2.x * fi + t2.y * fr) : (t2.x * fr - t2.y * fi);
+            }
+            const Split3 bs = split3(zb);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma_split3(A.as3[q][mt], bs, acc[mt]);
+        }
     } else if constexpr (CC > 0) {
         // all C gathered loads of the tile issued before its MFMAs (a register prefetch of the next
         // tile measured slower: 276 VGPRs, one wave per SIMD)
@@ -512,7 +551,7 @@ __device__ __forceinline__ void mix_tile(floatx16 (&acc)[MT], const MixGeom& g, 
             float2 t2 = tv[s];
             if (cj) t2.y = -t2.y;
             const float z = hh ? (t2.x * fi + t2.y * fr) : (t2.x * fr - t2.y * fi);
-            if constexpr (MixA<MT, CC, F16, NOAREG>::AREG) {
+            if constexpr (MixA<MT, CC, F16, NOAREG, SPLITOK>::AREG) {
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
                     acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(A.areg[s][mt], z, acc[mt], 0, 0, 0);
@@ -689,7 +728,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_cols_kernel(MixArgs a) {
         bnss[C2 + i] = a.bn_shift[i];
     }
     __syncthreads();
-    MixA<MT, CC, F16> A;
+    MixA<MT, CC, F16, false, false> A;   // f32-input MFMA here: the split measured slower (fewer waves)
     A.load(Wm, a.wmixT, a.Mpad, C2, hh, col);
     const MixGeom g = mix_geom(a, b, C);
     const int cs = wave / TPC, kb = wave % TPC;
@@ -702,7 +741,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_cols_kernel(MixArgs a) {
         const int kw = cg * CPW + cs, kh = kb * 32 + col;
         const bool kwv = kw < g.WP;
         floatx16 acc[MT];
-        mix_tile<MT, CC, F16>(acc, g, A, kwv ? kh * g.WP + kw : g.NB, C, hh, col);
+        mix_tile<MT, CC, F16, false, false>(acc, g, A, kwv ? kh * g.WP + kw : g.NB, C, hh, col);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
