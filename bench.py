@@ -1,8 +1,13 @@
 #!/usr/bin/env python3
 """bench.py — FFC-DCGAN generator forward throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gen64|fgan128|fgan128sn|gan64train]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+`--gpus N` without a launcher (WORLD_SIZE unset) starts the N ranks itself
+(fastfourierconvolution_amd/launch.py: N fresh child processes, one per GPU, before anything
+touches the GPU) and exits with their status; fewer than N visible GPUs is an error (exit 3).
+Under a launcher WORLD_SIZE must equal --gpus.
 
 Workload (BASELINE.json metric "FFC-generator fwd images/sec @ B=256 64x64x3"):
 FFCGenerator(nz=100, nc=3, ngf=64) (models/ffc_generator.py) forward, B=256 per GPU,
@@ -11,9 +16,14 @@ use batch statistics), synthetic z ~ N(0,1), weights from the reference's weight
 (fgan64_complete.py:22-31: conv N(0, 0.02), BN gamma N(1, 0.02), beta 0).
 One step = one generator forward over one batch; inputs resident in HBM.
 
-N > 1: one process per GPU, each rank a 256-sample shard of one global batch (weak scaling).
-Train-mode BN statistics are all-reduced over RCCL (SyncBN: the sharded result equals the
-global-batch forward); weights are broadcast once at init.  The step is hipGraph-captured.
+Scaling (``--scaling``, default strong): the global batch BASELINE.json names for the workload
+(gen64 256, fgan128 512 = configs[3], fgan128sn 1024 = configs[4]) is split over the N ranks
+(distributed.shard_range; z drawn once from the global seed and sliced), so every N measures the
+same job ("scaling": "strong").  ``--scaling weak`` keeps ``--batch`` samples per GPU instead.
+One process per GPU; train-mode BN statistics are all-reduced over RCCL (SyncBN: the sharded
+result equals the global-batch forward); weights are broadcast once at init.  The step is
+hipGraph-captured (the RCCL all-reduces inside the graph).  At N > 1 the gen64 line also carries
+the gathered global-batch output's parity against the CPU reference.
 
 The JSON line also carries:
   roofline      live per-kernel HIP-event timing of one eager pass (dominant kernel), MFMA f32 peak
@@ -67,11 +77,19 @@ def parse():
                         "gan64train: generator + discriminator 64x64x3 fwd+bwd + Adam (configs[2], B=256)")
     p.add_argument("--mix", choices=["fp32", "fp16"], default=None,
                    help="spectral mix arithmetic (default: fp16 for fgan128sn, fp32 otherwise)")
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="number of GPUs / ranks (default: WORLD_SIZE, or 1); starts the ranks itself when "
+                        "WORLD_SIZE is unset")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=None, help="samples per GPU (gen64: 256, fgan128: 64, "
-                                                                     "fgan128sn: 128)")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="strong: the workload's global batch split over the ranks; weak: --batch per GPU")
+    p.add_argument("--global-batch", type=int, default=None,
+                   help="strong scaling global batch (gen64: 256, fgan128: 512, fgan128sn: 1024)")
+    p.add_argument("--batch", type=int, default=None, help="weak scaling samples per GPU (gen64: 256, "
+                                                           "fgan128: 64, fgan128sn: 128)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launch + shard plan only, over gloo on the CPU (no GPU touched): rank 0 prints the plan")
     p.add_argument("--nz", type=int, default=100)
     p.add_argument("--nc", type=int, default=3)
     p.add_argument("--ngf", type=int, default=64)
@@ -153,6 +171,26 @@ def fgan_cpu_baseline(args, G, z_cpu, sn):
     parity = {"normwise_err_vs_cpu_ref": normwise_err(got, ref), "mode": f"train, B={nb}, explicit noise, fp64 oracle",
               "mix": args.mix, "tolerance": tol}
     return cpu, parity
+
+
+def sharded_parity(args, step, cpu_state, z_glob, global_batch, rank):
+    """N > 1 (gen64, strong scaling): one more sharded forward on every rank, outputs gathered to
+    the global batch (all_gather over RCCL), compared on rank 0 with the fp32 CPU reference path
+    run on the global z.  In train mode this checks the SyncBN all-reduces end to end: a naive
+    shard differs from the global-batch forward by ~3e-1 normwise."""
+    from fastfourierconvolution_amd.distributed import gather_batch
+    out = gather_batch(step().contiguous(), global_batch)
+    if rank != 0:
+        return None
+    from oracle.ffc_oracle import ffc_generator, normwise_err
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
+    with torch.no_grad():
+        ref = ffc_generator(z_glob, {k: v.clone() for k, v in cpu_state.items()}, args.nz, args.nc, args.ngf,
+                            args.bn_mode == "train", fft="torch")
+    if args.bn_mode != "train":
+        return None    # eval parity needs the GPU's running stats; the train-mode check is the SyncBN one
+    return {"normwise_err_vs_cpu_ref": normwise_err(out.cpu(), ref), "mode": f"train, global B={global_batch}, "
+            "sharded + SyncBN, outputs gathered", "tolerance": 1e-4}
 
 
 def weights_init(m):
@@ -299,25 +337,101 @@ def train_main(args):
     print(json.dumps(line))
 
 
+GLOBAL_BATCH = {"gen64": 256, "fgan128": 512, "fgan128sn": 1024}   # BASELINE.json configs[1..4]
+WEAK_BATCH = {"gen64": 256, "fgan128": 64, "fgan128sn": 128}
+
+
+def ranks_or_launch(args):
+    """-> (world, rank, local_rank) of this process.  With WORLD_SIZE unset and --gpus N > 1, start
+    the N ranks (fresh child processes; nothing here has touched the GPU) and exit with their
+    status.  Fewer visible GPUs than asked for, or a launcher world that disagrees with --gpus, is
+    an error (exit 3): a scaling line never silently reports another GPU count."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            raise SystemExit("--gpus must be >= 1")
+        if n > 1:
+            from fastfourierconvolution_amd.launch import spawn_ranks, visible_gpus
+            if not args.dry_run and visible_gpus() < n:
+                print(f"[bench] --gpus {n} but only {visible_gpus()} GPU(s) visible", file=sys.stderr)
+                sys.exit(3)
+            sys.exit(spawn_ranks(os.path.abspath(__file__), sys.argv[1:], n))
+        return 1, 0, 0
+    world = int(env_world)
+    if args.gpus is not None and args.gpus != world:
+        print(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(3)
+    rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not args.dry_run and local >= torch.cuda.device_count():
+        print(f"[bench] rank {rank}: LOCAL_RANK {local} but {torch.cuda.device_count()} GPU(s) visible",
+              file=sys.stderr)
+        sys.exit(3)
+    return world, rank, local
+
+
+def batch_plan(args, world, rank):
+    """-> (global_batch, this rank's [start, stop) of it)"""
+    from fastfourierconvolution_amd.distributed import shard_range
+    if args.scaling == "strong":
+        gb = args.global_batch or GLOBAL_BATCH[args.workload]
+        if gb < world:
+            raise SystemExit(f"global batch {gb} < {world} ranks")
+        return gb, shard_range(gb, rank, world)
+    per = args.batch or WEAK_BATCH[args.workload]
+    return per * world, (rank * per, (rank + 1) * per)
+
+
+def dry_run(args, world, rank):
+    """The launch and shard plan over gloo on the CPU: every rank reports its batch slice and the
+    checksum of its z slice; rank 0 checks they tile the global batch and prints one JSON line."""
+    import torch.distributed as dist
+    gb, (a, b) = batch_plan(args, world, rank)
+    if world > 1:
+        dist.init_process_group("gloo")
+    fgan = args.workload in ("fgan128", "fgan128sn")
+    zg = torch.randn((gb, 128) if fgan else (gb, args.nz, 1, 1), generator=torch.Generator().manual_seed(100))
+    mine = torch.tensor([float(a), float(b), float(zg[a:b].double().sum())], dtype=torch.float64)
+    parts = [torch.zeros_like(mine) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(parts, mine)
+    else:
+        parts = [mine]
+    if rank == 0:
+        spans = [(int(p[0]), int(p[1])) for p in parts]
+        ok = spans[0][0] == 0 and spans[-1][1] == gb and all(x[1] == y[0] for x, y in zip(spans, spans[1:]))
+        zsum = sum(float(p[2]) for p in parts)
+        print(json.dumps({"dry_run": True, "workload": args.workload, "n_gpus": world, "scaling": args.scaling,
+                          "global_batch": gb, "per_gpu_batch": [b - a for a, b in spans], "spans": spans,
+                          "tiles_global_batch": bool(ok and abs(zsum - float(zg.double().sum())) < 1e-6),
+                          "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and args.bn_mode == "train" else "")}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    world, rank, local = ranks_or_launch(args)
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if args.workload == "gan64train":
+        if world > 1:
+            raise SystemExit("gan64train is the single-GPU configs[2] workload")
         if args.batch is None:
             args.batch = 256
         return train_main(args)
-    if args.batch is None:
-        args.batch = {"gen64": 256, "fgan128": 64, "fgan128sn": 128}[args.workload]
     fgan = args.workload in ("fgan128", "fgan128sn")
     sn = args.workload == "fgan128sn"
     if args.mix is None:
         args.mix = "fp16" if sn else "fp32"
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    global_batch, (b0, b1) = batch_plan(args, world, rank)
+    args.batch = b1 - b0              # this rank's samples
     import torch.distributed as dist
     if world > 1:
+        import datetime
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=300))
     dev = torch.device("cuda", local)
 
     import fastfourierconvolution_amd as F
@@ -337,8 +451,14 @@ def main():
         D.broadcast_module(G)           # weights + BN buffers from rank 0, once
         if args.bn_mode == "train":
             D.enable_sync_bn()          # the only data-path exchange: BN moments all-reduce
-    gen = torch.Generator(device="cpu").manual_seed(100 + rank)
-    z_cpu = torch.randn((args.batch, 128) if fgan else (args.batch, args.nz, 1, 1), generator=gen)
+    if args.scaling == "strong":      # one global z (same seed for every N), this rank's slice
+        gen = torch.Generator(device="cpu").manual_seed(100)
+        z_glob = torch.randn((global_batch, 128) if fgan else (global_batch, args.nz, 1, 1), generator=gen)
+        z_cpu = z_glob[b0:b1].clone()
+    else:
+        gen = torch.Generator(device="cpu").manual_seed(100 + rank)
+        z_glob = None
+        z_cpu = torch.randn((args.batch, 128) if fgan else (args.batch, args.nz, 1, 1), generator=gen)
     z = z_cpu.to(dev)
 
     def step():
@@ -368,6 +488,11 @@ def main():
             print(f"[bench] graph capture failed ({e}); timing eagerly", file=sys.stderr)
             use_graph = False
             run = step
+        if world > 1:   # every rank must replay the same collectives: agree on graph vs eager
+            ok = torch.tensor([1 if use_graph else 0], device=dev, dtype=torch.int32)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if use_graph and ok.item() == 0:
+                use_graph, run = False, step
 
     if world > 1:
         dist.barrier()
@@ -383,7 +508,7 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    value = args.batch * world * args.steps / elapsed
+    value = global_batch * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
     # ---- live per-kernel roofline: one instrumented eager pass (HIP events on the launch stream)
@@ -418,9 +543,11 @@ def main():
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                     "algorithmic_bytes_per_step": b / max(1, args.profile_steps)}
 
-    # ---- CPU baseline + parity (rank 0, N=1 only)
+    # ---- CPU baseline + parity (rank 0, N=1 only); N > 1: the gathered sharded output (SyncBN)
     cpu = None
     parity = None
+    if world > 1 and not fgan and args.scaling == "strong" and not args.no_cpu_baseline:
+        parity = sharded_parity(args, step, cpu_state, z_glob, global_batch, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and fgan:
         cpu, parity = fgan_cpu_baseline(args, G, z_cpu, sn)
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -451,12 +578,13 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if args.mix == "fp32" else "f32 (fp16 spectral mix)",
+            "scaling": args.scaling, "vs_baseline": None,
+            "dtype": "f32" if args.mix == "fp32" else "f32 (fp16 spectral mix)",
             "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
             "config": {"workload": (f"fgan128 FGenerator(z=128, ngf=128){' + spectral norm (SNFFC)' if sn else ''} "
                                     "forward 128x128x3 (float output)" if fgan else
                                     f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) forward 64x64x{args.nc}"),
-                       "global_batch": args.batch * world, "per_gpu_batch": args.batch, "bn_mode": args.bn_mode,
+                       "global_batch": global_batch, "per_gpu_batch": args.batch, "bn_mode": args.bn_mode,
                        "spectral_mix": args.mix,
                        "hipgraph": use_graph, "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and
                                                                           args.bn_mode == "train" else "")},

@@ -138,11 +138,12 @@ def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: flo
                                                ptr(shift), stream), "ffc_bn_reduce_finalize")
         else:
             from .distributed import merge_moments
-            check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(moments), stream), "ffc_bn_reduce")
-            merge_moments(moments, group=grp)
-            check(L.ffc_bn_finalize(ptr(moments), C, gamma, beta, rm, rv, nbt, 1, int(update), momentum,
-                                    float(bn.eps), float(count_mult), ptr(scale), ptr(shift), stream),
-                  "ffc_bn_finalize")
+            with observe("bn_stats"):
+                check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(moments), stream), "ffc_bn_reduce")
+                merge_moments(moments, group=grp)
+                check(L.ffc_bn_finalize(ptr(moments), C, gamma, beta, rm, rv, nbt, 1, int(update), momentum,
+                                        float(bn.eps), float(count_mult), ptr(scale), ptr(shift), stream),
+                      "ffc_bn_finalize")
     else:
         check(L.ffc_bn_finalize(None, C, gamma, beta, rm, rv, nbt, 0, 0, momentum, float(bn.eps), 1.0,
                                 ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
