@@ -88,13 +88,16 @@ class observe:
 
 
 # --------------------------------------------------------------------------- SyncBN hook
-_SYNC = {"group": None}
+_SYNC = {"group": None, "world1": False}
 
 
-def set_sync_bn_group(group):
+def set_sync_bn_group(group, even_world1: bool = False):
     """Route train-mode BN moments through torch.distributed.all_reduce (RCCL) over ``group``
-    (None disables).  See fastfourierconvolution_amd.distributed.enable_sync_bn."""
+    (None disables).  See fastfourierconvolution_amd.distributed.enable_sync_bn.
+    ``even_world1``: keep the collective in a one-rank group (tests of the RCCL / hipGraph
+    machinery on a one-GPU box); a one-rank group is otherwise skipped."""
     _SYNC["group"] = group
+    _SYNC["world1"] = bool(even_world1)
 
 
 def _sync_group():
@@ -102,7 +105,7 @@ def _sync_group():
     if g is None:
         return None
     import torch.distributed as dist
-    if not dist.is_initialized() or dist.get_world_size(g) == 1:
+    if not dist.is_initialized() or (dist.get_world_size(g) == 1 and not _SYNC["world1"]):
         return None
     return g
 

@@ -54,9 +54,10 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
             dist.broadcast(t.data, src, group=group)
 
 
-def enable_sync_bn(group=None) -> None:
-    """Make every train-mode BN of this package use global (all-reduced) batch statistics."""
-    rt.set_sync_bn_group(group if group is not None else dist.group.WORLD)
+def enable_sync_bn(group=None, even_world1: bool = False) -> None:
+    """Make every train-mode BN of this package use global (all-reduced) batch statistics.
+    ``even_world1`` keeps the all-reduce in a one-rank group (tests)."""
+    rt.set_sync_bn_group(group if group is not None else dist.group.WORLD, even_world1)
 
 
 def disable_sync_bn() -> None:

@@ -1,0 +1,190 @@
+"""the checkpoint format (models/ffcmodel.py:31-107) and the evaluation
+caller (torch_fidelity/utils.py:160-208 + generative_model_modulewrapper.py:10-68).
+
+CPU: the checkpoint file name and dict layout, a round trip into fresh drop-in modules with the
+reference's state_dict key names (the golden manifest holds the names the reference's own
+modules produced), optimizer state, the error paths; the eval caller's noise stream and batching.
+GPU: a restored generator / discriminator gives bit-identical outputs, and the eval caller's
+batches (eval mode, no_grad, batches of 64, 2-D noise reshaped for FFCGenerator) match the fp64
+oracle; for the fgan128 FGenerator, its uint8 images.
+"""
+import contextlib
+import io
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import fastfourierconvolution_amd as F
+from fastfourierconvolution_amd.fidelity import GenerativeModelModuleWrapper, generate_batches, random_normal
+
+
+def _case(manifest, kind):
+    return next(c for c in manifest["cases"] if c["kind"] == kind)
+
+
+def _build(case):
+    kw = dict(case["ctor"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        return getattr(F, case["kind"])(**kw)
+
+
+def _randomize(mod, seed):
+    gen = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for k, v in mod.state_dict().items():
+            if v.is_floating_point():
+                v.copy_(torch.randn(v.shape, generator=gen) * 0.1 + (1.0 if k.endswith("running_var") else 0.0))
+            else:
+                v.fill_(seed)
+    return mod
+
+
+@pytest.mark.parametrize("kind", ["FFCGenerator", "FFCDiscriminator"])
+def test_checkpoint_round_trip_reference_keys(manifest, kind, tmp_path):
+    case = _case(manifest, kind)
+    m = _randomize(_build(case), 3)
+    opt = torch.optim.Adam(m.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    for p in m.parameters():           # give the optimizer some state to save
+        p.grad = torch.ones_like(p)
+    opt.step()
+    sched = torch.optim.lr_scheduler.StepLR(opt, 10)
+    d = tmp_path / "netG"
+    m.save_checkpoint(str(d), 1200, optimizer=opt, scheduler=sched)
+    path = d / "netG_1200_steps.pth"                 # models/ffcmodel.py:102-105
+    assert path.exists()
+    ck = torch.load(path, weights_only=True)
+    assert set(ck) == {"model_state_dict", "optimizer_state_dict", "scheduler_state_dict", "global_step"}
+    assert set(ck["model_state_dict"]) == set(case["specs"])       # the reference's key names
+    fresh = _build(case)
+    opt2 = torch.optim.Adam(fresh.parameters(), lr=1.0)
+    sched2 = torch.optim.lr_scheduler.StepLR(opt2, 3)
+    assert fresh.restore_checkpoint(str(path), opt2, sched2) == 1200
+    for k, v in m.state_dict().items():
+        assert torch.equal(fresh.state_dict()[k], v), k
+    assert opt2.param_groups[0]["lr"] == 2e-4 and sched2.step_size == 10
+    assert len(opt2.state) == len(opt.state)
+
+
+def test_checkpoint_named_and_errors(manifest, tmp_path):
+    m = _build(_case(manifest, "FFCGenerator"))
+    m.save_checkpoint(str(tmp_path / "x"), 5, name="custom.pth")
+    ck = torch.load(tmp_path / "x" / "custom.pth", weights_only=True)
+    assert ck["optimizer_state_dict"] is None and ck["scheduler_state_dict"] is None and ck["global_step"] == 5
+    with pytest.raises(ValueError):
+        m.restore_checkpoint("")
+
+
+def test_eval_caller_noise_and_batches():
+    """utils.py:171-186: one RandomState(seed) stream, (sz, z_size) float32 draws, batches of 64"""
+    seen = []
+
+    class Probe(nn.Module):
+        def forward(self, z):
+            seen.append(z.clone())
+            return z
+    w = GenerativeModelModuleWrapper(Probe(), 7, "normal", 0)
+    outs = list(generate_batches(w, 150, cuda=False))
+    assert [o.shape[0] for o in outs] == [64, 64, 22]
+    rng = np.random.RandomState(2020)
+    for z in seen:
+        assert z.dtype == torch.float32 and z.shape[1] == 7
+        assert torch.equal(z, torch.from_numpy(rng.randn(z.shape[0], 7)).float())
+    assert [o.shape[0] for o in generate_batches(w, 10, batch_size=64, cuda=False)] == [10]
+    with pytest.raises(ValueError):
+        GenerativeModelModuleWrapper(Probe(), 0, "normal", 0)
+    with pytest.raises(ValueError):
+        GenerativeModelModuleWrapper(Probe(), 4, "cauchy", 0)
+    with pytest.raises(ValueError):
+        list(generate_batches(Probe(), 4, cuda=False))
+
+
+def test_eval_caller_reshapes_for_ffc_generator():
+    with contextlib.redirect_stdout(io.StringIO()):
+        g = F.FFCGenerator(16, 3, 8)
+    w = GenerativeModelModuleWrapper(g, 16, "normal", 0)
+    assert not g.training and w._noise_4d
+    with contextlib.redirect_stdout(io.StringIO()):
+        fg = F.FGenerator(128)
+    assert not GenerativeModelModuleWrapper(fg, 128, "normal", 0)._noise_4d
+
+
+# --------------------------------------------------------------------------- GPU
+def _warm_running_stats(model, z):
+    for m in model.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m.momentum = 1.0
+    with torch.no_grad():
+        model.train()(z)
+    for m in model.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m.momentum = 0.1
+
+
+@pytest.mark.gpu
+def test_restored_models_bit_identical(tmp_path):
+    """G and D restored from a checkpoint (weights_only) into fresh modules reproduce the saved
+    models' outputs bit for bit, train and eval mode"""
+    torch.manual_seed(0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G, D = F.FFCGenerator(100, 3, 64).cuda(), F.FFCDiscriminator(3, 64).cuda()
+        G2, D2 = F.FFCGenerator(100, 3, 64), F.FFCDiscriminator(3, 64)
+    z = torch.randn(32, 100, 1, 1, generator=torch.Generator().manual_seed(1)).cuda()
+    _warm_running_stats(G, z)
+    _warm_running_stats(D, G(z).detach())
+    G.save_checkpoint(str(tmp_path / "netG"), 7)
+    D.save_checkpoint(str(tmp_path / "netD"), 7)
+    assert G2.restore_checkpoint(str(tmp_path / "netG" / "netG_7_steps.pth")) == 7
+    assert D2.restore_checkpoint(str(tmp_path / "netD" / "netD_7_steps.pth")) == 7
+    G2, D2 = G2.cuda(), D2.cuda()
+    with torch.no_grad():
+        for train in (False, True):
+            a = D.train(train)(G.train(train)(z))
+            b = D2.train(train)(G2.train(train)(z))
+            assert torch.equal(a, b), train
+
+
+@pytest.mark.gpu
+def test_eval_caller_ffc_generator_vs_oracle():
+    """FFCGenerator(100, 3, 64) through the eval caller: 150 samples in batches 64 / 64 / 22, eval
+    mode, no_grad, 2-D noise -> each batch equals the fp64 oracle on the same noise"""
+    from oracle.ffc_oracle import ffc_generator, normwise_err
+    torch.manual_seed(4)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G = F.FFCGenerator(100, 3, 64).cuda()
+    _warm_running_stats(G, torch.randn(64, 100, 1, 1, device="cuda"))
+    w = GenerativeModelModuleWrapper(G, 100, "normal", 0)
+    sd = {k: (v.detach().cpu().double() if v.is_floating_point() else v.cpu()) for k, v in G.state_dict().items()}
+    rng = np.random.RandomState(2020)
+    sizes = []
+    for fake in generate_batches(w, 150):
+        sizes.append(fake.shape[0])
+        z = random_normal(rng, (fake.shape[0], 100)).double().reshape(-1, 100, 1, 1)
+        with torch.no_grad():
+            ref = ffc_generator(z, sd, 100, 3, 64, False)
+        assert normwise_err(fake.cpu(), ref) <= 1e-4
+    assert sizes == [64, 64, 22] and not G.training
+
+
+@pytest.mark.gpu
+def test_eval_caller_fgan128_uint8_vs_oracle():
+    """fgan128 FGenerator through the eval caller: eval-mode uint8 images (fgan128_complete.py:516-521)
+    vs the oracle's float image quantised the same way (a value within fp32 rounding of an integer
+    step may land one code away)"""
+    from oracle.ffc_oracle import fgan128_generator, quantize_u8
+    torch.manual_seed(5)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G = F.FGenerator(128).cuda()
+    _warm_running_stats(G, torch.randn(8, 128, device="cuda"))
+    w = GenerativeModelModuleWrapper(G, 128, "normal", 0)
+    sd = {k: (v.detach().cpu().double() if v.is_floating_point() else v.cpu()) for k, v in G.state_dict().items()}
+    rng = np.random.RandomState(2020)
+    for fake in generate_batches(w, 6, batch_size=4):
+        assert fake.dtype == torch.uint8
+        z = random_normal(rng, (fake.shape[0], 128)).double()
+        with torch.no_grad():
+            ref = quantize_u8(fgan128_generator(z, sd, False).float())
+        d = (fake.cpu().int() - ref.int()).abs()
+        assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-3

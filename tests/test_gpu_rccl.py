@@ -1,0 +1,96 @@
+"""The RCCL side of the N > 1 path, as far as a one-GPU box can run it.
+
+RCCL needs one GPU per rank, so the multi-rank RCCL run happens only in the driver's 8-GPU
+scaling bench (bench.py --gpus N).  What a single GPU can check is the machinery that run relies
+on: a one-rank "nccl" (RCCL) process group, the SyncBN moment all-reduce routed through it
+(distributed.enable_sync_bn(even_world1=True) keeps the collective in a one-rank group), eager and
+captured inside a hipGraph together with the generator's kernels, replayed to the same output as
+the forward without the collective.  The numerics of the exchange itself (shards + merged moments
+== global batch) are covered over gloo in tests/test_distributed_cpu.py and, through the HIP
+kernels, in tests/test_gpu_parity.py::test_sharded_syncbn_gpu.
+"""
+import contextlib
+import io
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def rccl_world1():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        yield
+    finally:
+        from fastfourierconvolution_amd import distributed as D
+        D.disable_sync_bn()
+        dist.destroy_process_group()
+
+
+def test_rccl_moments_all_reduce_in_graph(rccl_world1):
+    from fastfourierconvolution_amd import distributed as D
+    m = torch.arange(30, dtype=torch.float64, device="cuda").reshape(10, 3)
+    ref = m.clone()
+    D.merge_moments(m)
+    torch.cuda.synchronize()
+    assert torch.equal(m, ref)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        D.merge_moments(m)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        m.mul_(2.0)
+        D.merge_moments(m)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(m, ref * 4)      # captured mul + replayed mul, the all-reduce in between
+
+
+def test_syncbn_generator_graph_over_rccl(rccl_world1):
+    """train-mode generator forward with every BN's moments all-reduced over RCCL: eager and
+    hipGraph-replayed outputs equal the forward without SyncBN, running statistics included"""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import distributed as D
+    from fastfourierconvolution_amd import _runtime as rt
+    torch.manual_seed(0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G = F.FFCGenerator(100, 3, 64).cuda().train()
+    z = torch.randn(32, 100, 1, 1, device="cuda")
+    state = {k: v.clone() for k, v in G.state_dict().items()}
+    with torch.no_grad():
+        ref = G(z).clone()
+        ref_state = {k: v.clone() for k, v in G.state_dict().items()}
+        G.load_state_dict(state)
+        D.enable_sync_bn(even_world1=True)
+        assert rt._sync_group() is not None
+        obs = rt.LaunchObserver()
+        rt.set_observer(obs)
+        eager = G(z).clone()
+        rt.set_observer(None)
+        assert obs.summary()["bn_stats"]["launches"] == 6      # the 6 SyncBN exchanges of the generator
+        # fused reduce+finalize vs reduce / all-reduce / finalize: same fp64 moments, maybe another order
+        torch.testing.assert_close(eager, ref, rtol=1e-6, atol=1e-6)
+        for k, v in ref_state.items():
+            torch.testing.assert_close(G.state_dict()[k], v, rtol=1e-6, atol=1e-7, msg=k)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            G(z)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = G(z)
+        graph.replay()
+        torch.cuda.synchronize()
+    torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)

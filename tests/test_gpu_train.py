@@ -87,7 +87,7 @@ class _KinkF:
         return torch.nn.functional.leaky_relu(x, slope)
 
 
-def _layer_checks(train: bool, B: int = 8):
+def _layer_checks(train: bool, B: int = 8, fp32_ref: bool = True, check_loss: bool = False):
     """config 3 architecture at full width (G nz=100 nc=3 ngf=64, D nc=3 ndf=64), loss =
     mean(D(G(z))), fwd + bwd on the HIP path, checked LAYER BY LAYER: for every FFC_BN_ACT, the
     oracle's vector-Jacobian product at the HIP path's own layer input and output gradient, with
@@ -97,7 +97,9 @@ def _layer_checks(train: bool, B: int = 8):
     measured here), and one flipped LeakyReLU moves a weight gradient by 5e-2 normwise -- that
     would test the kinks, not the kernels (a 1e-6 relative change of D's input moves D's input
     gradient by 5e-3 in fp64).  Each layer also runs in fp32 on the CPU (the reference's own arithmetic) for the
-    train-mode conditioning bound.  -> [(name, err vs fp64, fp32-reference err vs fp64)]"""
+    train-mode conditioning bound (``fp32_ref``).  ``check_loss``: the scalar loss against the fp64
+    oracle's end-to-end forward (<= 1e-4 relative).
+    -> [(name, err vs fp64, fp32-reference err vs fp64 or nan)]"""
     import fastfourierconvolution_amd as F
     from oracle.ffc_oracle import discriminator_layers, ffc_bn_act, generator_layers
     gen = torch.Generator().manual_seed(3)
@@ -132,6 +134,15 @@ def _layer_checks(train: bool, B: int = 8):
     zc = z.detach().cuda().requires_grad_(True)
     out = run("D", D, run("G", G, zc)).mean()
     out.backward()
+    if check_loss:
+        with torch.no_grad():
+            sd64 = {n: {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sds[n].items()}
+                    for n in ("G", "D")}
+            ref_loss = ffc_discriminator(ffc_generator(z.double(), sd64["G"], 100, 3, 64, train), sd64["D"], 3, 64,
+                                         train).mean().item()
+        rel = abs(out.item() - ref_loss) / abs(ref_loss)
+        print(f"loss {out.item():.8f} vs fp64 oracle {ref_loss:.8f}: rel {rel:.2e}")
+        assert rel <= TOL, rel
     cfgs = {"G": generator_layers(100, 3, 64), "D": discriminator_layers(3, 64)}
     mods = {"G": G, "D": D}
     res = []
@@ -140,7 +151,7 @@ def _layer_checks(train: bool, B: int = 8):
             xs = x if type(x) is tuple else (x,)
             params = {k: p for k, p in mods[name].named_parameters() if k.startswith(f"ffc{i}.") and p.grad is not None}
             ref = {}
-            for bits, dt in ((64, torch.float64), (32, torch.float32)):
+            for bits, dt in ((64, torch.float64), (32, torch.float32))[:2 if fp32_ref else 1]:
                 sd = {k: (v.to(dt).clone().requires_grad_(k in params)) if v.is_floating_point() else v.clone()
                       for k, v in sds[name].items()}
                 xin = [t.detach().cpu().to(dt).requires_grad_(True) if isinstance(t, torch.Tensor) else t for t in xs]
@@ -162,7 +173,8 @@ def _layer_checks(train: bool, B: int = 8):
             assert set(ref[64]) == set(mine), (name, i, set(ref[64]) ^ set(mine))
             for k in ref[64]:
                 res.append((f"{name}.{k}" if k.startswith("ffc") else f"{name}.ffc{i}.{k}",
-                            normwise_err(mine[k], ref[64][k]), normwise_err(ref[32][k], ref[64][k])))
+                            normwise_err(mine[k], ref[64][k]),
+                            normwise_err(ref[32][k], ref[64][k]) if fp32_ref else float("nan")))
     return res
 
 
