@@ -54,7 +54,10 @@ def test_rccl_moments_all_reduce_in_graph(rccl_world1):
         D.merge_moments(m)
     g.replay()
     torch.cuda.synchronize()
-    assert torch.equal(m, ref * 4)      # captured mul + replayed mul, the all-reduce in between
+    assert torch.equal(m, ref * 2)      # capture records without running: one replayed mul + all-reduce
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(m, ref * 4)
 
 
 def test_syncbn_generator_graph_over_rccl(rccl_world1):
