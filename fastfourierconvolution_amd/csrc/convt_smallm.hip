@@ -447,7 +447,7 @@ static __global__ void convt_smallm_pack_kernel(const float* __restrict__ w0, in
 }
 
 extern "C" size_t ffc_convt_smallm_pack_floats(int C0, int C1) {
-    return C0 > 0 && C1 >= 0 ? (size_t)(C0 + C1) * 64 : 0;
+    return C0 > 0 && C1 >= 0 ? ((size_t)C0 + (size_t)C1) * 64 : 0;
 }
 
 extern "C" int ffc_convt_smallm_pack(const float* w0, int C0, const float* w1, int C1, int M, float* wpack,

@@ -1019,7 +1019,7 @@ int mix_nsplit(int B, int H, int W) {
 }  // namespace
 
 extern "C" int ffc_fu2d_supported(int C, int H, int W, int up) {
-    if (C <= 0 || 2 * C > 128 || H != W || !(up == 1 || up == 2)) return 0;
+    if (C <= 0 || C > 64 || H != W || !(up == 1 || up == 2)) return 0;   // 2C <= 128
     if (!pow2_in(H, 16, 128)) return 0;
     const int h = H / up;
     if (!pow2_in(h, 8, 128)) return 0;

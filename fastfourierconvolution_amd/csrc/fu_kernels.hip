@@ -391,7 +391,7 @@ extern "C" int ffc_debug_fu_trace_read(void* dst, size_t bytes) {
 #endif
 
 extern "C" size_t ffc_fu_lds_bytes(int C, int H, int W) {
-    if (C <= 0 || !pow2_in(H, 4, 32) || !pow2_in(W, 4, 32)) return 0;
+    if (C <= 0 || C > 4096 || !pow2_in(H, 4, 32) || !pow2_in(W, 4, 32)) return 0;   // C > 4096 never fits LDS
     return fu_layout(C, H, W).bytes;
 }
 

@@ -289,6 +289,9 @@ extern "C" int ffc_debug_st_trace_read(void* dst, size_t bytes) {
 
 extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, int c) {
     if (Cin <= 0 || H <= 0 || W <= 0 || c <= 0 || hidden < 0) return 0;
+    // a sample in 160 KiB of LDS has < 40960 floats: larger dims never fit (and keep the layout
+    // arithmetic inside int range)
+    if (Cin > 65536 || H > 65536 || W > 65536 || c > 65536 || hidden > 65536) return 0;
     if (pool && ((H | W) & 1)) return 0;
     return st_layout(Cin, H, W, pool, hidden, c).bytes;
 }

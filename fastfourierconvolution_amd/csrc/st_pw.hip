@@ -142,7 +142,7 @@ typedef void (*PwKernel)(PwArgs);
 
 }  // namespace
 
-extern "C" int ffc_pw_gate_blocks(int HW) { return HW > 0 ? (HW + PW_PIX - 1) / PW_PIX : 0; }
+extern "C" int ffc_pw_gate_blocks(int HW) { return HW > 0 ? (int)(((long long)HW + PW_PIX - 1) / PW_PIX) : 0; }
 
 extern "C" size_t ffc_pw_gate_lds_bytes(int Cin, int M) {
     if (Cin <= 0 || M <= 0 || M > 128) return 0;
