@@ -44,7 +44,8 @@ class ConvJob(ctypes.Structure):
 class ConvPSeg(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("gate", c_void_p), ("C", c_int), ("Cpad", c_int), ("IH", c_int), ("IW", c_int),
                 ("mult_y", c_int), ("mult_x", c_int), ("org_y", c_int), ("org_x", c_int), ("PR", c_int),
-                ("PC", c_int), ("pool", c_int), ("vec4", c_int), ("cc", c_int), ("pad_", c_int)]
+                ("PC", c_int), ("pool", c_int), ("vec4", c_int), ("cc", c_int), ("direct", c_int),
+                ("qrow", c_int), ("qsample", c_int)]
 
 
 class ConvPPhase(ctypes.Structure):
@@ -72,6 +73,9 @@ SIGNATURES = [
     ("ffc_conv_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p, c_int, c_int, c_void_p]),
     ("ffc_conv_stat_rows_per_tile", c_int, [c_int]),
     ("ffc_convp_forward", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_int, c_void_p]),
+    ("ffc_convq_config", c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    ("ffc_convq_pack_a3", c_int, [ctypes.POINTER(ConvPJob), c_void_p, c_void_p, c_void_p]),
+    ("ffc_convq_forward", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_int, c_void_p]),
     ("ffc_split_bf16", c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p]),
     ("ffc_pw_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p]),
     ("ffc_pw_tiles", c_int, [c_int, c_int, c_int, c_int]),

@@ -269,6 +269,10 @@ class PatchPlan:
     nrb: int
     ncb: int
     cc: list = field(default_factory=list)   # per segment: channels per chunk (16, or 4 for 16 taps)
+    q: bool = False      # ffc_convq_forward plan (K order (chunk, tap, channel), pre-split operands)
+    mt: int = 1          # convq: M-tiles of 32 channels per wave (tiles step m0 by 32 * mt)
+    direct: list = field(default_factory=list)   # convq: per segment, B read straight from global
+    qstride: list = field(default_factory=list)  # convq: per segment LDS (row, sample) pixel strides
 
     @property
     def Mpad(self):
@@ -391,6 +395,143 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
                      a_total, cfg, NS, TR, TC, nrb, ncb, cc)
 
 
+# --------------------------------------------------------------------------- convq plans
+CONVQ_CFGS = {0: (1, 4), 1: (1, 2), 2: (2, 2), 3: (1, 1)}   # cfg -> (M-tiles, N-tiles) per wave
+CONVQ_MAX_UNITS = 256      # staging units per chunk (one per staging thread: 4 pixels x 8 channels)
+CONVQ_LDS_BUDGET = 150 * 1024  # LDS bytes per workgroup (one 8-wave workgroup per CU)
+
+
+def convq_strides(NS, TR, TC, PR, PC, pad=True):
+    """LDS (row, sample) pixel strides of the convq patch image.  A B fragment's lane n reads pixel
+    p(n) = ns * qsample + r * qrow + c (+ a tap offset) at 48 * p bytes; the 16 lanes of a
+    ds_read_b128 group are conflict-free when p(n) = n (mod 16) for every lane, i.e. qrow = TC and
+    qsample = TR * TC (mod 16)."""
+    if not pad:
+        return PC, PR * PC
+    qr = PC + ((TC - PC) % 16)
+    qs = PR * qr + ((TR * TC - PR * qr) % 16)
+    return qr, qs
+
+
+def convq_lds_bytes(NS, strides):
+    return 2 * (((max(NS * qs for _, qs in strides) * 96 + 255) // 256) * 256 + 256)
+
+
+def plan_convq_job(B: int, M: int, segs, cfg: int):
+    """ffc_convq_forward plan (4-phase stride-2 jobs: ConvTranspose2d k4 s2 segments staged through
+    LDS, 1x1 segments at the output resolution read directly), or None when it does not apply."""
+    segs = tuple(segs)
+    if any(sg.pool or sg.gate for sg in segs):
+        return None
+    base = plan_job(B, M, segs)
+    if (base.Sy, base.Sx) != (2, 2) or len(base.phases) != 4:
+        return None
+    mt, ntw = CONVQ_CFGS[cfg]
+    npix = 32 * ntw
+    PHm = max(ph.PH for ph in base.phases)
+    PWm = max(ph.PW for ph in base.phases)
+    TC = min(PWm, npix)
+    TR = min(PHm, max(1, npix // TC))
+    NS = max(1, min(B, npix // (TR * TC)))
+    nrb, ncb = -(-PHm // TR), -(-PWm // TC)
+    direct = [sg.kind == "pw" for sg in segs]
+    taps = []
+    for ph in base.phases:
+        row = []
+        for si, sg in enumerate(segs):
+            ty = _taps(sg, base.Sy, ph.py, sg.IH, ph.PH)
+            tx = _taps(sg, base.Sx, ph.px, sg.IW, ph.PW)
+            T = len(ty) * len(tx)
+            if (direct[si] and T not in (0, 1)) or T > 4:
+                return None
+            row.append((ty, tx))
+        taps.append(row)
+    cpad = [-(-sg.C // 16) * 16 for sg in segs]
+    org, prc = [], []
+    for si, sg in enumerate(segs):
+        my_, mx_ = base.mults[si]
+        if direct[si]:
+            if (my_, mx_) != (2, 2):
+                return None
+            org.append((0, 0))
+            prc.append((1, 1))
+            continue
+        oys = [o for row in taps for (k, o) in row[si][0]] or [0]
+        oxs = [o for row in taps for (k, o) in row[si][1]] or [0]
+        oy0, ox0 = min(oys), min(oxs)
+        PR = (TR - 1) * my_ + (max(oys) - oy0) + 1
+        PC = (TC - 1) * mx_ + (max(oxs) - ox0) + 1
+        if sg.IW % 4:
+            return None                    # staged in aligned 4-pixel groups
+        PC = 4 * patch_units_per_row(PC, True, False)   # image columns: groups from the aligned start
+        if 2 * NS * PR * (PC // 4) > CONVQ_MAX_UNITS:
+            return None
+        org.append((oy0, ox0))
+        prc.append((PR, PC))
+    staged = [prc[si] for si in range(len(segs)) if not direct[si]]
+    pad = bool(staged) and convq_lds_bytes(NS, [convq_strides(NS, TR, TC, PR, PC) for PR, PC in staged]) \
+        <= CONVQ_LDS_BUDGET
+    if os.environ.get("FFC_CONVQ_PAD") == "0":
+        pad = False
+    qstride = [convq_strides(NS, TR, TC, PR, PC, pad) for (PR, PC) in prc]
+    phases, ktab, taptab = [], [], []
+    a_total = 0
+    Mpad = -(-M // MPAD) * MPAD
+    for pi, ph in enumerate(base.phases):
+        d = dict(py=ph.py, px=ph.px, PH=ph.PH, PW=ph.PW, T=[], kseg=[], tap_base=[], tap_h=[])
+        k = 0
+        kt_off = len(ktab)
+        for si, sg in enumerate(segs):
+            ty, tx = taps[pi][si]
+            T = len(ty) * len(tx)
+            d["T"].append(T)
+            d["kseg"].append(k)
+            d["tap_base"].append(len(taptab))
+            d["tap_h"].append(0)
+            tl = [(ky, oy, kx, ox) for (ky, oy) in ty for (kx, ox) in tx]
+            # the kernel runs exactly 4 taps per staged segment (1 per direct one): missing taps (tiny
+            # inputs) are padded with zero weights reading the patch origin
+            TT = 1 if direct[si] else 4
+            d["T"][-1] = TT
+            for t in range(TT):
+                taptab.append(((tl[t][1] - org[si][0]) << 16) | (tl[t][3] - org[si][1]) if t < T else 0)
+            for c0 in range(0, cpad[si], 16):            # K order: chunk, tap, channel
+                for t in range(TT):
+                    for ch in range(c0, c0 + 16):
+                        if t < T and ch < sg.C:
+                            ky, oy, kx, ox = tl[t]
+                            ktab.append((si | (ch << 4), oy, ox, ky | (kx << 16)))
+                        else:
+                            ktab.append(PAD_ENTRY)
+            k += cpad[si] * TT
+        if k == 0:
+            return None
+        d["Kpad"] = k
+        d["K"] = k
+        d["kt_off"] = kt_off
+        d["a_off"] = a_total
+        a_total += Mpad * k
+        phases.append(d)
+    return PatchPlan(B, M, base.OH, base.OW, base.Sy, base.Sx, segs, base.mults, cpad, org, prc,
+                     [not d for d in direct], [pc for (_, pc) in prc], phases,
+                     np.asarray(ktab, dtype=np.int32).reshape(-1, 4), np.asarray(taptab or [0], dtype=np.int32),
+                     a_total, cfg, NS, TR, TC, nrb, ncb, [16] * len(segs), True, mt, direct, qstride)
+
+
+def pick_convq_cfg(B, M, segs, min_blocks=256):
+    """the largest per-wave tile (MT x NTW) whose grid still has >= min_blocks workgroups per job
+    (2 x 32-channel M-tiles only when M >= 64); FFC_CONVQ_CFG forces one (A/B measurements)"""
+    force = os.environ.get("FFC_CONVQ_CFG")
+    if force is not None:
+        return plan_convq_job(B, M, segs, int(force))
+    cands = ([2] if M >= 64 else []) + [0, 1, 3]
+    plans = [q for q in (plan_convq_job(B, M, segs, c) for c in cands) if q is not None]
+    for q in plans:
+        if q.npb * (-(-M // (32 * q.mt))) >= min_blocks:
+            return q
+    return plans[-1] if plans else None
+
+
 def pick_patch_cfg(B, M, segs, min_blocks=512):
     """4-phase jobs: NTW=4 unless that leaves fewer than `min_blocks` workgroups.  512 (2 per CU)
     suits the f32-MFMA products; the split-bf16 products pay a per-group A split that 4 N-tiles
@@ -443,7 +584,7 @@ def build_patch_tiles(plans, nxcd: int = 8):
         for j in order:
             pl = plans[j]
             for pb in range(lo, min(hi, pl.npb)):
-                for m0 in range(0, pl.M, 32):
+                for m0 in range(0, pl.M, 32 * pl.mt):
                     ordered.append((j, m0, pb, 0))
     remap = xcd_remap(len(ordered), nxcd)
     return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)

@@ -243,6 +243,9 @@ def pick_pw_cfg(B, M, Q):
 # operand, six piece products), "f32" = v_mfma_f32_32x32x2_f32 (A/B measurements, tests)
 CONV_ARITH = __import__("os").environ.get("FFC_CONV_ARITH", "split")
 PRESPLIT_A = __import__("os").environ.get("FFC_CONVP_PRESPLIT", "0") == "1"   # A/B knob: A3 planes (off: measured neutral / -1 %)
+# stride-2 transposed-conv jobs on ffc_convq_forward (operands split once while staged) under the
+# split-bf16 products; "0" keeps them on ffc_convp_forward (A/B measurements, tests)
+USE_CONVQ = __import__("os").environ.get("FFC_CONVQ", "1") == "1"
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
@@ -281,13 +284,16 @@ class ConvExec:
 
     def __init__(self, B, M, segs, weights, device, pw_ok=False):
         pw_only = all(sg.kind == "pw" and not sg.pool and not sg.gate for sg in segs)
-        pp = _plan.pick_patch_cfg(B, M, segs, 128 if CONV_ARITH == "split" else 512) if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None
+        qq = (_plan.pick_convq_cfg(B, M, segs) if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only
+              else None)
+        pp = qq or (_plan.pick_patch_cfg(B, M, segs, 128 if CONV_ARITH == "split" else 512)
+                    if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None)
         if pw_ok and pw_only and PW_KERNEL == "pw":
             self.kind, self.plan = "pw", _plan.plan_job(B, M, segs)
             self.launch_key = ("pw", pick_pw_cfg(B, M, self.plan.OH * self.plan.OW))
         elif pp is not None:
             self.kind, self.plan = "patch", pp
-            self.launch_key = ("patch", pp.cfg)
+            self.launch_key = ("q" if pp.q else "patch", pp.cfg)
         else:
             self.kind, self.plan = "gemm", _plan.plan_job(B, M, segs)
             self.launch_key = ("gemm",)
@@ -299,7 +305,7 @@ class ConvExec:
         # pack, so the kernel loads the pieces instead of splitting each chunk's A in registers
         self.a3_stride = -(-self.A.numel() // 8) * 8
         self.A3 = (torch.zeros(3 * self.a3_stride, device=device, dtype=torch.int16)
-                   if self.kind == "patch" and CONV_ARITH == "split" and PRESPLIT_A else None)
+                   if self.kind == "patch" and CONV_ARITH == "split" and (PRESPLIT_A or self.plan.q) else None)
         self.has_bias = any(w[4] is not None for w in weights)
         self.bias = torch.empty(M, device=device, dtype=torch.float32) if self.has_bias else None
         self._packed = None
@@ -347,6 +353,9 @@ class ConvExec:
             s.pool = int(sg.pool)
             s.vec4 = int(pl.vec4[i])
             s.cc = pl.cc[i]
+            s.direct = int(pl.direct[i]) if pl.q else 0
+            if pl.q:
+                s.qrow, s.qsample = pl.qstride[i]
         for i, ph in enumerate(pl.phases):
             p = job.ph[i]
             p.py, p.px, p.PH, p.PW, p.Kpad, p.a_off = ph["py"], ph["px"], ph["PH"], ph["PW"], ph["Kpad"], ph["a_off"]
@@ -374,7 +383,11 @@ class ConvExec:
         check(lib().ffc_conv_pack(ctypes.byref(job), wp, lay, kh, kw, bp, self.A.data_ptr(),
                                   ptr(self.bias), torch.cuda.current_stream(self.device).cuda_stream),
               "ffc_conv_pack")
-        if self.A3 is not None:
+        if self.A3 is not None and self.plan.q:
+            # fragment-ordered split planes (one coalesced 1 KiB load per A fragment piece)
+            check(lib().ffc_convq_pack_a3(ctypes.byref(self.base_job()), self.A.data_ptr(), self.A3.data_ptr(),
+                                          torch.cuda.current_stream(self.device).cuda_stream), "ffc_convq_pack_a3")
+        elif self.A3 is not None:
             check(lib().ffc_split_bf16(self.A.data_ptr(), self.A.numel(), self.A3.data_ptr(), self.a3_stride,
                                        torch.cuda.current_stream(self.device).cuda_stream), "ffc_split_bf16")
         self._packed = key
@@ -408,7 +421,7 @@ class LaunchPlan:
             self.ntiles = sum(lib().ffc_pw_tiles(e.plan.M, e.plan.B, e.plan.OH * e.plan.OW, self.cfg) for e in execs)
             self.tiles = None
             return
-        if self.key[0] == "patch":
+        if self.key[0] in ("patch", "q"):
             self.cfg = self.key[1]
             tiles = _plan.build_patch_tiles([e.plan for e in execs])
             self._rows = [e.plan.npb * 4 for e in execs]
@@ -432,6 +445,10 @@ class LaunchPlan:
             if self.key[0] == "pw":
                 for jb in jobs:
                     check(L.ffc_pw_forward(ctypes.byref(jb), self.cfg, stream), "ffc_pw_forward")
+            elif self.key[0] == "q":
+                arr = (_lib.ConvPJob * len(jobs))(*jobs)
+                check(L.ffc_convq_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
+                      "ffc_convq_forward")
             elif self.key[0] == "patch":
                 arr = (_lib.ConvPJob * len(jobs))(*jobs)
                 cfg = self.cfg | (_lib.CONVP_EXACT_F32 if CONV_ARITH == "f32" else 0)

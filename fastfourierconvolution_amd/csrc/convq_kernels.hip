@@ -1,0 +1,689 @@
+// Stride-2 transposed convolution as an implicit GEMM with the operands pre-split for the
+// fp32-accurate bf16 MFMA products (gfx950) — the local-branch hot path of FFCTranspose
+// (layers/ffc/ffc_transpose.py:79-86, ConvTranspose2d k4 s2 p1) with SpectralTransform.conv2
+// (spectral_transform.py:70-71,108) folded in as a 1x1 segment at the output resolution.
+//
+// Why a second patch kernel (convp_kernels.hip keeps the f32-MFMA and pooled/strided paths):
+// the split-bf16 products need every fp32 operand split into three exact bf16 pieces (hi, mid,
+// lo: ffc_internal.h split3).  convp splits each B fragment in registers at every use, and every
+// input element is used by 16 (phase, tap) fragments of a ConvT k4 s2 — ~11 VALU instructions
+// per MFMA (profiles/r01j/pmc_sq_convp.txt).  Here each input element is split ONCE per
+// workgroup, while it is staged:
+//   * staging (global -> registers -> split -> LDS): a unit = 8 consecutive channels of one patch
+//     pixel, loaded as 8 fp32 values one chunk ahead (in flight under the current chunk's MFMAs),
+//     split, stored as three bf16x8 pieces with ds_write_b128 into the LDS image
+//     [half h][patch pixel][piece] (48 bytes per pixel-half: the three reads of a fragment are one
+//     address + immediate offsets 0/16/32, and 16 consecutive pixels hit 16 distinct bank slots);
+//   * K order inside a segment is (16-channel chunk, tap, channel): a B fragment (lane = pixel n,
+//     half h = 8 channels) is three ds_read_b128, no VALU;
+//   * A (packed weights, same K order) is pre-split into three bf16 planes (ffc_split_bf16) and
+//     loaded as three 16-byte loads per (k16 step, M-tile).
+// The 1x1 segment at the output resolution (conv2) has no reuse across phases or taps, so its B
+// fragments are read straight from global memory and split in registers ("direct" segment).
+//
+// Workgroup = 8 waves, warp-specialised: waves 0-3 compute the 4 phases (py, px) of a pixel block
+// of NS samples x TR x TC phase-grid pixels (32*NTW pixels) -- wave w: MT M-tiles of 32 output
+// channels x NTW N-tiles of 32 pixels of phase w, MFMAs fed from LDS and registers only -- while
+// waves 4-7 stage the next chunk (global loads, split, LDS stores) into the other buffer; one
+// barrier per chunk.  Each SIMD holds one computing and one staging wave, so the matrix pipe
+// is never shared and the staging latency is off the MFMA path.  The compute waves also load
+// A for the chunk at its start (tap 0's A one chunk ahead).  Epilogue (bias, addend, BN partial
+// slab rows [block*4 + wave], activation) as in convp.
+#include "ffc_internal.h"
+
+#include <string>
+
+namespace {
+
+constexpr int QTHREADS = 512;   // 4 compute waves + 4 staging waves
+
+struct ConvQArgs {
+    ffc_convp_job jobs[2];
+    const int4* tiles;
+    int ebuf;                  // bytes per LDS buffer (multiple of 256)
+};
+
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+#ifdef FFC_TRACE_Q
+// Diagnostic build only (tools/trace_convq.py): per workgroup 16 u64:
+// [0] realtime start [1] realtime end (compute wave 0) [2] HW_ID | XCC_ID << 32
+// compute wave 0 cycles: [3] barrier waits [4] A issue + B tap-0 read [5] MFMA taps [6] direct segs
+// [7] epilogue [8] total; staging wave 4 cycles: [9] loads (issue -> data) [10] split + LDS store
+// [11] barrier waits [12] total; [13] chunks
+__device__ unsigned long long g_ffc_trace_q[16 * 16384];
+#define QSTAMP(t)                                                                           \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    } while (0)
+#endif
+
+__device__ __forceinline__ u32x4 lds_read16(const char* base, int off) {
+    return *reinterpret_cast<const u32x4*>(base + off);
+}
+
+template <int MT, int NTW>
+__global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const ConvQArgs& args = args_byval;
+#endif
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave_id = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool stager = wave_id >= 4;
+    const int wave = wave_id & 3;            // compute waves: the phase
+    const int stid = tid - 256;              // staging waves: unit slot 0..255
+    const int h = lane >> 5, cl = lane & 31;
+    const int4 tile = args.tiles[blockIdx.x];
+    const int ji = __builtin_amdgcn_readfirstlane(tile.x);
+    const int m0 = __builtin_amdgcn_readfirstlane(tile.y);
+    const int pb = __builtin_amdgcn_readfirstlane(tile.z);
+    const ffc_convp_job& J = args.jobs[ji];
+    const ffc_convp_phase& P = J.ph[wave];
+    const int ebuf = args.ebuf;
+
+    const int NS = J.NS, TR = J.TR, TC = J.TC;
+    const int bs = pb / (J.nrb * J.ncb);
+    const int prem = pb - bs * J.nrb * J.ncb;
+    const int rb = prem / J.ncb, cb = prem - rb * J.ncb;
+    const int b0 = bs * NS, r0 = rb * TR, c0 = cb * TC;
+    const int TRC = TR * TC;
+    const int nseg = J.nseg;
+
+    // this lane's pixel of each N-tile (phase-grid coordinates inside the block)
+    int pns[NTW], pr_[NTW], pc_[NTW];
+    bool pv[NTW];
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        const int q = nt * 32 + cl;
+        const int ns = q / TRC;
+        const int rem = q - ns * TRC;
+        const int r = rem / TC, c = rem - r * TC;
+        pns[nt] = ns;
+        pr_[nt] = r;
+        pc_[nt] = c;
+        pv[nt] = ns < NS && b0 + ns < J.B && r0 + r < P.PH && c0 + c < P.PW;
+    }
+
+    floatx16 acc[MT][NTW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mt][nt][r] = 0.0f;
+
+#ifdef FFC_TRACE_Q
+    const unsigned long long tq_rt0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long tq_0, tq_a, tq_b, tq_c, tq_d, tq_bar = 0, tq_A = 0, tq_mf = 0;
+    QSTAMP(tq_0);
+#endif
+    // A in fragment order (ffc_convq_pack_a3): fragment (M-tile, 16-k step) = three 1 KiB planes, lane l's
+    // 16 bytes at l * 16: one fully coalesced dwordx4 per (fragment, piece)
+    const int ksteps = P.Kpad >> 4;
+    const uint16_t* __restrict__ Afrag = J.A3 + 3 * P.a_off + (size_t)(m0 >> 5) * ksteps * 1536 + lane * 8;
+    auto load_A = [&](int k, Split3 (&a)[MT]) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const uint16_t* f = Afrag + ((size_t)mt * ksteps + (k >> 4)) * 1536;
+            a[mt].hi = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(f));
+            a[mt].mid = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(f + 512));
+            a[mt].lo = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(f + 1024));
+        }
+    };
+
+    // ---------------- staged segments: chunks of 16 channels, patch image in LDS
+    // The patch rows are staged in aligned 4-pixel groups from xa = ix0 & ~3 (IW % 4 == 0: a group is
+    // wholly inside or outside the row): one staging unit = (sample, patch row, group, channel
+    // half) = 8 channels x 4 pixels = 8 coalesced 16-byte loads; pixel e of the group is split and
+    // stored at image column 4 g + e.  Image pixel (ns, row, col) of channel half h sits at
+    // 48 * ((h * NS + ns) * qsample + row * qrow + col) bytes; the lane pixel (pc) of the compute
+    // side is image column pc * mult_x + xoff, xoff = ix0 - xa.
+    struct {
+        const float* x;
+        long long sstride;         // floats per sample (C * IH * IW)
+        int C, IHW, nunits;
+        int sb;                    // sample of the unit (-1: outside the batch / input / unit range)
+        int off;                   // in-sample offset of channel 0 at the group's first pixel
+        int hu;                    // the unit's channel half
+        int wb;                    // LDS byte offset of the group's first pixel inside a buffer (-1: none)
+    } st;
+    auto stage_setup = [&](int s) {
+        const ffc_convp_seg& S = J.seg[s];
+        st.x = S.x;
+        st.C = S.C;
+        st.IHW = S.IH * S.IW;
+        st.sstride = (long long)S.C * st.IHW;
+        const int PR = S.PR, G = S.PC >> 2, QR = S.qrow, QS = S.qsample;
+        const int ngrp = NS * PR * G;
+        st.nunits = 2 * ngrp;
+        const int iy0 = r0 * S.mult_y + S.org_y;
+        const int xa = (c0 * S.mult_x + S.org_x) & ~3;
+        const int n = stid;
+        const int hu = n >= ngrp ? 1 : 0;
+        const int q = n - hu * ngrp;
+        const int g = q % G, q1 = q / G;
+        const int pr = q1 % PR, ns = q1 / PR;
+        const int b = b0 + ns, iy = iy0 + pr, ix = xa + 4 * g;
+        const bool ok = n < st.nunits && b < J.B && (unsigned)iy < (unsigned)S.IH && (unsigned)ix < (unsigned)S.IW;
+        st.sb = ok ? b : -1;
+        st.off = iy * S.IW + ix;
+        st.hu = hu;
+        st.wb = n < st.nunits ? ((hu * NS + ns) * QS + pr * QR + 4 * g) * 48 : -1;
+    };
+    // every lane loads (a clamped, valid address) and selects afterwards: no branch around a load
+    auto stage_load = [&](floatx4 (&sv)[8], int ch0) {
+        const int cb = ch0 + 8 * st.hu;
+        const bool inb = st.sb >= 0;
+        const float* src = st.x + (inb ? (long long)st.sb * st.sstride + st.off : 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool ok = inb && cb + j < st.C;
+            const floatx4 v = *reinterpret_cast<const floatx4*>(src + (ok ? (long long)(cb + j) * st.IHW : 0));
+            const floatx4 z = {0.0f, 0.0f, 0.0f, 0.0f};
+            sv[j] = ok ? v : z;
+        }
+    };
+    auto stage_store = [&](const floatx4 (&sv)[8], int wb, char* buf) {
+        if (wb >= 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float v8[8] = {sv[0][e], sv[1][e], sv[2][e], sv[3][e], sv[4][e], sv[5][e], sv[6][e], sv[7][e]};
+                const Split3 sp = split3(v8);
+                u32x4* d = reinterpret_cast<u32x4*>(buf + wb + 48 * e);
+                d[0] = __builtin_bit_cast(u32x4, sp.hi);
+                d[1] = __builtin_bit_cast(u32x4, sp.mid);
+                d[2] = __builtin_bit_cast(u32x4, sp.lo);
+            }
+        }
+    };
+
+    // per-segment compute geometry: LDS byte offset of the lane's B fragment per (N-tile, tap);
+    // staged segments always run 4 taps (the plan pads missing ones with zero weights)
+    int kseg = 0;
+    int fb[NTW];        // per N-tile: byte offset of (h, lane pixel) inside a buffer
+    int tb[4];          // per tap: byte offset of the tap's pixel shift
+    auto compute_setup = [&](int s) {
+        const ffc_convp_seg& S = J.seg[s];
+        kseg = P.kseg[s];
+        const int QR = S.qrow, QS = S.qsample, nimg = NS * QS;
+        const int ix0 = c0 * S.mult_x + S.org_x, xoff = ix0 - (ix0 & ~3);
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+            fb[nt] = (h * nimg + pns[nt] * QS + pr_[nt] * S.mult_y * QR + pc_[nt] * S.mult_x + xoff) * 48;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int tt = P.tap[s][t];
+            tb[t] = ((tt >> 16) * QR + (tt & 0xFFFF)) * 48;
+        }
+    };
+
+    // staged segments first (direct = 0), in job order
+    int nstaged = 0;
+    for (int s = 0; s < nseg; ++s)
+        if (!J.seg[s].direct) nstaged += J.seg[s].Cpad >> 4;
+
+    if (nstaged > 0) {
+        int ss = 0;
+        while (J.seg[ss].direct) ++ss;
+        int cs = ss, sch = 0, cch = 0;   // stager / computer: segment and channel of their chunk
+        auto advance_stager = [&]() {
+            if (sch >= J.seg[ss].Cpad) {
+                do { ++ss; } while (ss < nseg && J.seg[ss].direct);
+                sch = 0;
+                if (ss < nseg) stage_setup(ss);
+            }
+        };
+        // two loops with the same barrier count: the staging and compute waves' registers are then
+        // disjoint live ranges (one loop with role branches inside keeps both sets alive)
+        if (stager) {
+            // two register slots: the loads of chunk c + 2 are in flight while chunk c + 1 is split and
+            // stored, so a chunk's load latency overlaps a whole chunk period of MFMAs
+#ifdef FFC_TRACE_Q
+            unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0;
+            QSTAMP(q0);
+#endif
+            floatx4 sv0[8], sv1[8];
+            int wb0 = -1, wb1 = -1;
+            stage_setup(ss);
+            auto issue = [&](floatx4 (&dst)[8], int& wb) {   // the chunk at the load cursor (ss, sch)
+                if (ss < nseg) {
+                    stage_load(dst, sch);
+                    wb = st.wb;
+                    sch += 16;
+                    advance_stager();
+                } else {
+                    wb = -1;
+                }
+            };
+            auto store_timed = [&](const floatx4 (&src)[8], int wb, char* buf) {
+#ifdef FFC_TRACE_Q
+                QSTAMP(qa);
+                float chk = src[0][0] + src[7][3];
+                asm volatile("" ::"v"(chk));   // data arrived
+                QSTAMP(qb);
+                ql += qb - qa;
+                stage_store(src, wb, buf);
+                QSTAMP(qa);
+                qs += qa - qb;
+#else
+                stage_store(src, wb, buf);
+#endif
+            };
+            auto bar = [&]() {
+#ifdef FFC_TRACE_Q
+                QSTAMP(qa);
+#endif
+#ifndef FFC_QPROBE_NOBAR
+                __syncthreads();   // next buffer written; everyone done reading the other
+#endif
+#ifdef FFC_TRACE_Q
+                QSTAMP(qb);
+                qw += qb - qa;
+#endif
+            };
+            issue(sv0, wb0);                 // chunk 0
+            issue(sv1, wb1);                 // chunk 1 (if any)
+            store_timed(sv0, wb0, lds);
+            bar();
+            for (int ci = 0; ci < nstaged; ci += 2) {
+#ifndef FFC_QPROBE_NOSTAGE
+                if (ci + 2 < nstaged) issue(sv0, wb0);
+                if (ci + 1 < nstaged) store_timed(sv1, wb1, lds + ebuf);
+#endif
+                bar();
+                if (ci + 1 >= nstaged) break;
+#ifndef FFC_QPROBE_NOSTAGE
+                if (ci + 3 < nstaged) issue(sv1, wb1);
+                if (ci + 2 < nstaged) store_timed(sv0, wb0, lds);
+#endif
+                bar();
+            }
+#ifdef FFC_TRACE_Q
+            QSTAMP(qa);
+            if (tid == 256) {
+                unsigned long long* tr = g_ffc_trace_q + 16 * blockIdx.x;
+                tr[9] = ql;
+                tr[10] = qs;
+                tr[11] = qw;
+                tr[12] = qa - q0;
+                tr[13] = nstaged;
+            }
+#endif
+            return;   // no barrier follows
+        }
+        Split3 anext[MT];   // tap 0's A of the coming chunk
+        compute_setup(cs);
+        load_A(kseg, anext);
+#ifdef FFC_TRACE_Q
+        QSTAMP(tq_a);
+#endif
+        __syncthreads();
+#ifdef FFC_TRACE_Q
+        QSTAMP(tq_b);
+        tq_bar += tq_b - tq_a;
+#endif
+        for (int ci = 0; ci < nstaged; ++ci) {
+#ifdef FFC_TRACE_Q
+            QSTAMP(tq_a);
+#endif
+            const bool more = ci + 1 < nstaged;
+            const char* cur = lds + (ci & 1) * ebuf;
+            // the computer's next chunk (segment cn, channel chn) for the A prefetch
+            int cn = cs, chn = cch + 16;
+            if (chn >= J.seg[cs].Cpad && more) {
+                do { ++cn; } while (J.seg[cn].direct);
+                chn = 0;
+            }
+            Split3 a[4][MT];
+            const int kc = kseg + cch * 4;   // chunk-major, then tap, then channel
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) a[0][mt] = anext[mt];
+#ifdef FFC_QPROBE_NOA
+            if (ci == 0)
+#endif
+#pragma unroll
+            for (int t = 1; t < 4; ++t) load_A(kc + 16 * t, a[t]);
+            // next chunk's tap 0 (the last chunk reloads its own: no branch around the load)
+            load_A(more ? P.kseg[cn] + chn * 4 : kc, anext);
+            __builtin_amdgcn_sched_barrier(0);
+#ifdef FFC_TRACE_Q
+            QSTAMP(tq_b);
+            tq_A += tq_b - tq_a;
+#endif
+            // B fragments of a whole tap (NTW x 3 ds_read_b128) one tap ahead of its MFMAs
+            u32x4 bq[2][NTW][3];
+            auto read_tap = [&](int t, u32x4 (&dst)[NTW][3]) {
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) {
+                    const char* p1 = cur + fb[nt] + tb[t];
+                    dst[nt][0] = lds_read16(p1, 0);
+                    dst[nt][1] = lds_read16(p1, 16);
+                    dst[nt][2] = lds_read16(p1, 32);
+                }
+            };
+#ifndef FFC_QPROBE_NOMFMA
+            read_tap(0, bq[0]);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t + 1 < 4) read_tap(t + 1, bq[(t + 1) & 1]);
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) {
+                    Split3 b;
+                    b.hi = __builtin_bit_cast(bf16x8, bq[t & 1][nt][0]);
+                    b.mid = __builtin_bit_cast(bf16x8, bq[t & 1][nt][1]);
+                    b.lo = __builtin_bit_cast(bf16x8, bq[t & 1][nt][2]);
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = mfma_split3(a[t][mt], b, acc[mt][nt]);
+                }
+                // keep the next tap's reads ahead of this tap's MFMAs (the scheduler otherwise sinks
+                // each read to just before its first use and waits on it)
+                if (t + 1 < 4) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTW, 0);    // DS_READ
+                    __builtin_amdgcn_sched_group_barrier(0x8, 6 * NTW * MT, 0); // MFMA
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#endif
+#ifdef FFC_TRACE_Q
+            QSTAMP(tq_a);
+            tq_mf += tq_a - tq_b;
+#endif
+            cch += 16;
+            if (cch >= J.seg[cs].Cpad && more) {
+                cs = cn;
+                cch = 0;
+                compute_setup(cs);
+            }
+#ifdef FFC_TRACE_Q
+            QSTAMP(tq_a);
+#endif
+#ifndef FFC_QPROBE_NOBAR
+            __syncthreads();   // next buffer written; everyone done reading this one
+#endif
+#ifdef FFC_TRACE_Q
+            QSTAMP(tq_b);
+            tq_bar += tq_b - tq_a;
+#endif
+        }
+    }
+#ifdef FFC_TRACE_Q
+    QSTAMP(tq_c);
+#endif
+    if (stager) return;   // no barrier follows
+
+    // ---------------- direct segments (1x1 at the output resolution): B straight from global
+    for (int s = 0; s < nseg; ++s) {
+        const ffc_convp_seg& S = J.seg[s];
+        if (!S.direct) continue;
+        const int IHW = S.IH * S.IW;
+        const float* xp[NTW];
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+            const int oy = (r0 + pr_[nt]) * J.Sy + P.py, ox = (c0 + pc_[nt]) * J.Sx + P.px;
+            const int b = pv[nt] ? b0 + pns[nt] : 0;
+            xp[nt] = S.x + ((long long)b * S.C + 8 * h) * IHW + (pv[nt] ? oy * S.IW + ox : 0);
+        }
+        for (int ch0 = 0; ch0 < S.Cpad; ch0 += 16) {
+            Split3 a[MT];
+            load_A(P.kseg[s] + ch0, a);
+            float bv[NTW][8];
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const bool ok = pv[nt] && ch0 + 8 * h + j < S.C;
+                    const float v = (ok ? xp[nt] : S.x)[ok ? (long long)(ch0 + j) * IHW : 0];
+                    bv[nt][j] = ok ? v : 0.0f;
+                }
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) {
+                const Split3 b = split3(bv[nt]);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = mfma_split3(a[mt], b, acc[mt][nt]);
+            }
+        }
+    }
+
+    // ---------------- epilogue: bias/addend, BN partials, activation, store
+    const size_t plane = (size_t)J.OH * J.OW;
+    int ob[NTW], oo[NTW];
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        ob[nt] = b0 + pns[nt];
+        oo[nt] = ((r0 + pr_[nt]) * J.Sy + P.py) * J.OW + ((c0 + pc_[nt]) * J.Sx + P.px);
+    }
+    auto epilogue = [&](floatx16 (&tacc)[NTW], const int mbase) {
+        if (J.bias || J.addend) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mbase + (r & 3) + 8 * (r >> 2);
+                if (m >= J.M) continue;
+                const float bv = J.bias ? J.bias[m] : 0.0f;
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) {
+                    float v = tacc[nt][r] + bv;
+                    if (J.addend && pv[nt]) v += J.addend[((size_t)ob[nt] * J.M + m) * plane + oo[nt]];
+                    tacc[nt][r] = v;
+                }
+            }
+        }
+        if (J.stats) {
+            float cntl = 0.0f;
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) cntl += pv[nt] ? 1.0f : 0.0f;
+            const float cnt = ffc::half_wave_sum(cntl);
+            float4* stp = reinterpret_cast<float4*>(J.stats) + ((size_t)pb * 4 + wave) * J.M;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mbase + (r & 3) + 8 * (r >> 2);
+                float s = 0.0f;
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) s += pv[nt] ? tacc[nt][r] : 0.0f;
+                const float mean = cnt > 0.0f ? ffc::half_wave_sum(s) / cnt : 0.0f;
+                float q = 0.0f;
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) {
+                    const float d = pv[nt] ? tacc[nt][r] - mean : 0.0f;
+                    q += d * d;
+                }
+                const float m2 = ffc::half_wave_sum(q);
+                if (cl == 0 && m < J.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
+            }
+        }
+        auto store = [&](auto actf) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mbase + (r & 3) + 8 * (r >> 2);
+                if (m < J.M) {
+#pragma unroll
+                    for (int nt = 0; nt < NTW; ++nt)
+                        if (pv[nt]) J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = actf(tacc[nt][r]);
+                }
+            }
+        };
+        const float ap = J.act_param;
+        switch (J.act) {
+            case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
+            case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
+            case FFC_ACT_TANH: store([](float v) { return tanhf(v); }); break;
+            case FFC_ACT_SIGMOID: store([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
+            case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
+            default: store([](float v) { return v; }); break;
+        }
+    };
+#ifdef FFC_QPROBE_NOEPI
+    if (acc[0][0][0] != 1234.5f) return;   // keep the accumulators live, skip the stores
+#endif
+#ifdef FFC_TRACE_Q
+    QSTAMP(tq_d);
+#endif
+    epilogue(acc[0], m0 + 4 * h);
+    if constexpr (MT > 1) epilogue(acc[1], m0 + 32 + 4 * h);
+#ifdef FFC_TRACE_Q
+    {
+        unsigned long long tq_e;
+        QSTAMP(tq_e);
+        if (tid == 0) {
+            unsigned long long* tr = g_ffc_trace_q + 16 * blockIdx.x;
+            tr[0] = tq_rt0;
+            tr[1] = __builtin_amdgcn_s_memrealtime();
+            tr[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                    ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+            tr[3] = tq_bar;
+            tr[4] = tq_A;
+            tr[5] = tq_mf;
+            tr[6] = tq_d - tq_c;
+            tr[7] = tq_e - tq_d;
+            tr[8] = tq_e - tq_0;
+        }
+    }
+#endif
+}
+
+template <int MT, int NTW>
+int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s) {
+    auto k = convq_kernel<MT, NTW>;
+    if (lds > 64 * 1024) {
+        static bool raised = false;   // per instantiation
+        if (!raised) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) {
+                ffc::set_error(std::string("ffc_convq_forward: hipFuncSetAttribute: ") + hipGetErrorString(e));
+                return FFC_E_LAUNCH;
+            }
+            raised = true;
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(ntiles), dim3(QTHREADS), lds, s, a);
+    return ffc::launch_status("ffc_convq_forward");
+}
+
+}  // namespace
+
+namespace {
+// A[phase][Mpad][Kpad] fp32 -> fragment-ordered split planes: element
+// 3 * a_off + ((mtile * Kpad/16 + kstep) * 3 + piece) * 512 + lane * 8 + j  holds piece `piece` of
+// A[m = 32 * mtile + (lane & 31)][k = 16 * kstep + 8 * (lane >> 5) + j]
+__global__ void pack_a3_kernel(const float* __restrict__ A, ffc_convp_job J, uint16_t* __restrict__ A3, long long total) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+        // i = (phase-local fragment lane) over all phases: find the phase
+        long long r = i;
+        int p = 0;
+        long long nfr = 0;
+        for (; p < J.nphase; ++p) {
+            nfr = (long long)(J.Mpad >> 5) * (J.ph[p].Kpad >> 4) * 64;
+            if (r < nfr) break;
+            r -= nfr;
+        }
+        const int lane = (int)(r & 63);
+        const long long fr = r >> 6;
+        const int ks = J.ph[p].Kpad >> 4;
+        const int mtile = (int)(fr / ks), kstep = (int)(fr - (long long)mtile * ks);
+        const int m = 32 * mtile + (lane & 31), k0 = 16 * kstep + 8 * (lane >> 5);
+        const float* src = A + J.ph[p].a_off + (size_t)m * J.ph[p].Kpad + k0;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = src[j];
+        const Split3 sp = split3(v);
+        uint16_t* dst = A3 + 3 * J.ph[p].a_off + (fr * 3) * 512 + lane * 8;
+        *reinterpret_cast<u32x4*>(dst) = __builtin_bit_cast(u32x4, sp.hi);
+        *reinterpret_cast<u32x4*>(dst + 512) = __builtin_bit_cast(u32x4, sp.mid);
+        *reinterpret_cast<u32x4*>(dst + 1024) = __builtin_bit_cast(u32x4, sp.lo);
+    }
+}
+}  // namespace
+
+extern "C" int ffc_convq_pack_a3(const ffc_convp_job* job, const float* A, uint16_t* A3, void* stream) {
+    FFC_CHECK_ARG(job && A && A3 && job->nphase >= 1 && job->nphase <= 4 && job->Mpad % 32 == 0,
+                  "ffc_convq_pack_a3: bad args");
+    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(A3) & 15) == 0, "ffc_convq_pack_a3: A3 must be 16-byte aligned");
+    long long total = 0;
+    for (int p = 0; p < job->nphase; ++p) {
+        FFC_CHECK_ARG(job->ph[p].Kpad % 16 == 0 && job->ph[p].Kpad > 0, "ffc_convq_pack_a3: Kpad % 16");
+        total += (long long)(job->Mpad >> 5) * (job->ph[p].Kpad >> 4) * 64;
+    }
+    const long long blocks = (total + 255) / 256;
+    hipLaunchKernelGGL(pack_a3_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                       (hipStream_t)stream, A, *job, A3, total);
+    return ffc::launch_status("ffc_convq_pack_a3");
+}
+
+#ifdef FFC_TRACE_Q
+extern "C" int ffc_debug_trace_read_q(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_ffc_trace_q), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
+extern "C" int ffc_convq_config(int cfg, int* mt, int* ntw) {
+    static const int T[4][2] = {{1, 4}, {1, 2}, {2, 2}, {1, 1}};
+    if (cfg < 0 || cfg > 3 || !mt || !ntw) return FFC_E_INVALID;
+    *mt = T[cfg][0];
+    *ntw = T[cfg][1];
+    return FFC_OK;
+}
+
+extern "C" int ffc_convq_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
+                                 void* stream) {
+    FFC_CHECK_ARG(jobs && tiles && njobs >= 1 && njobs <= 2 && ntiles > 0, "ffc_convq_forward: bad args");
+    int MT = 0, NTW = 0;
+    FFC_CHECK_ARG(ffc_convq_config(cfg, &MT, &NTW) == FFC_OK, "ffc_convq_forward: unknown cfg");
+    int npix_max = 0;
+    for (int j = 0; j < njobs; ++j) {
+        const ffc_convp_job& J = jobs[j];
+        FFC_CHECK_ARG(J.A3 && J.out && J.B > 0 && J.M > 0, "ffc_convq_forward: incomplete job (needs the A3 planes)");
+        FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(J.A3) & 15) == 0 && J.a3_stride % 8 == 0,
+                      "ffc_convq_forward: A3 planes need 16-byte alignment");
+        FFC_CHECK_ARG(J.nphase == 4 && J.Sy == 2 && J.Sx == 2, "ffc_convq_forward: 4-phase (stride-2) jobs only");
+        FFC_CHECK_ARG(J.nseg >= 1 && J.nseg <= FFC_MAX_SEG, "ffc_convq_forward: nseg out of range");
+        FFC_CHECK_ARG(J.Mpad % 128 == 0 && J.Mpad >= J.M, "ffc_convq_forward: Mpad");
+        FFC_CHECK_ARG(J.NS > 0 && J.TR > 0 && J.TC > 0 && J.nrb > 0 && J.ncb > 0 && J.NS * J.TR * J.TC <= 32 * NTW,
+                      "ffc_convq_forward: pixel block");
+        for (int p = 0; p < 4; ++p) FFC_CHECK_ARG(J.ph[p].Kpad % 16 == 0, "ffc_convq_forward: Kpad % 16");
+        for (int s = 0; s < J.nseg; ++s) {
+            const ffc_convp_seg& S = J.seg[s];
+            FFC_CHECK_ARG(S.x && S.Cpad % 16 == 0 && S.Cpad >= S.C && S.cc == 16, "ffc_convq_forward: segment channels");
+            FFC_CHECK_ARG(!S.pool && !S.gate, "ffc_convq_forward: pooled / gated segments use ffc_conv_forward");
+            for (int p = 0; p < 4; ++p) {
+                const int T = J.ph[p].T[s];
+                FFC_CHECK_ARG(S.direct ? T == 1 : T == 4,
+                              "ffc_convq_forward: taps per phase (4 staged, 1 direct; the plan pads)");
+            }
+            if (S.direct) {
+                FFC_CHECK_ARG(S.mult_y == 2 && S.mult_x == 2 && S.IH == J.OH && S.IW == J.OW,
+                              "ffc_convq_forward: direct segments are 1x1 at the output resolution");
+            } else {
+                FFC_CHECK_ARG(S.PR > 0 && S.PC > 0 && S.PC % 4 == 0 && S.qrow >= S.PC && S.qsample >= S.PR * S.qrow,
+                              "ffc_convq_forward: patch shape / LDS strides");
+                FFC_CHECK_ARG(S.vec4 && S.IW % 4 == 0 && (reinterpret_cast<uintptr_t>(S.x) & 15) == 0,
+                              "ffc_convq_forward: staged segments need IW % 4 == 0 and a 16-byte aligned input");
+                FFC_CHECK_ARG(2 * J.NS * S.PR * (S.PC / 4) <= 256,
+                              "ffc_convq_forward: patch too large for the staging waves (one unit per thread)");
+                const int npix = J.NS * S.qsample;   // LDS image pixels per channel half
+                if (npix > npix_max) npix_max = npix;
+            }
+        }
+    }
+    const size_t ebuf = ((size_t)npix_max * 96 + 255) / 256 * 256 + 256;   // + 256 B: buffers start on other banks
+    const size_t lds = npix_max > 0 ? 2 * ebuf : 16;
+    FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_convq_forward: patch too large");
+    ConvQArgs a;
+    a.ebuf = (int)ebuf;
+    a.jobs[0] = jobs[0];
+    a.jobs[1] = jobs[njobs > 1 ? 1 : 0];
+    a.tiles = reinterpret_cast<const int4*>(tiles);
+    hipStream_t s = (hipStream_t)stream;
+    switch (cfg) {
+        case 0: return launch_q<1, 4>(a, ntiles, lds, s);
+        case 1: return launch_q<1, 2>(a, ntiles, lds, s);
+        case 2: return launch_q<2, 2>(a, ntiles, lds, s);
+        case 3: return launch_q<1, 1>(a, ntiles, lds, s);
+    }
+    ffc::set_error("ffc_convq_forward: unknown cfg");
+    return FFC_E_INVALID;
+}

@@ -131,7 +131,11 @@ typedef struct ffc_convp_seg {
     int pool;
     int vec4;            /* 1: stage the patch in 16-byte groups (IW % 4 == 0, x 16-byte aligned) */
     int cc;              /* channels per chunk: 16 (taps 1, 2, 4) or 4 (16 taps) */
-    int pad_;
+    int direct;          /* ffc_convq_forward only: 1 = a 1x1 segment at the output resolution whose B
+                          * fragments are read straight from x (no patch); 0 = staged through LDS */
+    int qrow, qsample;   /* ffc_convq_forward only: LDS pixel strides of a patch row / sample (>= PC,
+                          * >= PR * qrow), padded so that the 16 lanes of a ds_read_b128 group hit 16
+                          * distinct bank slots */
 } ffc_convp_seg;
 
 typedef struct ffc_convp_phase {
@@ -173,6 +177,25 @@ typedef struct ffc_convp_job {
  * The pre-split packed weights of the split-bf16 patch conv (ffc_convp_job.A3). */
 int ffc_split_bf16(const float* x, long long n, uint16_t* planes, long long stride, void* stream);
 int ffc_convp_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
+                      void* stream);
+
+/* Stride-2 transposed convolution jobs (4 phases, FFCTranspose's ConvTranspose2d k4 s2 p1 + the folded
+ * SpectralTransform.conv2, layers/ffc/ffc_transpose.py:79-106, spectral_transform.py:108) with the
+ * operands pre-split for the fp32-accurate split-bf16 MFMA products: each input element is split
+ * into three bf16 pieces ONCE per workgroup while it is staged into LDS (ffc_convp_forward splits
+ * every B fragment at every use).  Same ffc_convp_job, with: K order per segment = (16-channel
+ * chunk, tap, channel); A3 (pre-split packed weights) required; staged segments' PR x PC = the
+ * patch in pixels (PC = row length), cc = 16; direct segments (1x1 at the output resolution, 1 tap)
+ * read B from global memory.  tiles: int4 {job, m0, pixel block, 0}, m0 in steps of 32 * MT.
+ * cfg 0..3 -> (MT M-tiles of 32 channels, NTW N-tiles of 32 pixels) per wave via ffc_convq_config. */
+int ffc_convq_config(int cfg, int* mt, int* ntw);
+/* The A3 operand of ffc_convq_forward: the packed weights A (ffc_conv_pack, phases at a_off, rows Mpad,
+ * Kpad per phase) split into three bf16 pieces and laid out in MFMA fragment order, element
+ * 3 * a_off + ((mtile * Kpad/16 + kstep) * 3 + piece) * 512 + lane * 8 + j for
+ * A[32 * mtile + (lane & 31)][16 * kstep + 8 * (lane >> 5) + j] (one 1 KiB coalesced load per fragment
+ * piece); A3 holds 3 * (total A floats) elements, 16-byte aligned. */
+int ffc_convq_pack_a3(const ffc_convp_job* job, const float* A, uint16_t* A3, void* stream);
+int ffc_convq_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                       void* stream);
 
 /* Weight packing for one job: A[phase][Mpad][Kpad] (zero padded), bias_out[M] = sum of

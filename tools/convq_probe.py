@@ -1,0 +1,84 @@
+"""Per-layer timing of the stride-2 ConvT launches (out_l + out_g jobs of one FFCTranspose layer,
+conv2 folded in) on ffc_convq_forward for every cfg and on ffc_convp_forward, HIP events over
+repeated launches.  Diagnostic only.   usage: convq_probe.py [B] [gen64|fgan128]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fastfourierconvolution_amd import _plan, _runtime as rt  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+model = sys.argv[2] if len(sys.argv) > 2 else "gen64"
+dev = torch.device("cuda", 0)
+# (C_l = C_g in, IH, M_l = M_g out, c of the ST = conv2 input channels)
+LAYERS = {"gen64": [(256, 4, 128, 64), (128, 8, 64, 32), (64, 16, 32, 16)],
+          "fgan128": [(128, 8, 64, 32), (64, 16, 32, 16), (32, 32, 64, 32), (32, 64, 64, 32)]}[model]
+
+
+def job_pair(C, IH, M, c):
+    g = torch.Generator().manual_seed(C + IH)
+    xl = torch.randn(B, C, IH, IH, generator=g).to(dev)
+    xg = torch.randn(B, C, IH, IH, generator=g).to(dev)
+    v = torch.randn(B, c, 2 * IH, 2 * IH, generator=g).to(dev)
+    wl = torch.randn(C, M, 4, 4, generator=g).to(dev) * 0.02
+    wg = torch.randn(C, M, 4, 4, generator=g).to(dev) * 0.02
+    wlg = torch.randn(C, M, 4, 4, generator=g).to(dev) * 0.02
+    w2 = torch.randn(M, c, 1, 1, generator=g).to(dev) * 0.02
+    segT = _plan.Seg("convT", C, IH, IH, 4, 2, 1)
+    jobs = [([segT, segT], [(wl, 1, 4, 4, None), (wg, 1, 4, 4, None)], [xl, xg]),
+            ([segT, _plan.Seg("pw", c, 2 * IH, 2 * IH)], [(wlg, 1, 4, 4, None), (w2, 0, 1, 1, None)], [xl, v])]
+    return jobs
+
+
+def time_layer(jobs, reps=20):
+    execs = [rt.ConvExec(B, w[0][0].shape[1] if w[0][1] == 1 else w[0][0].shape[0], segs, w, dev)
+             for segs, w, _ in jobs]
+    groups = {}
+    for e, (segs, w, xs) in zip(execs, jobs):
+        groups.setdefault(e.launch_key, []).append((e, xs))
+    launches = []
+    for key, items in groups.items():
+        lp = rt.LaunchPlan([e for e, _ in items], dev)
+        outs = [torch.empty(B, e.plan.M, e.plan.OH, e.plan.OW, device=dev) for e, _ in items]
+        structs = [e.job([(x, None) for x in xs], o) for (e, xs), o in zip(items, outs)]
+        launches.append((lp, structs, sum(e.flops for e, _ in items)))
+    s = torch.cuda.current_stream().cuda_stream
+    for lp, st, fl in launches:
+        lp.launch(st, s, fl)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        for lp, st, fl in launches:
+            lp.launch(st, s, fl)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    fl = sum(f for _, _, f in launches)
+    keys = "+".join(f"{lp.key}:{lp.ntiles}" for lp, _, _ in launches)
+    return us, fl / us / 1e6, keys
+
+
+def main():
+  for C, IH, M, c in LAYERS:
+    jobs = job_pair(C, IH, M, c)
+    row = [f"C{C}@{IH}x{IH}->M{M}"]
+    for var in ["convp", 0, 1, 2, 3]:
+        if var == "convp":
+            rt.USE_CONVQ = False
+            os.environ.pop("FFC_CONVQ_CFG", None)
+        else:
+            rt.USE_CONVQ = True
+            os.environ["FFC_CONVQ_CFG"] = str(var)
+        try:
+            us, tf, keys = time_layer(jobs)
+            row.append(f"{var}: {us:7.1f}us {tf:6.1f}TF [{keys}]")
+        except Exception as ex:  # noqa: BLE001
+            row.append(f"{var}: n/a ({type(ex).__name__})")
+    print(" | ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
