@@ -518,18 +518,27 @@ def plan_convq_job(B: int, M: int, segs, cfg: int):
                      a_total, cfg, NS, TR, TC, nrb, ncb, [16] * len(segs), True, mt, direct, qstride)
 
 
-def pick_convq_cfg(B, M, segs, min_blocks=256):
-    """the largest per-wave tile (MT x NTW) whose grid still has >= min_blocks workgroups per job
-    (2 x 32-channel M-tiles only when M >= 64); FFC_CONVQ_CFG forces one (A/B measurements)"""
+def convq_cost(q) -> float:
+    """Cycle estimate of a convq plan, fitted on MI355X (tools/convq_probe.py, r02): the workgroups
+    run in rounds of 256 CUs x (2 workgroups per CU for the (1, 1) tile, else 1), each chunk costs
+    768 cycles per 32 x 32 MFMA tile of a wave plus ~5500 cycles of fixed per-chunk latency
+    (staging hand-off, A loads, barrier); the pair of jobs of a layer is assumed alike."""
+    chunks = sum(c // 16 for c, d in zip(q.cpad, q.direct) if not d) + sum(c // 16 for c, d in zip(q.cpad, q.direct) if d)
+    wgs = 2 * q.npb * (-(-q.M // (32 * q.mt)))
+    mt, ntw = CONVQ_CFGS[q.cfg]
+    slots = 256 * (2 if (mt, ntw) == (1, 1) else 1)
+    return -(-wgs // slots) * chunks * (768.0 * mt * ntw + 5500.0)
+
+
+def pick_convq_cfg(B, M, segs):
+    """the convq configuration with the lowest convq_cost (MT = 2 only when M >= 64);
+    FFC_CONVQ_CFG forces one (A/B measurements)"""
     force = os.environ.get("FFC_CONVQ_CFG")
     if force is not None:
         return plan_convq_job(B, M, segs, int(force))
-    cands = ([2] if M >= 64 else []) + [0, 1, 3]
+    cands = ([0, 2] if M >= 64 else [0]) + [1, 3]
     plans = [q for q in (plan_convq_job(B, M, segs, c) for c in cands) if q is not None]
-    for q in plans:
-        if q.npb * (-(-M // (32 * q.mt))) >= min_blocks:
-            return q
-    return plans[-1] if plans else None
+    return min(plans, key=convq_cost) if plans else None
 
 
 def pick_patch_cfg(B, M, segs, min_blocks=512):

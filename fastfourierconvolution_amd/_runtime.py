@@ -243,9 +243,14 @@ def pick_pw_cfg(B, M, Q):
 # operand, six piece products), "f32" = v_mfma_f32_32x32x2_f32 (A/B measurements, tests)
 CONV_ARITH = __import__("os").environ.get("FFC_CONV_ARITH", "split")
 PRESPLIT_A = __import__("os").environ.get("FFC_CONVP_PRESPLIT", "0") == "1"   # A/B knob: A3 planes (off: measured neutral / -1 %)
-# stride-2 transposed-conv jobs on ffc_convq_forward (operands split once while staged) under the
-# split-bf16 products; "0" keeps them on ffc_convp_forward (A/B measurements, tests)
-USE_CONVQ = __import__("os").environ.get("FFC_CONVQ", "1") == "1"
+# stride-2 transposed-conv jobs on ffc_convq_forward (operands split once while staged, warp-specialised)
+# under the split-bf16 products.  It wins where the grid is small (<= CONVQ_MAX_CONVP_TILES convp
+# workgroups per job: the strong-scaling shards, fgan128's low-resolution layers) and loses to
+# ffc_convp_forward on large grids (measured, tools/convq_probe.py): "auto" picks per job, "1" /
+# "force" always convq where it applies, "0" never
+USE_CONVQ = __import__("os").environ.get("FFC_CONVQ", "auto") != "0"
+CONVQ_FORCE = __import__("os").environ.get("FFC_CONVQ", "auto") in ("1", "force")
+CONVQ_MAX_CONVP_TILES = 256
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
@@ -284,10 +289,11 @@ class ConvExec:
 
     def __init__(self, B, M, segs, weights, device, pw_ok=False):
         pw_only = all(sg.kind == "pw" and not sg.pool and not sg.gate for sg in segs)
-        qq = (_plan.pick_convq_cfg(B, M, segs) if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only
-              else None)
-        pp = qq or (_plan.pick_patch_cfg(B, M, segs, 128 if CONV_ARITH == "split" else 512)
-                    if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None)
+        pp = (_plan.pick_patch_cfg(B, M, segs, 128 if CONV_ARITH == "split" else 512)
+              if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None)
+        if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and (
+                CONVQ_FORCE or pp is None or pp.npb * (-(-M // 32)) <= CONVQ_MAX_CONVP_TILES):
+            pp = _plan.pick_convq_cfg(B, M, segs) or pp
         if pw_ok and pw_only and PW_KERNEL == "pw":
             self.kind, self.plan = "pw", _plan.plan_job(B, M, segs)
             self.launch_key = ("pw", pick_pw_cfg(B, M, self.plan.OH * self.plan.OW))
