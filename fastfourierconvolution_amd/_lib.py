@@ -76,6 +76,9 @@ SIGNATURES = [
     ("ffc_convq_config", c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("ffc_convq_pack_a3", c_int, [ctypes.POINTER(ConvPJob), c_void_p, c_void_p, c_void_p]),
     ("ffc_convq_forward", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_int, c_void_p]),
+    ("ffc_convq_split_floats", ctypes.c_longlong, [c_int, c_int, c_int]),
+    ("ffc_convq_forward_split", c_int, [ctypes.POINTER(ConvPJob), c_int, c_void_p, c_int, c_void_p, c_int, c_int,
+                                        c_int, c_void_p, c_void_p]),
     ("ffc_split_bf16", c_int, [c_void_p, ctypes.c_longlong, c_void_p, ctypes.c_longlong, c_void_p]),
     ("ffc_pw_forward", c_int, [ctypes.POINTER(ConvJob), c_int, c_void_p]),
     ("ffc_pw_tiles", c_int, [c_int, c_int, c_int, c_int]),

@@ -273,6 +273,7 @@ class PatchPlan:
     mt: int = 1          # convq: M-tiles of 32 channels per wave (tiles step m0 by 32 * mt)
     direct: list = field(default_factory=list)   # convq: per segment, B read straight from global
     qstride: list = field(default_factory=list)  # convq: per segment LDS (row, sample) pixel strides
+    ksplit: int = 1      # convq: K splits per output tile (ffc_convq_forward_split)
 
     @property
     def Mpad(self):
@@ -518,27 +519,105 @@ def plan_convq_job(B: int, M: int, segs, cfg: int):
                      a_total, cfg, NS, TR, TC, nrb, ncb, [16] * len(segs), True, mt, direct, qstride)
 
 
-def convq_cost(q) -> float:
+CONVQ_SPLIT_FIXED = 17500.0  # cycles: partial stores + the reduce launch (~7 us measured, r02 sweep)
+
+
+def convq_chunks(q) -> int:
+    """16-channel chunks of K per output tile (staged and direct segments)"""
+    return sum(c // 16 for c in q.cpad)
+
+
+def convq_cost(q, ksplit: int = 1) -> float:
     """Cycle estimate of a convq plan, fitted on MI355X (tools/convq_probe.py, r02): the workgroups
     run in rounds of 256 CUs x (2 workgroups per CU for the (1, 1) tile, else 1), each chunk costs
     768 cycles per 32 x 32 MFMA tile of a wave plus ~5500 cycles of fixed per-chunk latency
-    (staging hand-off, A loads, barrier); the pair of jobs of a layer is assumed alike."""
-    chunks = sum(c // 16 for c, d in zip(q.cpad, q.direct) if not d) + sum(c // 16 for c, d in zip(q.cpad, q.direct) if d)
-    wgs = 2 * q.npb * (-(-q.M // (32 * q.mt)))
+    (staging hand-off, A loads, barrier); a K split runs ceil(chunks / ksplit) chunks per
+    workgroup on ksplit x the workgroups, plus the partial-sum hand-off."""
+    wgs = q.npb * (-(-q.M // (32 * q.mt))) * ksplit
     mt, ntw = CONVQ_CFGS[q.cfg]
     slots = 256 * (2 if (mt, ntw) == (1, 1) else 1)
-    return -(-wgs // slots) * chunks * (768.0 * mt * ntw + 5500.0)
+    per_wg = -(-convq_chunks(q) // ksplit) * (768.0 * mt * ntw + 5500.0)
+    return -(-wgs // slots) * (per_wg + (CONVQ_SPLIT_FIXED if ksplit > 1 else 0.0))
+
+
+# Measured (cfg, ksplit) per convq launch group: tools/tune_convq.py sweeps every configuration
+# of the timed layer shapes on MI355X and writes convq_tuned.json; the cost model below is the
+# fallback for shapes the table does not hold.
+_TUNED = None
+
+
+def job_signature(B, M, segs) -> tuple:
+    return (int(B), int(M), tuple((sg.kind, sg.C, sg.IH, sg.IW, sg.k, sg.s, sg.p, sg.d, sg.op, sg.pool, sg.gate)
+                                  for sg in segs))
+
+
+def convq_tuned():
+    """{job signature: cfg}, {group signature (sorted job signatures): (cfg, ksplit)}"""
+    global _TUNED
+    if _TUNED is None:
+        import json
+        jobs, groups = {}, {}
+        path = os.environ.get("FFC_CONVQ_TUNED", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                               "convq_tuned.json"))
+        if path and os.path.exists(path):
+            with open(path) as f:
+                for e in json.load(f)["entries"]:
+                    sigs = tuple(sorted((B, M, tuple(tuple(sg) for sg in segs)) for B, M, segs in e["jobs"]))
+                    groups[sigs] = (int(e["cfg"]), int(e["ksplit"]))
+                    for sg in sigs:
+                        jobs[sg] = int(e["cfg"])
+        _TUNED = (jobs, groups)
+    return _TUNED
+
+
+def pick_convq_ksplit(q) -> int:
+    """K splits for a convq plan: the cheapest of 1, 2, 4, 8 by convq_cost with at least 4 chunks
+    per split; FFC_CONVQ_KSPLIT forces one (A/B measurements)"""
+    return pick_convq_ksplit_group([q])
+
+
+def pick_convq_ksplit_group(plans) -> int:
+    """one K split for the jobs of one convq launch (they share the grid): the cheapest by the
+    summed convq_cost, at least 4 chunks per split in every job; FFC_CONVQ_KSPLIT forces one"""
+    cmin = min(convq_chunks(q) for q in plans)
+    force = os.environ.get("FFC_CONVQ_KSPLIT")
+    if force is not None:
+        return max(1, min(8, int(force), cmin))
+    tuned = convq_tuned()[1].get(tuple(sorted(job_signature(q.B, q.M, q.segs) for q in plans)))
+    if tuned is not None and tuned[0] == plans[0].cfg:
+        return max(1, min(tuned[1], cmin))
+    ks = [k for k in (1, 2, 4, 8) if k == 1 or cmin >= 4 * k]
+    return min(ks, key=lambda k: (sum(convq_cost(q, k) for q in plans), k))
+
+
+def convq_slot_tiles(tiles) -> np.ndarray:
+    """the slot table of a K-split tile table: int32 [nslots, 4] {job, m0, pixel block, 0} in slot
+    order (split 0's row of every slot)"""
+    first = tiles[(tiles[:, 3] & 7) == 0]
+    out = np.zeros((first.shape[0], 4), dtype=np.int32)
+    out[first[:, 3] >> 3, :3] = first[:, :3]
+    return out
 
 
 def pick_convq_cfg(B, M, segs):
-    """the convq configuration with the lowest convq_cost (MT = 2 only when M >= 64);
-    FFC_CONVQ_CFG forces one (A/B measurements)"""
+    """the convq configuration (and K split) with the lowest convq_cost (MT = 2 only when M >= 64);
+    FFC_CONVQ_CFG forces the configuration (A/B measurements)"""
     force = os.environ.get("FFC_CONVQ_CFG")
+    tuned = convq_tuned()[0].get(job_signature(B, M, segs))
+    if os.environ.get("FFC_CONVQ_TUNED_LOG"):
+        import sys
+        print(f"[convq] tuned cfg {'hit' if tuned is not None else 'miss'}: {job_signature(B, M, segs)}",
+              file=sys.stderr)
     if force is not None:
-        return plan_convq_job(B, M, segs, int(force))
-    cands = ([0, 2] if M >= 64 else [0]) + [1, 3]
+        cands = [int(force)]
+    elif tuned is not None:
+        cands = [tuned]
+    else:
+        cands = ([0, 2] if M >= 64 else [0]) + [1, 3]
     plans = [q for q in (plan_convq_job(B, M, segs, c) for c in cands) if q is not None]
-    return min(plans, key=convq_cost) if plans else None
+    for q in plans:
+        q.ksplit = pick_convq_ksplit(q)
+    return min(plans, key=lambda q: convq_cost(q, q.ksplit)) if plans else None
 
 
 def pick_patch_cfg(B, M, segs, min_blocks=512):
@@ -569,8 +648,9 @@ def patch_tile_cost(pl) -> int:
     return max(ph["Kpad"] for ph in pl.phases)
 
 
-def build_patch_tiles(plans, nxcd: int = 8):
-    """int32 [ntiles, 4] {job, m0, pixel block, 0}, XCD-remapped.
+def build_patch_tiles(plans, nxcd: int = 8, ksplit: int = 1):
+    """int32 [ntiles, 4] {job, m0, pixel block, slot * 8 + split}, XCD-remapped (ksplit > 1: each
+    output tile (slot) as ksplit consecutive workgroups, one per K range; ffc_convq_forward_split).
 
     The pixel blocks are cut into nxcd contiguous ranges, one per XCD (blockIdx % 8), so the
     workgroups that share a block's input patch share an L2.  Within an XCD's run the heaviest
@@ -588,12 +668,15 @@ def build_patch_tiles(plans, nxcd: int = 8):
                         ordered.append((j, m0, pb, 0))
         remap = xcd_remap(len(ordered), nxcd)
         return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)
+    slot = 0
     for x in range(nxcd):
         lo, hi = npb * x // nxcd, npb * (x + 1) // nxcd
         for j in order:
             pl = plans[j]
             for pb in range(lo, min(hi, pl.npb)):
                 for m0 in range(0, pl.M, 32 * pl.mt):
-                    ordered.append((j, m0, pb, 0))
+                    for k in range(ksplit):
+                        ordered.append((j, m0, pb, slot * 8 + k if ksplit > 1 else 0))
+                    slot += 1
     remap = xcd_remap(len(ordered), nxcd)
     return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)

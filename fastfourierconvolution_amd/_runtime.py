@@ -287,11 +287,13 @@ class ConvExec:
     kind 'patch' -> ffc_convp_forward (LDS input patch, all phases per workgroup),
     kind 'gemm'  -> ffc_conv_forward (generic phase GEMM with gathered B)."""
 
-    def __init__(self, B, M, segs, weights, device, pw_ok=False):
+    def __init__(self, B, M, segs, weights, device, pw_ok=False, convq_cfg=None):
         pw_only = all(sg.kind == "pw" and not sg.pool and not sg.gate for sg in segs)
         pp = (_plan.pick_patch_cfg(B, M, segs, 128 if CONV_ARITH == "split" else 512)
               if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None)
-        if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and (
+        if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and convq_cfg is not None:
+            pp = _plan.plan_convq_job(B, M, segs, convq_cfg) or pp   # the launch group's common cfg
+        elif USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and (
                 CONVQ_FORCE or pp is None or pp.npb * (-(-M // 32)) <= CONVQ_MAX_CONVP_TILES):
             pp = _plan.pick_convq_cfg(B, M, segs) or pp
         if pw_ok and pw_only and PW_KERNEL == "pw":
@@ -427,10 +429,21 @@ class LaunchPlan:
             self.ntiles = sum(lib().ffc_pw_tiles(e.plan.M, e.plan.B, e.plan.OH * e.plan.OW, self.cfg) for e in execs)
             self.tiles = None
             return
+        self.ksplit, self.part, self.slots, self.nslots = 1, None, None, 0
         if self.key[0] in ("patch", "q"):
             self.cfg = self.key[1]
-            tiles = _plan.build_patch_tiles([e.plan for e in execs])
+            if self.key[0] == "q":   # one K split for the launch's jobs (small batches: fill the CUs)
+                self.ksplit = _plan.pick_convq_ksplit_group([e.plan for e in execs])
+            tiles = _plan.build_patch_tiles([e.plan for e in execs], ksplit=self.ksplit)
             self._rows = [e.plan.npb * 4 for e in execs]
+            if self.ksplit > 1:   # partial fragments, added by the reduce launch of ffc_convq_forward_split
+                slots = _plan.convq_slot_tiles(tiles)
+                self.nslots = slots.shape[0]
+                n = lib().ffc_convq_split_floats(self.cfg, self.nslots, self.ksplit)
+                if n <= 0:
+                    raise RuntimeError("ffc_convq_split_floats: bad configuration")
+                self.part = torch.empty(n, device=device, dtype=torch.float32)
+                self.slots = torch.from_numpy(slots).to(device)
         else:
             self.cfg = _plan.pick_tile_cfg([e.plan.M for e in execs])
             tiles, nslots = _plan.build_tiles([e.plan for e in execs], self.cfg)
@@ -453,8 +466,14 @@ class LaunchPlan:
                     check(L.ffc_pw_forward(ctypes.byref(jb), self.cfg, stream), "ffc_pw_forward")
             elif self.key[0] == "q":
                 arr = (_lib.ConvPJob * len(jobs))(*jobs)
-                check(L.ffc_convq_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
-                      "ffc_convq_forward")
+                if self.ksplit > 1:
+                    check(L.ffc_convq_forward_split(arr, len(jobs), self.tiles.data_ptr(), self.ntiles,
+                                                    self.slots.data_ptr(), self.nslots, self.cfg, self.ksplit,
+                                                    self.part.data_ptr(), stream),
+                          "ffc_convq_forward_split")
+                else:
+                    check(L.ffc_convq_forward(arr, len(jobs), self.tiles.data_ptr(), self.ntiles, self.cfg, stream),
+                          "ffc_convq_forward")
             elif self.key[0] == "patch":
                 arr = (_lib.ConvPJob * len(jobs))(*jobs)
                 cfg = self.cfg | (_lib.CONVP_EXACT_F32 if CONV_ARITH == "f32" else 0)

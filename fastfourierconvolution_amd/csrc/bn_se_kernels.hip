@@ -12,33 +12,60 @@ namespace {
 
 constexpr int RED_THREADS = 256;
 
-// one block per channel: merge rows of a {n, mean, M2} slab into fp64 raw moments
-__device__ void reduce_channel(const float4* __restrict__ slab, int nrows, int C, int c, double* out3) {
-    __shared__ double sh[3][RED_THREADS];
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// one block per channel: merge rows of a {n, mean, M2} slab into fp64 raw moments {n, sum, sumsq}
+// (fixed order: strided per-thread sums, a shuffle tree per wave, the waves in order), returned
+// in thread 0's m[] and stored to out3.  Latency-bound (a few hundred rows): every thread keeps
+// its loads in flight (unrolled by 4) and the tree needs one barrier.
+__device__ void reduce_channel(const float4* __restrict__ slab, int nrows, int C, int c, double* out3, double (&m)[3]) {
+    __shared__ double sh[RED_THREADS / 64][3];
     double n = 0.0, s = 0.0, q = 0.0;
-    for (int r = threadIdx.x; r < nrows; r += RED_THREADS) {
+    int r = threadIdx.x;
+    for (; r + 3 * RED_THREADS < nrows; r += 4 * RED_THREADS) {
+        float4 e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = slab[(size_t)(r + u * RED_THREADS) * C + c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double en = e[u].x, em = e[u].y;
+            n += en;
+            s += en * em;
+            q += (double)e[u].z + en * em * em;
+        }
+    }
+    for (; r < nrows; r += RED_THREADS) {
         const float4 e = slab[(size_t)r * C + c];
         const double en = e.x, em = e.y;
         n += en;
         s += en * em;
         q += (double)e.z + en * em * em;
     }
-    sh[0][threadIdx.x] = n;
-    sh[1][threadIdx.x] = s;
-    sh[2][threadIdx.x] = q;
-    __syncthreads();
-    for (int w = RED_THREADS / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-            sh[0][threadIdx.x] += sh[0][threadIdx.x + w];
-            sh[1][threadIdx.x] += sh[1][threadIdx.x + w];
-            sh[2][threadIdx.x] += sh[2][threadIdx.x + w];
-        }
-        __syncthreads();
+    n = wave_sum_f64(n);
+    s = wave_sum_f64(s);
+    q = wave_sum_f64(q);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sh[w][0] = n;
+        sh[w][1] = s;
+        sh[w][2] = q;
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        out3[0] = sh[0][0];
-        out3[1] = sh[1][0];
-        out3[2] = sh[2][0];
+        m[0] = m[1] = m[2] = 0.0;
+#pragma unroll
+        for (int i = 0; i < RED_THREADS / 64; ++i) {
+            m[0] += sh[i][0];
+            m[1] += sh[i][1];
+            m[2] += sh[i][2];
+        }
+        out3[0] = m[0];
+        out3[1] = m[1];
+        out3[2] = m[2];
     }
 }
 
@@ -55,7 +82,25 @@ struct FinalizeArgs {
     float* shift;
 };
 
-__device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a) {
+// the per-channel BN parameters finalize_channel reads, loaded up front (their latency then
+// overlaps the slab reduction)
+struct FinalizeIn {
+    float g, bb, rm, rv;
+    int64_t nbt;
+};
+
+__device__ __forceinline__ FinalizeIn finalize_load(int c, const FinalizeArgs& a) {
+    FinalizeIn in;
+    in.g = a.gamma ? a.gamma[c] : 1.0f;
+    in.bb = a.beta ? a.beta[c] : 0.0f;
+    const bool need_running = !a.use_batch_stats || a.update_running;
+    in.rm = need_running ? a.running_mean[c] : 0.0f;
+    in.rv = need_running ? a.running_var[c] : 0.0f;
+    in.nbt = a.update_running && a.momentum < 0.0f ? *a.nbt : 0;
+    return in;
+}
+
+__device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a, const FinalizeIn& in) {
     float mean, var;
     if (a.use_batch_stats) {
         const double n = m3[0];
@@ -66,26 +111,29 @@ __device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a)
         var = (float)v;
         if (a.update_running) {
             float f = a.momentum;
-            if (f < 0.0f) f = 1.0f / (float)(*a.nbt + 1);  // momentum=None: cumulative average
+            if (f < 0.0f) f = 1.0f / (float)(in.nbt + 1);  // momentum=None: cumulative average
             const double nfull = n * (double)a.count_mult;
             const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
-            a.running_mean[c] = (1.0f - f) * a.running_mean[c] + f * mean;
-            a.running_var[c] = (1.0f - f) * a.running_var[c] + f * (float)unb;
+            a.running_mean[c] = (1.0f - f) * in.rm + f * mean;
+            a.running_var[c] = (1.0f - f) * in.rv + f * (float)unb;
         }
     } else {
-        mean = a.running_mean[c];
-        var = a.running_var[c];
+        mean = in.rm;
+        var = in.rv;
     }
     const float inv = 1.0f / sqrtf(var + a.eps);
-    const float g = a.gamma ? a.gamma[c] : 1.0f;
-    const float bb = a.beta ? a.beta[c] : 0.0f;
-    const float sc = g * inv;
+    const float sc = in.g * inv;
     a.scale[c] = sc;
-    a.shift[c] = bb - mean * sc;
+    a.shift[c] = in.bb - mean * sc;
+}
+
+__device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a) {
+    finalize_channel(m3, c, a, finalize_load(c, a));
 }
 
 __global__ void bn_reduce_kernel(const float4* __restrict__ slab, int nrows, int C, double* moments) {
-    reduce_channel(slab, nrows, C, blockIdx.x, moments + 3 * blockIdx.x);
+    double m[3];
+    reduce_channel(slab, nrows, C, blockIdx.x, moments + 3 * blockIdx.x, m);
 }
 
 __global__ void bn_finalize_kernel(const double* __restrict__ moments, int C, FinalizeArgs a) {
@@ -102,9 +150,11 @@ __global__ void bn_bump_kernel(int64_t* nbt) {
 __global__ void bn_reduce_finalize_kernel(const float4* __restrict__ slab, int nrows, int C, double* moments,
                                           FinalizeArgs a) {
     const int c = blockIdx.x;
-    reduce_channel(slab, nrows, C, c, moments + 3 * c);
-    __syncthreads();
-    if (threadIdx.x == 0) finalize_channel(moments + 3 * c, c, a);
+    FinalizeIn in = {};
+    if (threadIdx.x == 0) in = finalize_load(c, a);
+    double m[3];
+    reduce_channel(slab, nrows, C, c, moments + 3 * c, m);
+    if (threadIdx.x == 0) finalize_channel(m, c, a, in);
     if (a.bump_here && c == 0 && threadIdx.x == 0) *a.nbt += 1;
 }
 

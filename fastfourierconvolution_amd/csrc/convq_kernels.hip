@@ -41,6 +41,8 @@ struct ConvQArgs {
     ffc_convp_job jobs[2];
     const int4* tiles;
     int ebuf;                  // bytes per LDS buffer (multiple of 256)
+    int ksplit;                // K splits per output tile (1: no split)
+    float* part;               // ksplit > 1: per (slot, split, wave) fragment partial sums
 };
 
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -64,6 +66,139 @@ __device__ __forceinline__ u32x4 lds_read16(const char* base, int off) {
     return *reinterpret_cast<const u32x4*>(base + off);
 }
 
+// Pixel geometry of lane `lane` of compute wave `wave` (= phase) in pixel block pb: per N-tile the
+// sample / phase-grid row / column inside the block and whether the pixel exists.
+template <int NTW>
+struct QGeom {
+    int b0, r0, c0;
+    int pns[NTW], pr_[NTW], pc_[NTW];
+    bool pv[NTW];
+};
+
+template <int NTW>
+__device__ __forceinline__ QGeom<NTW> q_geometry(const ffc_convp_job& J, int wave, int lane, int pb) {
+    QGeom<NTW> g;
+    const ffc_convp_phase& P = J.ph[wave];
+    const int NS = J.NS, TR = J.TR, TC = J.TC, TRC = TR * TC;
+    const int bs = pb / (J.nrb * J.ncb);
+    const int prem = pb - bs * J.nrb * J.ncb;
+    const int rb = prem / J.ncb, cb = prem - rb * J.ncb;
+    g.b0 = bs * NS;
+    g.r0 = rb * TR;
+    g.c0 = cb * TC;
+    const int cl = lane & 31;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        const int q = nt * 32 + cl;
+        const int ns = q / TRC;
+        const int rem = q - ns * TRC;
+        const int r = rem / TC, c = rem - r * TC;
+        g.pns[nt] = ns;
+        g.pr_[nt] = r;
+        g.pc_[nt] = c;
+        g.pv[nt] = ns < NS && g.b0 + ns < J.B && g.r0 + r < P.PH && g.c0 + c < P.PW;
+    }
+    return g;
+}
+
+// one wave's fragments as MT x NTW x 4 coalesced floatx4 rows of 64 lanes
+template <int MT, int NTW>
+__device__ __forceinline__ void store_partial(float* dst, int lane, const floatx16 (&acc)[MT][NTW]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const floatx4 v = {acc[mt][nt][4 * r4], acc[mt][nt][4 * r4 + 1], acc[mt][nt][4 * r4 + 2],
+                                   acc[mt][nt][4 * r4 + 3]};
+                *reinterpret_cast<floatx4*>(dst + ((mt * NTW + nt) * 4 + r4) * 256 + lane * 4) = v;
+            }
+}
+
+// Epilogue of one compute wave (phase `wave`) of output tile (pb, m0): bias / addend, the BN partial
+// slab rows [pb * 4 + wave], activation, scattered stores
+template <int MT, int NTW>
+__device__ __forceinline__ void convq_epilogue(const ffc_convp_job& J, int wave, int lane, int pb, int m0,
+                                               floatx16 (&acc)[MT][NTW]) {
+    const QGeom<NTW> g = q_geometry<NTW>(J, wave, lane, pb);
+    const ffc_convp_phase& P = J.ph[wave];
+    const int h = lane >> 5, cl = lane & 31;
+    const int b0 = g.b0, r0 = g.r0, c0 = g.c0;
+    const int* pns = g.pns;
+    const int* pr_ = g.pr_;
+    const int* pc_ = g.pc_;
+    const bool* pv = g.pv;
+    const size_t plane = (size_t)J.OH * J.OW;
+    int ob[NTW], oo[NTW];
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+        ob[nt] = b0 + pns[nt];
+        oo[nt] = ((r0 + pr_[nt]) * J.Sy + P.py) * J.OW + ((c0 + pc_[nt]) * J.Sx + P.px);
+    }
+    auto epilogue = [&](floatx16 (&tacc)[NTW], const int mbase) {
+        if (J.bias || J.addend) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mbase + (r & 3) + 8 * (r >> 2);
+                if (m >= J.M) continue;
+                const float bv = J.bias ? J.bias[m] : 0.0f;
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) {
+                    float v = tacc[nt][r] + bv;
+                    if (J.addend && pv[nt]) v += J.addend[((size_t)ob[nt] * J.M + m) * plane + oo[nt]];
+                    tacc[nt][r] = v;
+                }
+            }
+        }
+        if (J.stats) {
+            float cntl = 0.0f;
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) cntl += pv[nt] ? 1.0f : 0.0f;
+            const float cnt = ffc::half_wave_sum(cntl);
+            float4* stp = reinterpret_cast<float4*>(J.stats) + ((size_t)pb * 4 + wave) * J.M;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mbase + (r & 3) + 8 * (r >> 2);
+                float s = 0.0f;
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) s += pv[nt] ? tacc[nt][r] : 0.0f;
+                const float mean = cnt > 0.0f ? ffc::half_wave_sum(s) / cnt : 0.0f;
+                float q = 0.0f;
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) {
+                    const float d = pv[nt] ? tacc[nt][r] - mean : 0.0f;
+                    q += d * d;
+                }
+                const float m2 = ffc::half_wave_sum(q);
+                if (cl == 0 && m < J.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
+            }
+        }
+        auto store = [&](auto actf) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mbase + (r & 3) + 8 * (r >> 2);
+                if (m < J.M) {
+#pragma unroll
+                    for (int nt = 0; nt < NTW; ++nt)
+                        if (pv[nt]) J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = actf(tacc[nt][r]);
+                }
+            }
+        };
+        const float ap = J.act_param;
+        switch (J.act) {
+            case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
+            case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
+            case FFC_ACT_TANH: store([](float v) { return tanhf(v); }); break;
+            case FFC_ACT_SIGMOID: store([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
+            case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
+            default: store([](float v) { return v; }); break;
+        }
+    };
+    epilogue(acc[0], m0 + 4 * h);
+    if constexpr (MT > 1) epilogue(acc[1], m0 + 32 + 4 * h);
+}
+
 template <int MT, int NTW>
 __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -82,6 +217,9 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
     const int ji = __builtin_amdgcn_readfirstlane(tile.x);
     const int m0 = __builtin_amdgcn_readfirstlane(tile.y);
     const int pb = __builtin_amdgcn_readfirstlane(tile.z);
+    const int tw = __builtin_amdgcn_readfirstlane(tile.w);
+    const int ks = tw & 7, slot = tw >> 3;   // K split of this workgroup, output tile slot
+    const int nsplit = args.ksplit;
     const ffc_convp_job& J = args.jobs[ji];
     const ffc_convp_phase& P = J.ph[wave];
     const int ebuf = args.ebuf;
@@ -222,15 +360,27 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
         }
     };
 
-    // staged segments first (direct = 0), in job order
-    int nstaged = 0;
-    for (int s = 0; s < nseg; ++s)
-        if (!J.seg[s].direct) nstaged += J.seg[s].Cpad >> 4;
+    // K = the staged segments' 16-channel chunks (in job order), then the direct segments' chunks;
+    // K split ks of nsplit takes the chunk range [lo, hi) of that sequence
+    int nstaged = 0, ndirect = 0;
+    for (int s = 0; s < nseg; ++s) {
+        if (J.seg[s].direct) ndirect += J.seg[s].Cpad >> 4;
+        else nstaged += J.seg[s].Cpad >> 4;
+    }
+    const int ntot = nstaged + ndirect;
+    const int lo = ntot * ks / nsplit, hi = ntot * (ks + 1) / nsplit;
+    const int slo = min(lo, nstaged), nst = min(hi, nstaged) - slo;
+    const int dlo = max(lo, nstaged) - nstaged, dhi = max(hi, nstaged) - nstaged;
 
-    if (nstaged > 0) {
+    if (nst > 0) {
         int ss = 0;
         while (J.seg[ss].direct) ++ss;
-        int cs = ss, sch = 0, cch = 0;   // stager / computer: segment and channel of their chunk
+        int c0k = slo;   // first chunk of this split: segment ss, chunk c0k inside it
+        while (c0k >= (J.seg[ss].Cpad >> 4)) {
+            c0k -= J.seg[ss].Cpad >> 4;
+            do { ++ss; } while (J.seg[ss].direct);
+        }
+        int cs = ss, sch = 16 * c0k, cch = 16 * c0k;   // stager / computer: segment and channel of their chunk
         auto advance_stager = [&]() {
             if (sch >= J.seg[ss].Cpad) {
                 do { ++ss; } while (ss < nseg && J.seg[ss].direct);
@@ -290,16 +440,16 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
             issue(sv1, wb1);                 // chunk 1 (if any)
             store_timed(sv0, wb0, lds);
             bar();
-            for (int ci = 0; ci < nstaged; ci += 2) {
+            for (int ci = 0; ci < nst; ci += 2) {
 #ifndef FFC_QPROBE_NOSTAGE
-                if (ci + 2 < nstaged) issue(sv0, wb0);
-                if (ci + 1 < nstaged) store_timed(sv1, wb1, lds + ebuf);
+                if (ci + 2 < nst) issue(sv0, wb0);
+                if (ci + 1 < nst) store_timed(sv1, wb1, lds + ebuf);
 #endif
                 bar();
-                if (ci + 1 >= nstaged) break;
+                if (ci + 1 >= nst) break;
 #ifndef FFC_QPROBE_NOSTAGE
-                if (ci + 3 < nstaged) issue(sv1, wb1);
-                if (ci + 2 < nstaged) store_timed(sv0, wb0, lds);
+                if (ci + 3 < nst) issue(sv1, wb1);
+                if (ci + 2 < nst) store_timed(sv0, wb0, lds);
 #endif
                 bar();
             }
@@ -311,14 +461,14 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
                 tr[10] = qs;
                 tr[11] = qw;
                 tr[12] = qa - q0;
-                tr[13] = nstaged;
+                tr[13] = nst;
             }
 #endif
             return;   // no barrier follows
         }
         Split3 anext[MT];   // tap 0's A of the coming chunk
         compute_setup(cs);
-        load_A(kseg, anext);
+        load_A(kseg + cch * 4, anext);
 #ifdef FFC_TRACE_Q
         QSTAMP(tq_a);
 #endif
@@ -327,11 +477,11 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
         QSTAMP(tq_b);
         tq_bar += tq_b - tq_a;
 #endif
-        for (int ci = 0; ci < nstaged; ++ci) {
+        for (int ci = 0; ci < nst; ++ci) {
 #ifdef FFC_TRACE_Q
             QSTAMP(tq_a);
 #endif
-            const bool more = ci + 1 < nstaged;
+            const bool more = ci + 1 < nst;
             const char* cur = lds + (ci & 1) * ebuf;
             // the computer's next chunk (segment cn, channel chn) for the A prefetch
             int cn = cs, chn = cch + 16;
@@ -417,9 +567,14 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
     if (stager) return;   // no barrier follows
 
     // ---------------- direct segments (1x1 at the output resolution): B straight from global
+    int dbase = 0;
     for (int s = 0; s < nseg; ++s) {
         const ffc_convp_seg& S = J.seg[s];
         if (!S.direct) continue;
+        const int nch = S.Cpad >> 4;
+        const int c_lo = max(dlo - dbase, 0), c_hi = min(dhi - dbase, nch);
+        dbase += nch;
+        if (c_lo >= c_hi) continue;
         const int IHW = S.IH * S.IW;
         const float* xp[NTW];
 #pragma unroll
@@ -428,7 +583,7 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
             const int b = pv[nt] ? b0 + pns[nt] : 0;
             xp[nt] = S.x + ((long long)b * S.C + 8 * h) * IHW + (pv[nt] ? oy * S.IW + ox : 0);
         }
-        for (int ch0 = 0; ch0 < S.Cpad; ch0 += 16) {
+        for (int ch0 = 16 * c_lo; ch0 < 16 * c_hi; ch0 += 16) {
             Split3 a[MT];
             load_A(P.kseg[s] + ch0, a);
             float bv[NTW][8];
@@ -449,81 +604,18 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
         }
     }
 
-    // ---------------- epilogue: bias/addend, BN partials, activation, store
-    const size_t plane = (size_t)J.OH * J.OW;
-    int ob[NTW], oo[NTW];
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-        ob[nt] = b0 + pns[nt];
-        oo[nt] = ((r0 + pr_[nt]) * J.Sy + P.py) * J.OW + ((c0 + pc_[nt]) * J.Sx + P.px);
-    }
-    auto epilogue = [&](floatx16 (&tacc)[NTW], const int mbase) {
-        if (J.bias || J.addend) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = mbase + (r & 3) + 8 * (r >> 2);
-                if (m >= J.M) continue;
-                const float bv = J.bias ? J.bias[m] : 0.0f;
-#pragma unroll
-                for (int nt = 0; nt < NTW; ++nt) {
-                    float v = tacc[nt][r] + bv;
-                    if (J.addend && pv[nt]) v += J.addend[((size_t)ob[nt] * J.M + m) * plane + oo[nt]];
-                    tacc[nt][r] = v;
-                }
-            }
-        }
-        if (J.stats) {
-            float cntl = 0.0f;
-#pragma unroll
-            for (int nt = 0; nt < NTW; ++nt) cntl += pv[nt] ? 1.0f : 0.0f;
-            const float cnt = ffc::half_wave_sum(cntl);
-            float4* stp = reinterpret_cast<float4*>(J.stats) + ((size_t)pb * 4 + wave) * J.M;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = mbase + (r & 3) + 8 * (r >> 2);
-                float s = 0.0f;
-#pragma unroll
-                for (int nt = 0; nt < NTW; ++nt) s += pv[nt] ? tacc[nt][r] : 0.0f;
-                const float mean = cnt > 0.0f ? ffc::half_wave_sum(s) / cnt : 0.0f;
-                float q = 0.0f;
-#pragma unroll
-                for (int nt = 0; nt < NTW; ++nt) {
-                    const float d = pv[nt] ? tacc[nt][r] - mean : 0.0f;
-                    q += d * d;
-                }
-                const float m2 = ffc::half_wave_sum(q);
-                if (cl == 0 && m < J.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
-            }
-        }
-        auto store = [&](auto actf) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = mbase + (r & 3) + 8 * (r >> 2);
-                if (m < J.M) {
-#pragma unroll
-                    for (int nt = 0; nt < NTW; ++nt)
-                        if (pv[nt]) J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = actf(tacc[nt][r]);
-                }
-            }
-        };
-        const float ap = J.act_param;
-        switch (J.act) {
-            case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
-            case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
-            case FFC_ACT_TANH: store([](float v) { return tanhf(v); }); break;
-            case FFC_ACT_SIGMOID: store([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
-            case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
-            default: store([](float v) { return v; }); break;
-        }
-    };
 #ifdef FFC_QPROBE_NOEPI
     if (acc[0][0][0] != 1234.5f) return;   // keep the accumulators live, skip the stores
 #endif
+    // ---------------- K split: store this split's fragments; convq_reduce_kernel adds them
+    if (nsplit > 1) {
+        store_partial<MT, NTW>(args.part + ((size_t)(slot * nsplit + ks) * 4 + wave) * (MT * NTW * 1024), lane, acc);
+        return;
+    }
 #ifdef FFC_TRACE_Q
     QSTAMP(tq_d);
 #endif
-    epilogue(acc[0], m0 + 4 * h);
-    if constexpr (MT > 1) epilogue(acc[1], m0 + 32 + 4 * h);
+    convq_epilogue<MT, NTW>(J, wave, lane, pb, m0, acc);
 #ifdef FFC_TRACE_Q
     {
         unsigned long long tq_e;
@@ -545,8 +637,51 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #endif
 }
 
+// K split, second pass: workgroup = one output tile (slot), wave w = phase w; adds the ksplit
+// partial fragments in split order (deterministic) and runs the epilogue.  A separate launch
+// rather than a last-arriver in convq_kernel: making the partials visible across XCDs from inside
+// the kernel takes an L2 writeback per wave (buffer_wbl2), which cost more than the split saved.
 template <int MT, int NTW>
-int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s) {
+__global__ __launch_bounds__(256) void convq_reduce_kernel(ConvQArgs args_byval, const int4* __restrict__ slots) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const ConvQArgs& args = args_byval;
+#endif
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int4 tile = slots[blockIdx.x];
+    const int ji = __builtin_amdgcn_readfirstlane(tile.x);
+    const int m0 = __builtin_amdgcn_readfirstlane(tile.y);
+    const int pb = __builtin_amdgcn_readfirstlane(tile.z);
+    const int nsplit = args.ksplit;
+    constexpr int FR = MT * NTW * 1024;
+    const float* base = args.part + ((size_t)blockIdx.x * nsplit * 4 + wave) * FR + lane * 4;
+    floatx16 acc[MT][NTW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                // all nsplit (<= 8) partials in flight at once: clamped loads, then the sum in split order
+                const float* p = base + ((mt * NTW + nt) * 4 + r4) * 256;
+                floatx4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    v[k] = *reinterpret_cast<const floatx4*>(p + (size_t)(k < nsplit ? k : 0) * 4 * FR);
+                floatx4 sum = v[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k)
+                    if (k < nsplit) sum += v[k];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[mt][nt][4 * r4 + e] = sum[e];
+            }
+    convq_epilogue<MT, NTW>(args.jobs[ji], wave, lane, pb, m0, acc);
+}
+
+template <int MT, int NTW>
+int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const int4* slots, int nslots) {
     auto k = convq_kernel<MT, NTW>;
     if (lds > 64 * 1024) {
         static bool raised = false;   // per instantiation
@@ -561,7 +696,13 @@ int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s) {
         }
     }
     hipLaunchKernelGGL(k, dim3(ntiles), dim3(QTHREADS), lds, s, a);
-    return ffc::launch_status("ffc_convq_forward");
+    if (a.ksplit > 1) {
+        const int rc = ffc::launch_status("ffc_convq_forward_split");
+        if (rc != FFC_OK) return rc;
+        auto r = convq_reduce_kernel<MT, NTW>;
+        hipLaunchKernelGGL(r, dim3(nslots), dim3(256), 0, s, a, slots);
+    }
+    return ffc::launch_status("ffc_convq_forward_split");
 }
 
 }  // namespace
@@ -628,11 +769,28 @@ extern "C" int ffc_convq_config(int cfg, int* mt, int* ntw) {
     return FFC_OK;
 }
 
+extern "C" long long ffc_convq_split_floats(int cfg, int nslots, int ksplit) {
+    int MT = 0, NTW = 0;
+    if (ffc_convq_config(cfg, &MT, &NTW) != FFC_OK || nslots < 0 || ksplit < 1 || ksplit > 8) return -1;
+    return ksplit > 1 ? (long long)nslots * ksplit * 4 * MT * NTW * 1024 : 0;
+}
+
 extern "C" int ffc_convq_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                                  void* stream) {
+    return ffc_convq_forward_split(jobs, njobs, tiles, ntiles, nullptr, 0, cfg, 1, nullptr, stream);
+}
+
+extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles,
+                                       const int* slot_tiles, int nslots, int cfg, int ksplit, float* part,
+                                       void* stream) {
     FFC_CHECK_ARG(jobs && tiles && njobs >= 1 && njobs <= 2 && ntiles > 0, "ffc_convq_forward: bad args");
     int MT = 0, NTW = 0;
     FFC_CHECK_ARG(ffc_convq_config(cfg, &MT, &NTW) == FFC_OK, "ffc_convq_forward: unknown cfg");
+    FFC_CHECK_ARG(ksplit >= 1 && ksplit <= 8, "ffc_convq_forward: 1 <= ksplit <= 8");
+    FFC_CHECK_ARG(ksplit == 1 || (part && (reinterpret_cast<uintptr_t>(part) & 15) == 0),
+                  "ffc_convq_forward: ksplit > 1 needs the partial buffer (16-byte aligned)");
+    FFC_CHECK_ARG(ksplit == 1 || (slot_tiles && nslots > 0 && (long long)nslots * ksplit == ntiles),
+                  "ffc_convq_forward: ksplit > 1 needs the slot table (ntiles = nslots * ksplit)");
     int npix_max = 0;
     for (int j = 0; j < njobs; ++j) {
         const ffc_convp_job& J = jobs[j];
@@ -677,12 +835,15 @@ extern "C" int ffc_convq_forward(const ffc_convp_job* jobs, int njobs, const int
     a.jobs[0] = jobs[0];
     a.jobs[1] = jobs[njobs > 1 ? 1 : 0];
     a.tiles = reinterpret_cast<const int4*>(tiles);
+    a.ksplit = ksplit;
+    a.part = part;
+    const int4* sl = reinterpret_cast<const int4*>(slot_tiles);
     hipStream_t s = (hipStream_t)stream;
     switch (cfg) {
-        case 0: return launch_q<1, 4>(a, ntiles, lds, s);
-        case 1: return launch_q<1, 2>(a, ntiles, lds, s);
-        case 2: return launch_q<2, 2>(a, ntiles, lds, s);
-        case 3: return launch_q<1, 1>(a, ntiles, lds, s);
+        case 0: return launch_q<1, 4>(a, ntiles, lds, s, sl, nslots);
+        case 1: return launch_q<1, 2>(a, ntiles, lds, s, sl, nslots);
+        case 2: return launch_q<2, 2>(a, ntiles, lds, s, sl, nslots);
+        case 3: return launch_q<1, 1>(a, ntiles, lds, s, sl, nslots);
     }
     ffc::set_error("ffc_convq_forward: unknown cfg");
     return FFC_E_INVALID;

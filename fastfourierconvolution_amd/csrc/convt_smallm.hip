@@ -77,6 +77,10 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     const int qy = 2 * (tid >> 4), qx = 2 * (tid & 15);   // top-left of this thread's 2x2 input pixels
     const int M = a.M, C0 = a.C[0];
     const int Ct = C0 + (a.nseg > 1 ? a.C[1] : 0);
+    // one base plus a per-lane offset: a lane-varying select between a.x[0] and a.x[1] is folded
+    // into a per-lane load of the selected kernel argument
+    const float* xs0 = a.x[0];
+    const long long xd1 = a.nseg > 1 ? (long long)(a.x[1] - a.x[0]) : 0;   // segment 1 base - segment 0 base
     float* pbuf = lds;   // [2 stages][NQ][CPQ][PB]
     // packed weights [Ct][16 taps][4 m] (ffc_convt_smallm_pack), read through the scalar cache:
     // a channel's 64 values are wave-uniform and sit in SGPRs, so the FMAs need no LDS traffic
@@ -93,15 +97,20 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             const int ci = CT_CPQ * (CT_NQ * k + q) + cl;
             const int g = nn % (CT_PS / 4), pr = nn / (CT_PS / 4);
             const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
-            r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (n >= CT_CPQ * CT_G || ci >= Ct || (unsigned)iy >= (unsigned)a.IH) continue;
-            const int s = ci < C0 ? 0 : 1;
-            const int c = s == 0 ? ci : ci - C0;
-            const float* x = a.x[s] + ((size_t)b * a.C[s] + c) * a.IH * a.IW;
+            const bool rok = n < CT_CPQ * CT_G && ci < Ct && (unsigned)iy < (unsigned)a.IH;
+            const size_t ihw = (size_t)a.IH * a.IW;
+            const float* x = xs0 + (ci < C0 ? (long long)((size_t)b * C0 + ci) * ihw
+                                            : xd1 + (long long)((size_t)b * a.C[1] + (ci - C0)) * ihw);
             const float* row = x + (size_t)iy * a.IW;
             if (VEC) {
-                if ((unsigned)ix < (unsigned)a.IW) r[j] = *reinterpret_cast<const float4*>(row + ix);
+                // unconditional load at a clamped address, then a select: a load under a branch
+                // is waited for before the next one issues
+                const bool ok = rok && (unsigned)ix < (unsigned)a.IW;
+                const float4 v = *reinterpret_cast<const float4*>(ok ? row + ix : xs0);
+                r[j] = ok ? v : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             } else {
+                r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (!rok) continue;
                 if ((unsigned)ix < (unsigned)a.IW) r[j].x = row[ix];
                 if ((unsigned)(ix + 1) < (unsigned)a.IW) r[j].y = row[ix + 1];
                 if ((unsigned)(ix + 2) < (unsigned)a.IW) r[j].z = row[ix + 2];

@@ -33,15 +33,20 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
     const int ntn = (a.N + DN_BN - 1) / DN_BN;
     const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
     const int b0 = tm * DN_BM;
-    const int KS = a.K + 1;
+    const int KS = 2 * KH + 1;   // rows zero-padded to 2 KH: the MFMA loop reads without bounds checks
     // coalesced rows of A, 8 loads in flight per thread before their LDS stores
+    const auto rA = ffc::buf_rsrc(a.A, (unsigned long long)a.B * a.K * 4);
+    const auto rW = ffc::buf_rsrc(a.Wt, (unsigned long long)a.K * a.N * 4);
     for (int i0 = 0; i0 < DN_BM * a.K; i0 += 8 * DN_THREADS) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int i = i0 + u * DN_THREADS + tid;
             const int r = i / a.K;
-            v[u] = (i < DN_BM * a.K && b0 + r < a.B) ? a.A[(size_t)b0 * a.K + i] : 0.0f;
+            // unconditional load from a clamped address, then select: a branch around each load
+            // makes hipcc wait for every load on its own
+            const bool ok = i < DN_BM * a.K && b0 + r < a.B;
+            v[u] = ffc::buf_ld(rA, ok ? (unsigned)(((size_t)b0 * a.K + i) * 4) : ffc::OOB);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -49,6 +54,10 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
             const int r = i / a.K, k = i - r * a.K;
             if (i < DN_BM * a.K) As[r * KS + k] = v[u];
         }
+    }
+    for (int i = tid; i < DN_BM * (KS - a.K); i += DN_THREADS) {   // zero the row tails
+        const int r = i / (KS - a.K), k = a.K + (i - r * (KS - a.K));
+        As[r * KS + k] = 0.0f;
     }
     __syncthreads();
     const int wr = wave >> 1, wc = wave & 1;
@@ -64,16 +73,12 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
 #pragma unroll
     for (int u = 0; u < KH; ++u) {
         const int k = 2 * u + hh;
-        wa[u] = (k < a.K && nv) ? a.Wt[(size_t)k * a.N + n] : 0.0f;
+        const bool ok = k < a.K && nv;
+        wa[u] = ffc::buf_ld(rW, ok ? (unsigned)(((size_t)k * a.N + n) * 4) : ffc::OOB);
     }
 #pragma unroll
-    for (int u = 0; u < KH; ++u) {
-        if (2 * u < a.K) {
-            const int k = 2 * u + hh;
-            const float av = k < a.K ? ar[k] : 0.0f;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, wa[u], acc, 0, 0, 0);
-        }
-    }
+    for (int u = 0; u < KH; ++u)   // k >= K: zero A (padded rows) and zero W
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * u + hh], wa[u], acc, 0, 0, 0);
     if (!nv) return;
     const float bv = a.bias ? a.bias[n] : 0.0f;
     float* dst;
@@ -103,7 +108,7 @@ extern "C" int ffc_dense_forward(const float* A, const float* Wt, const float* b
     FFC_CHECK_ARG(K <= DN_KMAX, "ffc_dense_forward: K > 256");
     DenseArgs a{A, Wt, bias, out0, out1, B, K, N, N0, act, act_param};
     const int grid = ((B + DN_BM - 1) / DN_BM) * ((N + DN_BN - 1) / DN_BN);
-    const size_t lds = sizeof(float) * DN_BM * (K + 1);
+    const size_t lds = sizeof(float) * DN_BM * (2 * (K <= 128 ? 64 : 128) + 1);
     if (K <= 128)
         hipLaunchKernelGGL(dense_kernel<64>, dim3(grid), dim3(DN_THREADS), lds, (hipStream_t)stream, a);
     else

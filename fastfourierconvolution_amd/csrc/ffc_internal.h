@@ -65,6 +65,21 @@ static __device__ __forceinline__ floatx16 mfma_split3(const Split3& a, const Sp
 
 namespace ffc {
 
+// Bounds-checked loads through a buffer descriptor: an out-of-range byte offset returns 0, so a
+// masked element is a load at offset OOB instead of `ok ? p[i] : 0`, which hipcc compiles into a
+// branch around the load and a wait per element.  The base (and size) must be wave-uniform.
+constexpr unsigned OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned long long nbytes) {
+    const int n = nbytes >= 0x7FFFFFFFull ? 0x7FFFFFFF : (int)nbytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ floatx4 buf_ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
 void set_error(const std::string& msg);
 int launch_status(const char* what);  // FFC_OK or FFC_E_LAUNCH after checking hipGetLastError
 

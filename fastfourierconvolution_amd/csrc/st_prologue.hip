@@ -30,7 +30,10 @@ struct StArgs {
     int gate_off, hv_off, st_off, red_off, scr_off, wt_off, w1_off, w2_off;
 };
 
-constexpr int ST_THREADS = 256;
+// 8 waves: at the batch sizes of a strong-scaling shard (32..256 samples = workgroups, at most one
+// per CU) the kernel is latency-bound, and more waves shorten every phase (SE loops, conv1 split-K)
+constexpr int ST_THREADS = 512;
+constexpr int ST_WAVES = ST_THREADS / 64;
 
 #ifdef FFC_TRACE
 // Diagnostic build only: per workgroup {realtime start, end, s_memtime at phase boundaries 0..5}.
@@ -58,8 +61,8 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     float* gate = sm + a.gate_off;       // [Cin]
     float* hv = sm + a.hv_off;           // [hid]
     float* st = sm + a.st_off;           // [ntile][c][3]
-    float* red = sm + a.red_off;         // [4 waves][16][64] split-K partials
-    float* scr = sm + a.scr_off;         // [4 waves][32 x 33] tile-stats scratch
+    float* red = sm + a.red_off;         // [ST_WAVES][16][64] split-K partials
+    float* scr = sm + a.scr_off;         // [ST_WAVES][32 x 33] tile-stats scratch
     float* wt = sm + a.wt_off;           // [Cin][Mpad] conv1 weight (when staged)
     const int hid = a.hid;
 
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     const int h2 = lane >> 5, col = lane & 31;
     const int MT = Mpad / 32, NT = (hw + 31) / 32;
     const int tiles = MT * NT;
-    const int nsplit = tiles >= 4 ? 1 : 4 / tiles;
+    const int nsplit = tiles >= ST_WAVES ? 1 : ST_WAVES / tiles;
     const int KS = Cin / 2;
     const float* wa = a.wt_off >= 0 ? wt : a.wcT;
     auto mfma_range = [&](int mt, int nt, int s0, int s1, bool odd_tail) {
@@ -248,9 +251,9 @@ StLayout st_layout(int Cin, int H, int W, int pool, int hid, int c) {
     L.st_off = (int)o;
     o += (nt * c * 3 + 3) / 4 * 4;
     L.red_off = (int)o;
-    o += 4 * 16 * 64;
+    o += ST_WAVES * 16 * 64;
     L.scr_off = (int)o;
-    o += 4 * ffc::TILE_SCRATCH;
+    o += ST_WAVES * ffc::TILE_SCRATCH;
     const size_t base = o;
     const bool w12_ok = hid > 0 && ((size_t)hid * Cin) % 4 == 0;
     for (int opt = 0; opt < 3; ++opt) {   // 0: conv1 + SE weights staged, 1: conv1 only, 2: neither

@@ -184,7 +184,7 @@ class _FFCExec:
         """plan / pack / launch the GEMM(s) of the given branches (one launch per kernel kind),
         then BN statistics and BN+activation passes.  -> (out_l, out_g)"""
         outs = {"l": 0, "g": 0}
-        execs, jobs, post = [], [], []
+        execs, jobs, post, built = [], [], [], []
         jb_name = {}
         dense = []   # (name, (W (M', C, 1, 1), layout, 1, 1, bias), input, out, act, M')
         for name, segs, w, inp, add, act, bn, M in branches:
@@ -231,8 +231,21 @@ class _FFCExec:
             jb_name[id(out)] = name
             execs.append(ex)
             jobs.append((ex, inp, out, act, bn, addend))
+            built.append((key, B, M, segs, w))
         if dense:
             self._launch_dense(dense, B, stream)
+        # the layer's convq jobs share one launch, so one configuration: when they picked different
+        # ones (untuned shapes), rebuild them on the costliest job's (cached: happens once)
+        qi = [i for i, jb in enumerate(jobs) if jb[0].launch_key[0] == "q"]
+        if len({jobs[i][0].launch_key for i in qi}) > 1:
+            cfg = max((jobs[i][0].plan for i in qi), key=_plan.convq_cost).cfg
+            cache = self._ffc_cache()
+            for i in qi:
+                ckey, cB, cM, csegs, cw = built[i]
+                ex2 = rt.ConvExec(cB, cM, csegs, cw, dev, convq_cfg=cfg)
+                if ex2.launch_key[0] == "q":
+                    cache[ckey] = ex2
+                    jobs[i] = (ex2,) + jobs[i][1:]
         groups = {}
         for jb in jobs:
             groups.setdefault(jb[0].launch_key, []).append(jb)

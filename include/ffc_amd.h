@@ -197,6 +197,17 @@ int ffc_convq_config(int cfg, int* mt, int* ntw);
 int ffc_convq_pack_a3(const ffc_convp_job* job, const float* A, uint16_t* A3, void* stream);
 int ffc_convq_forward(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles, int cfg,
                       void* stream);
+/* K-split variant (small batches: too few output tiles to fill 256 CUs).  Each output tile (slot)
+ * runs as ksplit workgroups over contiguous ranges of its 16-channel chunks (staged segments, then
+ * direct ones) that store fp32 partial fragments to part (ffc_convq_split_floats(cfg, nslots,
+ * ksplit) floats, 16-byte aligned); a second launch adds each slot's partials in split order
+ * (deterministic) and runs the epilogue.  tiles: ntiles = nslots * ksplit int4 {job, m0, pixel
+ * block, slot * 8 + split}; slot_tiles: nslots int4 {job, m0, pixel block, 0} in slot order.
+ * ksplit = 1 is ffc_convq_forward (slot_tiles / part unused). */
+long long ffc_convq_split_floats(int cfg, int nslots, int ksplit);
+int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, const int* tiles, int ntiles,
+                            const int* slot_tiles, int nslots, int cfg, int ksplit, float* part,
+                            void* stream);
 
 /* Weight packing for one job: A[phase][Mpad][Kpad] (zero padded), bias_out[M] = sum of
  * segment biases.  w_layout[s]: 0 = Conv2d (O, I, kh, kw), 1 = ConvTranspose2d (I, O, kh, kw).

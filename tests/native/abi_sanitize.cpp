@@ -100,6 +100,13 @@ static void validation_paths() {
     EXPECT_INVALID(ffc_convp_forward(&pj, 0, tiles, 1, 0, nullptr), "ffc_convp_forward");
     EXPECT_INVALID(ffc_convp_forward(&pj, 1, tiles, 1, 0, nullptr), "incomplete job");
     EXPECT_INVALID(ffc_split_bf16(cp, 16, reinterpret_cast<uint16_t*>(p), 12, nullptr), "ffc_split_bf16");
+    EXPECT_INVALID(ffc_convq_forward(&pj, 0, tiles, 1, 0, nullptr), "ffc_convq_forward");
+    EXPECT_INVALID(ffc_convq_forward(&pj, 1, tiles, 1, 7, nullptr), "unknown cfg");
+    EXPECT_INVALID(ffc_convq_forward(&pj, 1, tiles, 1, 0, nullptr), "needs the A3 planes");
+    EXPECT_INVALID(ffc_convq_forward_split(&pj, 1, tiles, 1, tiles, 1, 0, 9, p, nullptr), "ksplit <= 8");
+    EXPECT_INVALID(ffc_convq_forward_split(&pj, 1, tiles, 2, tiles, 1, 0, 2, nullptr, nullptr), "partial buffer");
+    EXPECT_INVALID(ffc_convq_forward_split(&pj, 1, tiles, 3, tiles, 1, 0, 2, p, nullptr), "slot table");
+    EXPECT_INVALID(ffc_convq_pack_a3(nullptr, cp, reinterpret_cast<uint16_t*>(p), nullptr), "ffc_convq_pack_a3");
     EXPECT_INVALID(ffc_dense_forward(cp, cp, nullptr, 1, 300, 8, 8, p, nullptr, 0, 0.f, nullptr), "K > 256");
     EXPECT_INVALID(ffc_dense_forward(cp, cp, nullptr, 1, 16, 8, 4, p, nullptr, 0, 0.f, nullptr), "output split");
     EXPECT_INVALID(ffc_convt_smallm_pack(cp, 4, nullptr, 0, 5, p, nullptr), "");
@@ -165,6 +172,15 @@ static void shape_queries() {
             (void)ffc_convt_smallm_pack_floats(a, b);
             (void)ffc_conv_stat_rows_per_tile(a & 3);
         }
+    for (int cfg = -1; cfg < 6; ++cfg)
+        for (int ks = -1; ks < 10; ++ks) (void)ffc_convq_split_floats(cfg, 1 << 20, ks);
+    int mt = 0, ntw = 0;
+    EXPECT_EQ(ffc_convq_config(2, &mt, &ntw), FFC_OK);
+    EXPECT_EQ(mt * 10 + ntw, 22);
+    EXPECT_EQ(ffc_convq_config(4, &mt, &ntw), FFC_E_INVALID);
+    EXPECT_EQ(ffc_convq_split_floats(3, 10, 4), 10LL * 4 * 4 * 1024);
+    EXPECT_EQ(ffc_convq_split_floats(0, 10, 1), 0LL);
+    EXPECT_EQ(ffc_convq_split_floats(0, 10, 9), -1LL);
     EXPECT_EQ(ffc_fu_lds_bytes(16, 64, 64), (size_t)0);
     EXPECT_EQ(ffc_fu2d_supported(65, 64, 64, 1), 0);
     EXPECT_EQ(ffc_fu2d_supported(32, 128, 128, 1), 1);

@@ -127,3 +127,46 @@ def test_convq_rejects_unsupported():
                         (64, 64, 64, 64), (64, 256, 16, 128)]:
         segs = [_plan.Seg("convT", C, IH, IH, 4, 2, 1), _plan.Seg("convT", C, IH, IH, 4, 2, 1)]
         assert _plan.pick_convq_cfg(B, M, segs) is not None, (B, C, IH, M)
+
+
+@pytest.mark.parametrize("ksplit", [1, 2, 4, 8])
+def test_convq_split_tiles(ksplit):
+    """K-split tile table: every (job, m0, pixel block) output tile appears once per split, with one
+    slot shared by its splits (tile.w = slot * 8 + split); slots are dense 0..nslots-1"""
+    segs = [_plan.Seg("convT", 64, 8, 8, 4, 2, 1), _plan.Seg("pw", 16, 16, 16)]
+    q = _plan.plan_convq_job(6, 96, segs, 3)
+    t = _plan.build_patch_tiles([q], ksplit=ksplit)
+    ntiles = q.npb * (-(-q.M // (32 * q.mt)))
+    assert t.shape == (ntiles * ksplit, 4)
+    if ksplit == 1:
+        assert (t[:, 3] == 0).all()
+        return
+    slot, ks = t[:, 3] >> 3, t[:, 3] & 7
+    assert sorted(set(slot.tolist())) == list(range(ntiles))
+    for s in range(ntiles):
+        rows = t[slot == s]
+        assert sorted(ks[slot == s].tolist()) == list(range(ksplit))
+        assert (rows[:, :3] == rows[0, :3]).all()
+    assert len({tuple(r) for r in t[:, :3].tolist()}) == ntiles
+    st = _plan.convq_slot_tiles(t)
+    assert st.shape == (ntiles, 4) and (st[:, 3] == 0).all()
+    for s in range(ntiles):
+        assert (t[slot == s][0, :3] == st[s, :3]).all()
+
+
+def test_convq_ksplit_choice():
+    """small batches split K (more workgroups than 256 CUs' worth of output tiles), large ones do
+    not; at least 4 chunks per split; FFC_CONVQ_KSPLIT forces"""
+    import os
+    segs = [_plan.Seg("convT", 256, 4, 4, 4, 2, 1), _plan.Seg("convT", 256, 4, 4, 4, 2, 1),
+            _plan.Seg("pw", 64, 8, 8)]
+    big_segs = [_plan.Seg("convT", 64, 16, 16, 4, 2, 1), _plan.Seg("convT", 64, 16, 16, 4, 2, 1),
+                _plan.Seg("pw", 16, 32, 32)]
+    small, big = _plan.pick_convq_cfg(32, 128, segs), _plan.pick_convq_cfg(256, 32, big_segs)
+    assert small.ksplit > 1 and _plan.convq_chunks(small) >= 4 * small.ksplit
+    assert big.ksplit == 1
+    os.environ["FFC_CONVQ_KSPLIT"] = "3"
+    try:
+        assert _plan.pick_convq_cfg(32, 128, segs).ksplit == 3
+    finally:
+        os.environ.pop("FFC_CONVQ_KSPLIT")

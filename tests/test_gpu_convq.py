@@ -14,7 +14,7 @@ from oracle.ffc_oracle import normwise_err
 pytestmark = pytest.mark.gpu
 
 
-def _run(B, C0, C1, Cv, IH, M, cfg, bias=False, addend=False, stats=False, act=0, seed=0):
+def _run(B, C0, C1, Cv, IH, M, cfg, bias=False, addend=False, stats=False, act=0, seed=0, ksplit=None):
     from fastfourierconvolution_amd import _lib, _plan, _runtime as rt
     g = torch.Generator().manual_seed(seed)
     segs, ws, xs = [], [], []
@@ -30,18 +30,24 @@ def _run(B, C0, C1, Cv, IH, M, cfg, bias=False, addend=False, stats=False, act=0
     bvec = torch.randn(M, generator=g).cuda() if bias else None
     weights = [(w, 1 if s.kind == "convT" else 0, w.shape[2], w.shape[3], bvec if i == 0 else None)
                for i, (s, w) in enumerate(zip(segs, ws))]
-    old = os.environ.get("FFC_CONVQ_CFG")
-    os.environ["FFC_CONVQ_CFG"] = str(cfg)
+    env = {"FFC_CONVQ_CFG": str(cfg)}
+    if ksplit is not None:
+        env["FFC_CONVQ_KSPLIT"] = str(ksplit)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         ex = rt.ConvExec(B, M, segs, weights, xs[0].device)
+        lp = rt.LaunchPlan([ex], xs[0].device) if ex.launch_key[0] == "q" else None
     finally:
-        if old is None:
-            os.environ.pop("FFC_CONVQ_CFG")
-        else:
-            os.environ["FFC_CONVQ_CFG"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     if ex.launch_key[0] != "q":
         pytest.skip("no convq plan for this shape / configuration")
-    lp = rt.LaunchPlan([ex], xs[0].device)
+    if ksplit is not None:
+        assert lp.ksplit == min(ksplit, _plan.convq_chunks(ex.plan))
     ref = 0
     for s, w, x in zip(segs, ws, xs):
         ref = ref + (F.conv_transpose2d(x, w, stride=2, padding=1) if s.kind == "convT" else F.conv2d(x, w))
@@ -52,8 +58,14 @@ def _run(B, C0, C1, Cv, IH, M, cfg, bias=False, addend=False, stats=False, act=0
         ref = ref + add
     out = torch.full(ref.shape, float("nan"), device="cuda")
     slab = torch.zeros((lp.stat_rows(0), M, 4), device="cuda") if stats else None
-    lp.launch([ex.job([(x, None) for x in xs], out, act, 0.1, add, slab)], torch.cuda.current_stream().cuda_stream)
+    job = ex.job([(x, None) for x in xs], out, act, 0.1, add, slab)
+    lp.launch([job], torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
+    if lp.ksplit > 1:   # a second launch reproduces the first bit for bit
+        first = out.clone()
+        lp.launch([job], torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(out, first)
     pre = ref
     if act == 2:
         ref = F.leaky_relu(ref, 0.1)
@@ -80,6 +92,21 @@ def _run(B, C0, C1, Cv, IH, M, cfg, bias=False, addend=False, stats=False, act=0
                                              (7, 128, 128, 0, 8, 64), (2, 8, 8, 8, 32, 36), (3, 32, 32, 32, 64, 64)])
 def test_convq_vs_torch(cfg, B, C0, C1, Cv, IH, M):
     _run(B, C0, C1, Cv, IH, M, cfg, seed=cfg + 10 * B)
+
+
+@pytest.mark.parametrize("ksplit", [2, 3, 8])
+@pytest.mark.parametrize("cfg", [0, 2, 3])
+@pytest.mark.parametrize("B,C0,C1,Cv,IH,M", [(3, 20, 12, 8, 4, 40), (5, 7, 9, 16, 12, 70), (7, 128, 128, 0, 8, 64),
+                                             (2, 64, 64, 16, 16, 32), (1, 16, 0, 48, 8, 32)])
+def test_convq_ksplit(ksplit, cfg, B, C0, C1, Cv, IH, M):
+    """K split: contiguous chunk ranges (staged, then direct) per workgroup, partial fragments summed
+    in split order by the last arrival, counters re-zeroed (a second launch is bit-identical)"""
+    _run(B, C0, C1, Cv, IH, M, cfg, seed=cfg + 3 * B + ksplit, ksplit=ksplit)
+
+
+@pytest.mark.parametrize("cfg", [0, 2])
+def test_convq_ksplit_epilogue(cfg):
+    _run(3, 24, 8, 8, 8, 48, cfg, bias=True, addend=True, stats=True, act=2, seed=7, ksplit=4)
 
 
 @pytest.mark.parametrize("cfg", [0, 2])

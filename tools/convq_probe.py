@@ -9,12 +9,13 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fastfourierconvolution_amd import _plan, _runtime as rt  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+B = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 256
 model = sys.argv[2] if len(sys.argv) > 2 else "gen64"
 dev = torch.device("cuda", 0)
 # (C_l = C_g in, IH, M_l = M_g out, c of the ST = conv2 input channels)
-LAYERS = {"gen64": [(256, 4, 128, 64), (128, 8, 64, 32), (64, 16, 32, 16)],
-          "fgan128": [(128, 8, 64, 32), (64, 16, 32, 16), (32, 32, 64, 32), (32, 64, 64, 32)]}[model]
+LAYERS_ALL = {"gen64": [(256, 4, 128, 64), (128, 8, 64, 32), (64, 16, 32, 16)],
+              "fgan128": [(128, 8, 64, 32), (64, 16, 32, 16), (32, 32, 64, 32), (32, 64, 64, 32)]}
+LAYERS = LAYERS_ALL.get(model, LAYERS_ALL["gen64"])
 
 
 def job_pair(C, IH, M, c):
@@ -57,8 +58,30 @@ def time_layer(jobs, reps=20):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     fl = sum(f for _, _, f in launches)
-    keys = "+".join(f"{lp.key}:{lp.ntiles}" for lp, _, _ in launches)
+    keys = "+".join(f"{lp.key}:{lp.ntiles}:k{lp.ksplit}" for lp, _, _ in launches)
     return us, fl / us / 1e6, keys
+
+
+def sweep_ksplit():
+    """every (cfg, ksplit) per layer: FFC_CONVQ_SWEEP=1 convq_probe.py <B>"""
+    rt.USE_CONVQ = True
+    for C, IH, M, c in LAYERS:
+        jobs = job_pair(C, IH, M, c)
+        row = [f"B{B} C{C}@{IH}x{IH}->M{M}"]
+        for cfg in (0, 1, 2, 3):
+            os.environ["FFC_CONVQ_CFG"] = str(cfg)
+            for k in (1, 2, 4, 8):
+                os.environ["FFC_CONVQ_KSPLIT"] = str(k)
+                try:
+                    us, tf, keys = time_layer(jobs)
+                    row.append(f"c{cfg}k{k} {us:6.1f}")
+                except Exception as ex:  # noqa: BLE001
+                    row.append(f"c{cfg}k{k} n/a")
+        os.environ.pop("FFC_CONVQ_CFG", None)
+        os.environ.pop("FFC_CONVQ_KSPLIT", None)
+        us, tf, keys = time_layer(jobs)
+        row.append(f"auto {us:6.1f} [{keys}]")
+        print(" | ".join(row), flush=True)
 
 
 def main():
@@ -81,4 +104,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sweep_ksplit() if os.environ.get("FFC_CONVQ_SWEEP") else main()

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Measure every (cfg, ksplit) of ffc_convq_forward on the timed layer shapes and write the table
+the planner reads (fastfourierconvolution_amd/convq_tuned.json; _plan.convq_tuned).
+
+    python tools/tune_convq.py gen64:256,128,64,32 fgan128:512,256,128,64 [--out PATH]
+
+Per FFCTranspose layer the launch group is its out_l + out_g job pair (tools/convq_probe.py
+job_pair: ConvT k4 s2 local/global segments, SpectralTransform.conv2 folded in as a 1x1
+segment); the pair is timed with HIP events over repeated launches for cfg 0..3 x ksplit 1, 2,
+4, 8.  The fastest configuration wins; within 3 % the smaller ksplit (less traffic) is kept.
+Only shapes whose default plan is convq (small grids) are written."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("specs", nargs="+", help="model:B,B,...")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "fastfourierconvolution_amd", "convq_tuned.json"))
+    args = ap.parse_args()
+    os.environ["FFC_CONVQ_TUNED"] = ""          # measure, do not read the old table
+    import convq_probe as P
+    from fastfourierconvolution_amd import _plan, _runtime as rt
+    entries = []
+    for spec in args.specs:
+        model, bs = spec.split(":")
+        for B in [int(b) for b in bs.split(",")]:
+            P.B = B
+            for C, IH, M, c in P.LAYERS_ALL[model]:
+                jobs = P.job_pair(C, IH, M, c)
+                os.environ.pop("FFC_CONVQ_CFG", None)
+                os.environ.pop("FFC_CONVQ_KSPLIT", None)
+                execs = [rt.ConvExec(B, w[0][0].shape[1] if w[0][1] == 1 else w[0][0].shape[0], segs, w, P.dev)
+                         for segs, w, _ in jobs]
+                if any(e.launch_key[0] != "q" for e in execs):
+                    print(f"{model} B{B} C{C}@{IH}: not a convq shape ({[e.launch_key for e in execs]})", flush=True)
+                    continue
+                res = []
+                for cfg in (0, 1, 2, 3):
+                    for k in (1, 2, 4, 8):
+                        os.environ["FFC_CONVQ_CFG"] = str(cfg)
+                        os.environ["FFC_CONVQ_KSPLIT"] = str(k)
+                        try:
+                            us, _, keys = P.time_layer(jobs, reps=30)
+                        except Exception:  # noqa: BLE001 - configuration does not fit this shape
+                            continue
+                        if keys.count("+") == 0 and f":k{k}" in keys:
+                            res.append((us, k, cfg))
+                os.environ.pop("FFC_CONVQ_CFG", None)
+                os.environ.pop("FFC_CONVQ_KSPLIT", None)
+                best = min(res)
+                pick = min((r for r in res if r[0] <= best[0] * 1.03), key=lambda r: (r[1], r[0]))
+                sigs = []
+                for segs, w, _ in jobs:
+                    Mj = w[0][0].shape[1] if w[0][1] == 1 else w[0][0].shape[0]
+                    sigs.append(list(_plan.job_signature(B, Mj, segs)))
+                entries.append({"model": model, "layer": f"C{C}@{IH}x{IH}->M{M}", "jobs": sigs, "cfg": pick[2],
+                                "ksplit": pick[1], "us": round(pick[0], 2),
+                                "k1_best_us": round(min(r[0] for r in res if r[1] == 1), 2)})
+                print(f"{model} B{B} C{C}@{IH}: cfg {pick[2]} ksplit {pick[1]} {pick[0]:.1f} us "
+                      f"(best k=1 {entries[-1]['k1_best_us']:.1f} us)", flush=True)
+    with open(args.out, "w") as f:
+        json.dump({"device": "MI355X (gfx950)", "tool": "tools/tune_convq.py", "entries": entries}, f, indent=1)
+    print(f"wrote {len(entries)} entries to {args.out}")
+
+
+if __name__ == "__main__":
+    main()
