@@ -59,6 +59,10 @@ constexpr int CT_PB = CT_PR * CT_PS;         // floats per channel patch
 constexpr int CT_NQ = 4;                     // channel quarters
 constexpr int CT_THREADS = CT_QT * CT_NQ;
 constexpr int CT_CMAX = 256;                 // channels (both segments) whose weights fit in LDS
+// float offset of the staged weights: behind the patch double buffer (and the partial-sum combine
+// area, which reuses the patch buffers: CT_QT * 16 * 4 floats <= the patch buffers)
+constexpr int CT_WOFF = 2 * CT_NQ * CT_CPQ * CT_PB;
+static_assert(CT_QT * 16 * 4 <= CT_WOFF, "combine area must fit in the patch buffers");
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -82,11 +86,13 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     const float* xs0 = a.x[0];
     const long long xd1 = a.nseg > 1 ? (long long)(a.x[1] - a.x[0]) : 0;   // segment 1 base - segment 0 base
     float* pbuf = lds;   // [2 stages][NQ][CPQ][PB]
-    // packed weights [Ct][16 taps][4 m] (ffc_convt_smallm_pack), read through the scalar cache:
-    // a channel's 64 values are wave-uniform and sit in SGPRs, so the FMAs need no LDS traffic
+    // packed weights [Ct][16 taps][4 m] (ffc_convt_smallm_pack), staged once into LDS behind the
+    // patch buffers and read as wave-uniform (broadcast) ds_read_b128: scalar loads per channel
+    // would put an SMEM round trip (and an lgkmcnt(0) that also drains the LDS reads) in every
+    // channel step
     typedef float fx4 __attribute__((ext_vector_type(4)));
-    typedef const __attribute__((address_space(4))) fx4* cf4;
-    const cf4 wpk = (cf4)a.wpack;
+    fx4* wlds = reinterpret_cast<fx4*>(lds + CT_WOFF);
+    for (int i = threadIdx.x; i < Ct * 16; i += CT_THREADS) wlds[i] = reinterpret_cast<const fx4*>(a.wpack)[i];
 
     // step k of quarter q: channels CPQ (NQ k + q) + {0 .. CPQ-1}
     auto load = [&](int k, float4 (&r)[CT_GT]) {
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             v[i][2] = mid.y;
             v[i][3] = p[i * CT_PS + 3];
         }
-        const cf4 wc = wpk + ci * 16;
+        const fx4* wc = wlds + ci * 16;
 #pragma unroll
         for (int ky = 0; ky < 4; ++ky) {
             const int py = (ky & 1) ? 0 : 1, dy = ky == 0 ? 1 : (ky == 3 ? -1 : 0);
@@ -498,9 +504,7 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     a.act = act;
     a.act_param = act_param;
 
-    const size_t main_bytes = (size_t)2 * CT_NQ * CT_CPQ * CT_PB * sizeof(float);
-    const size_t comb_bytes = (size_t)CT_QT * 16 * M * sizeof(float);
-    const size_t lds = main_bytes > comb_bytes ? main_bytes : comb_bytes;
+    const size_t lds = ((size_t)CT_WOFF + (size_t)(C0 + (x1 ? C1 : 0)) * 64) * sizeof(float);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
     typedef void (*CtKernel)(SmallMArgs);

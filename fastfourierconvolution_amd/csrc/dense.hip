@@ -34,41 +34,14 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
     const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
     const int b0 = tm * DN_BM;
     const int KS = 2 * KH + 1;   // rows zero-padded to 2 KH: the MFMA loop reads without bounds checks
-    // coalesced rows of A, 8 loads in flight per thread before their LDS stores
     const auto rA = ffc::buf_rsrc(a.A, (unsigned long long)a.B * a.K * 4);
     const auto rW = ffc::buf_rsrc(a.Wt, (unsigned long long)a.K * a.N * 4);
-    for (int i0 = 0; i0 < DN_BM * a.K; i0 += 8 * DN_THREADS) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u * DN_THREADS + tid;
-            const int r = i / a.K;
-            // unconditional load from a clamped address, then select: a branch around each load
-            // makes hipcc wait for every load on its own
-            const bool ok = i < DN_BM * a.K && b0 + r < a.B;
-            v[u] = ffc::buf_ld(rA, ok ? (unsigned)(((size_t)b0 * a.K + i) * 4) : ffc::OOB);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = i0 + u * DN_THREADS + tid;
-            const int r = i / a.K, k = i - r * a.K;
-            if (i < DN_BM * a.K) As[r * KS + k] = v[u];
-        }
-    }
-    for (int i = tid; i < DN_BM * (KS - a.K); i += DN_THREADS) {   // zero the row tails
-        const int r = i / (KS - a.K), k = a.K + (i - r * (KS - a.K));
-        As[r * KS + k] = 0.0f;
-    }
-    __syncthreads();
     const int wr = wave >> 1, wc = wave & 1;
     const int n = tn * DN_BN + wc * 32 + col;
     const bool nv = n < a.N;
-    const float* ar = As + (wr * 32 + col) * KS;   // this lane's A row
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-    // the lane's whole W column (k = 2u + hh, K <= 2 * KH) issued at once: one global-load latency
-    // per launch instead of one per 16-deep chunk (K = 100: 21 -> ~5 us)
+    // every global load of the workgroup in flight at once -- the lane's whole W column (k = 2u + hh,
+    // K <= 2 KH) and its share of the 64 x K A tile -- so the launch pays one memory latency
+    // (bounds-checked buffer loads: out-of-range elements read 0, no branch per load)
     float wa[KH];
 #pragma unroll
     for (int u = 0; u < KH; ++u) {
@@ -76,6 +49,30 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
         const bool ok = k < a.K && nv;
         wa[u] = ffc::buf_ld(rW, ok ? (unsigned)(((size_t)k * a.N + n) * 4) : ffc::OOB);
     }
+    constexpr int NA = DN_BM * 2 * KH / DN_THREADS;   // A elements per thread (K <= 2 KH)
+    float v[NA];
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+        const int i = u * DN_THREADS + tid;
+        const int r = i / a.K;
+        const bool ok = i < DN_BM * a.K && b0 + r < a.B;
+        v[u] = ffc::buf_ld(rA, ok ? (unsigned)(((size_t)b0 * a.K + i) * 4) : ffc::OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+        const int i = u * DN_THREADS + tid;
+        const int r = i / a.K, k = i - r * a.K;
+        if (i < DN_BM * a.K) As[r * KS + k] = v[u];
+    }
+    for (int i = tid; i < DN_BM * (KS - a.K); i += DN_THREADS) {   // zero the row tails
+        const int r = i / (KS - a.K), k = a.K + (i - r * (KS - a.K));
+        As[r * KS + k] = 0.0f;
+    }
+    __syncthreads();
+    const float* ar = As + (wr * 32 + col) * KS;   // this lane's A row
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
 #pragma unroll
     for (int u = 0; u < KH; ++u)   // k >= K: zero A (padded rows) and zero W
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * u + hh], wa[u], acc, 0, 0, 0);

@@ -2,6 +2,7 @@
 results database (rocpd format, the default output of `rocprofv3 --kernel-trace --stats -d DIR`).
 
     python tools/rocpd_stats.py gpurun_out/prof_train/run_results.db > profiles/rXX/kernel_stats.csv
+    python tools/rocpd_stats.py --step <db> [first kernel of a step]   # the last step, launch by launch
 """
 import csv
 import sqlite3
@@ -19,5 +20,23 @@ def main(path):
         w.writerow([name, n, tot, round(avg, 1), round(100.0 * tot / total, 2), mn, mx])
 
 
+
+
+def last_step(path, first_kernel="dense_kernel"):
+    """the kernel sequence of the last step in a trace (from the last launch of `first_kernel`):
+    duration (us), workgroups, name -- where a step's time goes, launch by launch"""
+    c = sqlite3.connect(path)
+    rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
+    i0 = max(i for i, r in enumerate(rows) if first_kernel in r[0])
+    out = [((e - s) / 1e3, g // max(1, w), n) for n, s, e, g, w in rows[i0:]]
+    return out
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    if len(sys.argv) > 2 and sys.argv[1] == "--step":
+        seq = last_step(sys.argv[2], *(sys.argv[3:4]))
+        for us, wg, name in seq:
+            print(f"{us:8.2f} us {wg:7d} WG  {name[:90]}")
+        print(f"{sum(s[0] for s in seq):8.2f} us total, {len(seq)} launches")
+    else:
+        main(sys.argv[1])
