@@ -65,6 +65,14 @@ class ConvPJob(ctypes.Structure):
                 ("act", c_int), ("act_param", c_float), ("A3", c_void_p), ("a3_stride", ctypes.c_longlong)]
 
 
+class BnFold(ctypes.Structure):
+    """ffc_bn_fold: a train-mode BatchNorm finalized inside its consumer kernel"""
+    _fields_ = [("slab", c_void_p), ("nrows", c_int), ("C", c_int), ("gamma", c_void_p), ("beta", c_void_p),
+                ("running_mean", c_void_p), ("running_var", c_void_p), ("num_batches_tracked", c_void_p),
+                ("update_running", c_int), ("momentum", c_float), ("eps", c_float), ("count_mult", c_float),
+                ("scale_out", c_void_p), ("shift_out", c_void_p)]
+
+
 # (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
 SIGNATURES = [
     ("ffc_last_error", ctypes.c_char_p, []),
@@ -98,6 +106,9 @@ SIGNATURES = [
                             c_void_p]),
     ("ffc_fu_forward", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_fu_forward_ex", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                  c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, ctypes.POINTER(BnFold),
+                                  ctypes.POINTER(BnFold), c_void_p, c_void_p]),
     ("ffc_fu_pack_mix", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_pack_transpose", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_fu_lds_bytes", c_size_t, [c_int, c_int, c_int]),
@@ -176,10 +187,10 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (c_int * 6)()
-        lib.ffc_struct_sizes(sizes, 6)
+        sizes = (c_int * 7)()
+        lib.ffc_struct_sizes(sizes, 7)
         want = (ctypes.sizeof(ConvSeg), ctypes.sizeof(ConvPhase), ctypes.sizeof(ConvJob),
-                ctypes.sizeof(ConvPSeg), ctypes.sizeof(ConvPPhase), ctypes.sizeof(ConvPJob))
+                ctypes.sizeof(ConvPSeg), ctypes.sizeof(ConvPPhase), ctypes.sizeof(ConvPJob), ctypes.sizeof(BnFold))
         if tuple(sizes) != want:
             raise FFCError(f"ABI struct layout mismatch: library {tuple(sizes)} vs binding {want}")
         _lib = lib

@@ -153,6 +153,55 @@ def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: flo
     return scale, shift
 
 
+# Train-mode BNs whose consumer kernel finalizes them in-kernel (ffc_bn_fold) instead of a
+# separate ffc_bn_reduce_finalize launch: single rank only (SyncBN all-reduces the moments between
+# the merge and the finalize).  FFC_BN_FOLD=0 restores the separate launch (A/B measurements).
+BN_FOLD = __import__("os").environ.get("FFC_BN_FOLD", "1") != "0"
+# slab rows x channels up to which the fold beats the separate launch (each consumer workgroup
+# reads the whole slab; measured on MI355X, r02)
+BN_FOLD_MAX = int(__import__("os").environ.get("FFC_BN_FOLD_MAX", "4096"))
+# the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
+FU_SPILL = __import__("os").environ.get("FFC_FU_SPILL", "1") != "0"
+
+
+class BnFoldDesc:
+    """an ffc_bn_fold for ``bn`` over the partial rows ``slab`` plus the tensors it points at;
+    scale / shift receive the folded affine (written by the consumer's workgroup 0)"""
+
+    def __init__(self, bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device):
+        _, update = bn_mode(bn)
+        self.slab = slab
+        self.scale = torch.empty(C, device=device, dtype=torch.float32)
+        self.shift = torch.empty(C, device=device, dtype=torch.float32)
+        self.bn = bn
+        self.struct = _lib.BnFold(
+            ptr(slab), int(nrows), int(C),
+            ptr(bn.weight.detach()) if bn.weight is not None else None,
+            ptr(bn.bias.detach()) if bn.bias is not None else None,
+            ptr(bn.running_mean) if update else None, ptr(bn.running_var) if update else None,
+            ptr(bn.num_batches_tracked) if update else None, int(update),
+            -1.0 if bn.momentum is None else float(bn.momentum), float(bn.eps), float(count_mult),
+            ptr(self.scale), ptr(self.shift))
+
+    def materialize(self, stream):
+        """(scale, shift) by the separate reduce + finalize launch (consumers without a fold)"""
+        return bn_scale_shift(self.bn, self.struct.C, self.slab, self.struct.nrows, self.struct.count_mult,
+                              self.scale.device, stream)
+
+
+def bn_fold(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device):
+    """a BnFoldDesc when ``bn`` can be finalized inside its consumer (batch statistics, one rank),
+    else None (use bn_scale_shift)"""
+    use_batch, _ = bn_mode(bn)
+    if not (BN_FOLD and use_batch and slab is not None and _sync_group() is None):
+        return None
+    if nrows * C > BN_FOLD_MAX:   # every consumer workgroup merges all rows: only small slabs pay
+        return None
+    if bn.num_features != C:
+        raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
+    return BnFoldDesc(bn, C, slab, nrows, count_mult, device)
+
+
 def act_code(mod: nn.Module):
     """activation module -> (FFC_ACT_* code, parameter).  layers/ffc/ffc_bn_act.py:63-67."""
     if isinstance(mod, nn.Identity):

@@ -1,0 +1,116 @@
+// BatchNorm finalized inside the kernel that consumes it (ffc_bn_fold, include/ffc_amd.h): every
+// workgroup merges the producer's {n, mean, M2} partial rows itself -- a fixed-order fp64 merge, so
+// every workgroup forms bit-identical scale / shift -- and workgroup 0 alone updates the running
+// statistics (nn.BatchNorm2d semantics, torch/nn/modules/batchnorm.py as called from
+// layers/ffc/*.py) and writes the folded scale / shift out for later kernels.  Saves the separate
+// reduce + finalize launch per BN (bn_se_kernels.hip) on the single-rank path.
+#pragma once
+
+#include "ffc_internal.h"
+
+namespace ffc {
+
+__device__ __forceinline__ double shfl_xor_f64(double v, int m) { return __shfl_xor(v, m, 64); }
+
+// BLOCK threads (whole waves).  A wave reads 4 partial rows x 16 consecutive channels per load
+// (four 256-byte segments); lane = 16 rg + oc.  The waves of a 16-channel block split its rows
+// ((wave-in-block, rg) interleaved), merge rg with a fixed xor tree, and the wave partials meet
+// in `scratch` (3 doubles per (block, wave, channel)) in wave order: a fixed merge order, so every
+// workgroup forms bit-identical scale / shift.  Writes sc[o], sh[o] (LDS) for o < f.C; workgroup
+// 0 (leader) also updates the running statistics, bumps num_batches_tracked (after every channel
+// read it) and stores scale_out / shift_out.  Ends with a barrier.  scratch: bn_fold_scratch().
+__host__ __device__ constexpr int bn_fold_scratch_doubles(int block) { return 3 * block / 4; }
+
+template <int BLOCK>
+__device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool leader, double* scratch) {
+    constexpr int NW = BLOCK / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int oc = lane & 15, rg = lane >> 4;
+    const int nb = (f.C + 15) >> 4;                 // 16-channel blocks
+    const int wpb = nb >= NW ? 1 : NW / nb;         // waves per block
+    const int RS = 4 * wpb;                         // row stride of one lane
+    const float4* slab = reinterpret_cast<const float4*>(f.slab);
+    const int64_t nbt = (leader && f.update_running && f.momentum < 0.0f) ? *f.num_batches_tracked : 0;
+    for (int cb0 = 0; cb0 < nb; cb0 += NW / wpb) {
+        const int cb = cb0 + wave / wpb, k = wave % wpb;
+        const int o = cb * 16 + oc;
+        const bool live = cb < nb && wave < (NW / wpb) * wpb;
+        const int oo = o < f.C ? o : f.C - 1;
+        double n = 0.0, s = 0.0, q = 0.0;
+        if (live) {
+            int r = k * 4 + rg;
+            for (; r + 3 * RS < f.nrows; r += 4 * RS) {   // four rows in flight per lane
+                float4 e[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) e[u] = slab[(size_t)(r + u * RS) * f.C + oo];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double en = e[u].x, em = e[u].y;
+                    n += en;
+                    s += en * em;
+                    q += (double)e[u].z + en * em * em;
+                }
+            }
+            for (; r < f.nrows; r += RS) {
+                const float4 e = slab[(size_t)r * f.C + oo];
+                const double en = e.x, em = e.y;
+                n += en;
+                s += en * em;
+                q += (double)e.z + en * em * em;
+            }
+        }
+        n += shfl_xor_f64(n, 16);
+        s += shfl_xor_f64(s, 16);
+        q += shfl_xor_f64(q, 16);
+        n += shfl_xor_f64(n, 32);
+        s += shfl_xor_f64(s, 32);
+        q += shfl_xor_f64(q, 32);
+        if (live && rg == 0) {
+            double* d = scratch + 3 * (wave * 16 + oc);
+            d[0] = n;
+            d[1] = s;
+            d[2] = q;
+        }
+        __syncthreads();
+        // one thread per channel of this round: the wpb wave partials in wave order, then finalize
+        if (tid < (NW / wpb) * 16) {
+            const int cbl = tid >> 4, c2 = cb0 + cbl, oc2 = tid & 15, o2 = c2 * 16 + oc2;
+            if (c2 < nb && o2 < f.C) {
+                double N = 0.0, S = 0.0, Q = 0.0;
+                for (int w = 0; w < wpb; ++w) {
+                    const double* d = scratch + 3 * ((cbl * wpb + w) * 16 + oc2);
+                    N += d[0];
+                    S += d[1];
+                    Q += d[2];
+                }
+                const double mu = S / N;
+                double v = Q / N - mu * mu;
+                if (v < 0.0) v = 0.0;
+                const float mean = (float)mu, var = (float)v;
+                const float inv = 1.0f / sqrtf(var + f.eps);
+                const float g = f.gamma ? f.gamma[o2] : 1.0f;
+                const float b = f.beta ? f.beta[o2] : 0.0f;
+                const float scale = g * inv;
+                const float shift = b - mean * scale;
+                sc[o2] = scale;
+                sh[o2] = shift;
+                if (leader) {
+                    if (f.update_running) {
+                        float fm = f.momentum;
+                        if (fm < 0.0f) fm = 1.0f / (float)(nbt + 1);   // momentum=None: cumulative average
+                        const double nfull = N * (double)f.count_mult;
+                        const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
+                        f.running_mean[o2] = (1.0f - fm) * f.running_mean[o2] + fm * mean;
+                        f.running_var[o2] = (1.0f - fm) * f.running_var[o2] + fm * (float)unb;
+                    }
+                    if (f.scale_out) f.scale_out[o2] = scale;
+                    if (f.shift_out) f.shift_out[o2] = shift;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (leader && f.update_running && tid == 0) *f.num_batches_tracked += 1;
+}
+
+}  // namespace ffc

@@ -35,5 +35,6 @@ extern "C" int ffc_struct_sizes(int* out, int n) {
     out[3] = (int)sizeof(ffc_convp_seg);
     out[4] = (int)sizeof(ffc_convp_phase);
     out[5] = (int)sizeof(ffc_convp_job);
+    if (n >= 7) out[6] = (int)sizeof(ffc_bn_fold);
     return FFC_OK;
 }

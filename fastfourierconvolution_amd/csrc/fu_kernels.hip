@@ -15,6 +15,7 @@
 // twice (pass 0 then pass 1) and recomputes the cheap FFT+mix instead of spilling Y to HBM,
 // so a train-mode FU moves 2 reads + 1 write of the activation (SURVEY.md §8d "12*N_r").
 #include "ffc_internal.h"
+#include "bn_common.h"
 
 #include <cmath>
 #include <mutex>
@@ -64,8 +65,11 @@ struct FuArgs {
     int C, Mpad, in_relu, residual, has_in_affine;
     int wm_lds;   // mix weight staged in LDS (when it fits beside the Z/Y planes)
     int scr_off;  // float offset of the pass-0 stats scratch in LDS
-    int bn_off;   // float offset of the pass-1 BN scale/shift (4C floats)
+    int bn_off;   // float offset of the pass-1 BN scale/shift (4C floats), then the folded input affine (2C)
     float norm;
+    ffc_bn_fold in_fold, mix_fold;   // BNs finalized in-kernel (has_*: in use)
+    int has_in_fold, has_mix_fold;
+    float* yspill;                   // (B, 2C, NB) mix output: written by pass 0, read by pass 1
 };
 
 constexpr int FU_THREADS = 512;
@@ -94,16 +98,21 @@ __device__ unsigned long long g_fu_trace[8 * 4096];
 #define FU_STAMP(i) do { } while (0)
 #endif
 
-// s row (channel ch, output row y) = transform(t) nearest-upsampled by UP
+// s row (channel ch, output row y) = transform(t) nearest-upsampled by UP; the input affine from
+// LDS (folded in this kernel) or global memory
 template <int W, int UP>
-__device__ __forceinline__ void load_s_row(const FuArgs& a, int b, int ch, int y, int H, float (&s)[W]) {
+__device__ __forceinline__ void load_s_row(const FuArgs& a, const float* insc, int b, int ch, int y, int H,
+                                           float (&s)[W]) {
     constexpr int tW = W / UP;
     const int tH = H / UP;
     const float* trow = a.t + ((size_t)(b * a.C + ch) * tH + y / UP) * tW;
     float tv[tW];
     load_row<tW>(trow, tv);
     float sc = 1.0f, sh = 0.0f;
-    if (a.has_in_affine) {
+    if (a.has_in_fold) {
+        sc = insc[ch];
+        sh = insc[a.C + ch];
+    } else if (a.has_in_affine) {
         sc = a.in_scale[ch];
         sh = a.in_shift[ch];
     }
@@ -130,7 +139,8 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     float* Yre = Zim + C * NB;
     float* Yim = Yre + C * NB;
     float* Wm = Yim + C * NB;   // mix weight (2C, Mpad), staged by LDS-DMA under the FFT phases
-    if (a.wm_lds) {
+    const bool from_spill = PASS == 1 && a.yspill != nullptr;   // pass 1 without the recompute
+    if (a.wm_lds && !from_spill) {
         typedef __attribute__((address_space(1))) void* gptr_t;
         typedef __attribute__((address_space(3))) void* lptr_t;
         const int n4 = (C2 * a.Mpad) >> 2;   // Mpad is a multiple of 32
@@ -146,19 +156,43 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     if (tid == 0) g_fu_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
     FU_STAMP(0);
+    const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
+    const int MT = (C2 + 31) >> 5, NTL = (NB + 31) >> 5;
     float* bnss = smem + a.bn_off;    // pass 1: BN scale [2C] | shift [2C]
+    float* insc = bnss + 2 * C2;      // folded input affine: scale [C] | shift [C]
+    // fold scratch: the Z/Y planes, all free until the row R2C / spill load below
+    double* fscr = reinterpret_cast<double*>(smem);
+    if (a.has_in_fold) ffc::bn_fold_block<FU_THREADS>(a.in_fold, insc, insc + C, blockIdx.x == 0, fscr);
     if constexpr (PASS == 1) {
-        for (int i = tid; i < C2; i += FU_THREADS) {
-            bnss[i] = a.bn_scale[i];
-            bnss[C2 + i] = a.bn_shift[i];
+        if (a.has_mix_fold) {
+            ffc::bn_fold_block<FU_THREADS>(a.mix_fold, bnss, bnss + C2, blockIdx.x == 0, fscr);
+        } else {
+            for (int i = tid; i < C2; i += FU_THREADS) {
+                bnss[i] = a.bn_scale[i];
+                bnss[C2 + i] = a.bn_shift[i];
+            }
         }
     }
+    if (from_spill) {
+        // Y of this sample from pass 0 -> BN + ReLU -> the Y planes (float4: NB is a multiple of 4)
+        __syncthreads();
+        const float4* ys = reinterpret_cast<const float4*>(a.yspill + (size_t)b * C2 * NB);
+        for (int i = tid; i < C2 * NB / 4; i += FU_THREADS) {
+            const int o = (4 * i) / NB, n = 4 * i - o * NB;
+            const float4 v = ys[i];
+            const float sc = bnss[o], sh = bnss[C2 + o];
+            float* dst = ((o & 1) ? Yim : Yre) + (o >> 1) * NB + n;
+            *reinterpret_cast<float4*>(dst) = make_float4(fmaxf(fmaf(v.x, sc, sh), 0.0f), fmaxf(fmaf(v.y, sc, sh), 0.0f),
+                                                          fmaxf(fmaf(v.z, sc, sh), 0.0f), fmaxf(fmaf(v.w, sc, sh), 0.0f));
+        }
+        __syncthreads();
+    } else {
 
     // 1. row R2C (real W-point FFT per (channel,row)), input transform fused
     for (int r = tid; r < C * H; r += FU_THREADS) {
         const int ch = r / H, y = r - ch * H;
         float re[W], im[W];
-        load_s_row<W, UP>(a, b, ch, y, H, re);
+        load_s_row<W, UP>(a, insc, b, ch, y, H, re);
 #pragma unroll
         for (int x = 0; x < W; ++x) im[x] = 0.0f;
         fft_reg<W, false>(re, im);
@@ -196,8 +230,6 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
 
     // 3. spectral mix on MFMA: Y[o][n] = sum_i Wmix[o][i] Z[i][n], Z[2c+h] = (h ? Im : Re)(channel c)
     //    k-step s feeds k-slot h = lane>>5 with channel s, component h.
-    const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
-    const int MT = (C2 + 31) >> 5, NTL = (NB + 31) >> 5;
     for (int tile = wave; tile < MT * NTL; tile += FU_THREADS / 64) {
         const int mt = tile % MT, nt = tile / MT;
         floatx16 acc;
@@ -219,6 +251,14 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         const int n = nt * 32 + col;
         const bool nvalid = n < NB;
         if constexpr (PASS == 0) {
+            if (a.yspill) {   // raw Y for pass 1 (row o: 32 consecutive bins per store)
+                float* ys = a.yspill + (size_t)b * C2 * NB;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (nvalid && o < C2) ys[(size_t)o * NB + n] = acc[r];
+                }
+            }
             const int nv = min(32, NB - nt * 32);
             float mean, m2;
             ffc::tile_row_stats(acc, nv, smem + a.scr_off + wave * ffc::TILE_SCRATCH, mean, m2);
@@ -242,6 +282,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     }
     __syncthreads();
     FU_STAMP(3);
+    }   // !from_spill
 
     if constexpr (PASS == 0) {
         FU_STAMP(4);
@@ -308,7 +349,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             fft_reg<W, true>(re, im);
             if (a.residual) {
                 float s[W];
-                load_s_row<W, UP>(a, b, ch, y, H, s);
+                load_s_row<W, UP>(a, insc, b, ch, y, H, s);
 #pragma unroll
                 for (int x = 0; x < W; ++x) re[x] += s[x];
             }
@@ -373,7 +414,7 @@ FuLayout fu_layout(int C, int H, int W) {
     for (int wm = 1; wm >= 0; --wm) {
         const size_t wfl = wm ? fu_wm_floats(C) : 0;
         const size_t scr = in_y ? 0 : FU_SCRATCH;
-        const size_t floats = 4 * plane + wfl + scr + 4 * (size_t)C;
+        const size_t floats = 4 * plane + wfl + scr + 6 * (size_t)C;
         if (4 * floats <= 160 * 1024)
             return {4 * floats, wm, (int)(in_y ? 3 * plane : 4 * plane + wfl), (int)(4 * plane + wfl + scr)};
     }
@@ -399,6 +440,15 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
                               const float* in_shift, int in_relu, const float* wmixT, int pass,
                               float* stats_slab, const float* bn_scale, const float* bn_shift, int residual,
                               float* out, void* stream) {
+    return ffc_fu_forward_ex(t, B, C, H, W, up, in_scale, in_shift, in_relu, wmixT, pass, stats_slab, bn_scale,
+                             bn_shift, residual, out, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                                 const float* in_shift, int in_relu, const float* wmixT, int pass, float* stats_slab,
+                                 const float* bn_scale, const float* bn_shift, int residual, float* out,
+                                 const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill,
+                                 void* stream) {
     FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu_forward: B and C must be positive");
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu_forward: up must be 1 or 2");
     FFC_CHECK_ARG(pass == 0 || pass == 1, "ffc_fu_forward: pass must be 0 or 1");
@@ -408,7 +458,20 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
     FFC_CHECK_ARG(t && wmixT, "ffc_fu_forward: null input");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu_forward: in_scale/in_shift pairing");
     if (pass == 0) FFC_CHECK_ARG(stats_slab != nullptr, "ffc_fu_forward: pass 0 needs stats_slab");
-    if (pass == 1) FFC_CHECK_ARG(bn_scale && bn_shift && out, "ffc_fu_forward: pass 1 needs bn_scale/shift/out");
+    if (pass == 1)
+        FFC_CHECK_ARG(((bn_scale && bn_shift) || mix_fold) && out, "ffc_fu_forward: pass 1 needs bn_scale/shift/out");
+    FFC_CHECK_ARG(!in_fold || (pass == 0 && !in_scale && in_fold->scale_out && in_fold->shift_out),
+                  "ffc_fu_forward: in_fold is pass 0 only, replaces in_scale/in_shift and needs scale_out/shift_out");
+    FFC_CHECK_ARG(!mix_fold || pass == 1, "ffc_fu_forward: mix_fold is pass 1 only");
+    for (const ffc_bn_fold* f : {in_fold, mix_fold})
+        FFC_CHECK_ARG(!f || (f->slab && f->nrows > 0 &&
+                             (!f->update_running || (f->running_mean && f->running_var && f->num_batches_tracked))),
+                      "ffc_fu_forward: incomplete ffc_bn_fold");
+    FFC_CHECK_ARG(!in_fold || in_fold->C == C, "ffc_fu_forward: in_fold->C != C");
+    FFC_CHECK_ARG(!mix_fold || mix_fold->C == 2 * C, "ffc_fu_forward: mix_fold->C != 2C");
+    FFC_CHECK_ARG((!in_fold && !mix_fold) ||
+                      (size_t)16 * C * H * (W / 2 + 1) >= sizeof(double) * ffc::bn_fold_scratch_doubles(FU_THREADS),
+                  "ffc_fu_forward: plane too small for an in-kernel BN fold (use bn_scale / in_scale)");
     FuKernel k = pick_kernel(H, W, up, pass);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu_forward: no kernel instance");
     FuArgs a;
@@ -430,6 +493,14 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
     a.wm_lds = lay.wm_lds;
     a.scr_off = lay.scr_off;
     a.bn_off = lay.bn_off;
+    a.has_in_fold = in_fold != nullptr;
+    a.has_mix_fold = mix_fold != nullptr;
+    if (in_fold) {
+        a.in_fold = *in_fold;
+        a.has_in_affine = 1;
+    }
+    if (mix_fold) a.mix_fold = *mix_fold;
+    a.yspill = yspill;
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;

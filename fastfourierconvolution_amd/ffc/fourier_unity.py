@@ -4,6 +4,8 @@ Same constructor, attribute names (``conv_layer``, ``bn``, ``relu``) and state_d
 forward runs the fused HIP Fourier unit (csrc/fu_kernels.hip) instead of
 rfftn -> 1x1 conv -> BatchNorm2d -> ReLU -> irfftn.
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -45,8 +47,14 @@ class FourierUnitSN(nn.Module):
             self._mix_key = key
         return self._mixT
 
-    def _run(self, t, up=1, in_scale=None, in_shift=None, in_relu=False, residual=False):
-        """fused FU over s = transform(t) (see include/ffc_amd.h ffc_fu_forward)."""
+    @staticmethod
+    def _fold_ok(C, H, W):
+        """the fused kernel's planes hold the in-kernel BN fold's scratch (csrc/bn_common.h)"""
+        return 16 * C * H * (W // 2 + 1) >= 8 * 3 * 512 // 4
+
+    def _run(self, t, up=1, in_scale=None, in_shift=None, in_relu=False, residual=False, in_fold=None):
+        """fused FU over s = transform(t) (see include/ffc_amd.h ffc_fu_forward_ex).  in_fold: the
+        input BN (SpectralTransform.bn1) as an rt.BnFoldDesc, finalized inside pass 0."""
         B, C, th, tw = t.shape
         H, W = th * up, tw * up
         self._check(C)
@@ -59,8 +67,13 @@ class FourierUnitSN(nn.Module):
             fused = False
         if fused and staged_ok and (rt.FU_PATH == "staged" or (rt.FU_PATH == "auto" and B < rt.FU_FUSED_MIN_BATCH)):
             fused = False
+        if in_fold is not None and fused and not self._fold_ok(C, H, W):
+            in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
+            in_fold = None
         if not fused:
             if L.ffc_fu2d_supported(C, H, W, up):
+                if in_fold is not None:
+                    in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
                 return self._run2d(t, up, in_scale, in_shift, in_relu, residual)
             raise NotImplementedError(f"Fourier unit supports H,W in {{4,8,16,32}} with 16*C*H*(W/2+1) <= 160 KiB "
                                       f"(fused) or square H=W in {{16,32,64,128}} with 2C <= 128 (staged); "
@@ -70,18 +83,32 @@ class FourierUnitSN(nn.Module):
         mixT = self._packed_mix(dev, stream)
         use_batch, _ = rt.bn_mode(self.bn)
         n_r = float(B * C * H * W)              # fused FU moves 4*N_r per read/write
+        n_y = float(B * 2 * C * H * (W // 2 + 1))
+        sc = sh = mix_fold = yspill = None
         if use_batch:
             slab = torch.empty((B, 2 * C, 4), device=dev, dtype=torch.float32)
-            with rt.observe("fu_pass0", bytes=4.0 * n_r):
-                check(L.ffc_fu_forward(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
-                                     0, ptr(slab), None, None, 0, None, stream), "ffc_fu_forward(pass 0)")
-            sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, B, 1.0, dev, stream)
+            # pass 0 keeps its mix output Y for pass 1 (no second row R2C + column FFT + mix)
+            yspill = torch.empty(int(n_y), device=dev, dtype=torch.float32) if rt.FU_SPILL else None
+            with rt.observe("fu_pass0", bytes=4.0 * n_r + (4.0 * n_y if rt.FU_SPILL else 0.0)):
+                check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
+                                          None if in_fold else ptr(in_shift), int(in_relu), ptr(mixT), 0, ptr(slab),
+                                          None, None, 0, None, ctypes.byref(in_fold.struct) if in_fold else None,
+                                          None, ptr(yspill), stream), "ffc_fu_forward(pass 0)")
+            if in_fold is not None:          # pass 0's workgroup 0 wrote the folded bn1 affine
+                in_scale, in_shift = in_fold.scale, in_fold.shift
+            mix_fold = rt.bn_fold(self.bn, 2 * C, slab, B, 1.0, dev) if self._fold_ok(C, H, W) else None
+            if mix_fold is None:
+                sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, B, 1.0, dev, stream)
         else:
+            if in_fold is not None:
+                in_scale, in_shift = in_fold.materialize(stream)
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
-        with rt.observe("fu_pass1", bytes=8.0 * n_r):
-            check(L.ffc_fu_forward(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
-                                 1, None, ptr(sc), ptr(sh), int(residual), ptr(out), stream), "ffc_fu_forward(pass 1)")
+        with rt.observe("fu_pass1", bytes=(4.0 * n_y + 4.0 * n_r if yspill is not None else 4.0 * n_r) + 4.0 * n_r):
+            check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT), 1,
+                                      None, ptr(sc), ptr(sh), int(residual), ptr(out), None,
+                                      ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), stream),
+                  "ffc_fu_forward(pass 1)")
         return out
 
     def _packed_mix16(self, device, stream):

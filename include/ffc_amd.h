@@ -41,7 +41,7 @@ extern "C" {
 const char* ffc_last_error(void);
 int ffc_abi_version(void);
 /* sizeof(ffc_conv_seg), (ffc_conv_phase), (ffc_conv_job), (ffc_convp_seg), (ffc_convp_phase),
- * (ffc_convp_job) -> out[0..5] */
+ * (ffc_convp_job) -> out[0..5]; n >= 7: sizeof(ffc_bn_fold) -> out[6] */
 int ffc_struct_sizes(int* out, int n);
 
 /* ------------------------------------------------------------------ local branch
@@ -310,6 +310,39 @@ int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up, const flo
 int ffc_fu_pack_mix(const float* w, int C2, float* wmixT, void* stream);
 /* LDS bytes the fused FU kernel needs (0 if unsupported) */
 size_t ffc_fu_lds_bytes(int C, int H, int W);
+
+/* A train-mode BatchNorm finalized inside the kernel that applies it (single rank: no all-reduce
+ * between the batch-statistics merge and the finalize).  Each workgroup of the consumer merges
+ * the producer's partial rows slab[nrows][C] float4 {n, mean, M2, 0} in a fixed order (bit-identical
+ * scale / shift everywhere); workgroup 0 updates running_mean / running_var (unbiased variance
+ * over n * count_mult samples, momentum < 0 = cumulative average), bumps num_batches_tracked
+ * (update_running) and writes scale_out / shift_out when given.  Replaces ffc_bn_reduce_finalize
+ * + passing its scale / shift. */
+typedef struct ffc_bn_fold {
+    const float* slab;
+    int nrows, C;
+    const float* gamma;
+    const float* beta;
+    float* running_mean;
+    float* running_var;
+    int64_t* num_batches_tracked;
+    int update_running;
+    float momentum, eps, count_mult;
+    float* scale_out;
+    float* shift_out;
+} ffc_bn_fold;
+
+/* ffc_fu_forward with the BNs folded in and pass 1 fed from pass 0 (no recompute):
+ *   in_fold (optional, pass 0): bn1 of SpectralTransform finalized in-kernel from its slab, used as
+ *           (in_scale, in_shift), and written to in_fold->scale_out / shift_out (required) for pass 1
+ *           and later kernels (pass 1 then takes them as in_scale / in_shift);
+ *   mix_fold (optional, pass 1): the FU's own BN from pass 0's slab instead of bn_scale / bn_shift;
+ *   yspill (optional, both passes): (B, 2C, H, W/2+1) floats: pass 0 stores the mix output Y there,
+ *           pass 1 applies BN + ReLU to it instead of recomputing row R2C + column FFT + mix. */
+int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                      const float* in_shift, int in_relu, const float* wmixT, int pass, float* stats_slab,
+                      const float* bn_scale, const float* bn_shift, int residual, float* out,
+                      const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream);
 
 /* Large-plane Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56, for planes whose
  * per-sample spectrum does not fit one workgroup's LDS: the fgan128 generator's 64x64 and

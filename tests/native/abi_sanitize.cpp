@@ -132,6 +132,25 @@ static void validation_paths() {
                    "pairing");
     EXPECT_INVALID(ffc_fu_forward(cp, 1, 4, 8, 8, 1, nullptr, nullptr, 0, cp, 1, nullptr, nullptr, nullptr, 0,
                                   nullptr, nullptr), "pass 1 needs");
+    {
+        ffc_bn_fold f;
+        std::memset(&f, 0, sizeof(f));
+        f.slab = cp;
+        f.nrows = 1;
+        f.C = 4;
+        EXPECT_INVALID(ffc_fu_forward_ex(cp, 1, 4, 8, 8, 1, nullptr, nullptr, 1, cp, 0, p, nullptr, nullptr, 0, nullptr,
+                                         &f, nullptr, nullptr, nullptr), "needs scale_out");
+        f.scale_out = p;
+        f.shift_out = p;
+        f.update_running = 1;
+        EXPECT_INVALID(ffc_fu_forward_ex(cp, 1, 4, 8, 8, 1, nullptr, nullptr, 1, cp, 0, p, nullptr, nullptr, 0, nullptr,
+                                         &f, nullptr, nullptr, nullptr), "incomplete ffc_bn_fold");
+        f.update_running = 0;
+        EXPECT_INVALID(ffc_fu_forward_ex(cp, 1, 4, 8, 8, 1, nullptr, nullptr, 1, cp, 0, p, nullptr, nullptr, 0, nullptr,
+                                         nullptr, &f, nullptr, nullptr), "mix_fold is pass 1 only");
+        EXPECT_INVALID(ffc_fu_forward_ex(cp, 1, 4, 8, 8, 1, nullptr, nullptr, 1, cp, 1, nullptr, nullptr, nullptr, 0, p,
+                                         nullptr, &f, nullptr, nullptr), "mix_fold->C != 2C");
+    }
     EXPECT_INVALID(ffc_fu2d_r2c(cp, 1, 4, 48, 48, nullptr, nullptr, 0, p, nullptr), "unsupported plane");
     EXPECT_INVALID(ffc_fu2d_mix(cp, 1, 65, 64, 64, 1, cp, 0, p, nullptr, nullptr, nullptr, nullptr), "unsupported");
     EXPECT_INVALID(ffc_fu2d_mix(cp, 1, 8, 64, 64, 1, cp, 2, p, nullptr, nullptr, nullptr, nullptr), "pass must be");

@@ -45,7 +45,8 @@ def test_argument_validation_without_gpu():
     """invalid shapes are rejected before any launch, with a readable error"""
     lib = _lib.load()
     # Z/Y planes (Re, Im) + the mix weight (2C x ceil32(2C), whole 256-float DMA groups)
-    assert lib.ffc_fu_lds_bytes(16, 32, 32) == 16 * 16 * 32 * 17 + 4 * 32 * 32 + 4 * 4 * 16   # + BN scale/shift
+    # + BN scale/shift (4C) + the folded input affine (2C)
+    assert lib.ffc_fu_lds_bytes(16, 32, 32) == 16 * 16 * 32 * 17 + 4 * 32 * 32 + 4 * 6 * 16
     assert lib.ffc_fu_lds_bytes(16, 64, 64) == 0          # large planes: the staged FU (ffc_fu2d_*)
     assert lib.ffc_fu2d_supported(16, 64, 64, 2) == 1 and lib.ffc_fu2d_supported(32, 128, 128, 1) == 1
     assert lib.ffc_fu2d_supported(65, 64, 64, 1) == 0     # 2C > 128

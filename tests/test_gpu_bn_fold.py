@@ -1,0 +1,73 @@
+"""BN folded into its consumer (ffc_bn_fold, csrc/bn_common.h) and the fused FU's pass 1 fed from
+pass 0's spilled mix output (ffc_fu_forward_ex yspill) against the separate reduce/finalize launch
+and the recompute: SpectralTransform (layers/ffc/spectral_transform.py:79-108 with
+FourierUnitSN, fourier_unity.py:32-56) in train mode on the fused per-sample FU path, momentum
+0.1 and None (cumulative average), several steps (running statistics, num_batches_tracked).
+Outputs within 1e-6 normwise (the folded merge order differs from bn_reduce_finalize's only in
+fp64 rounding); buffers within 1e-6; num_batches_tracked exact; the default path bitwise
+deterministic."""
+import contextlib
+import copy
+import io
+
+import pytest
+import torch
+
+from oracle.ffc_oracle import normwise_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _st(cin, cout, momentum, seed):
+    import fastfourierconvolution_amd as F
+    torch.manual_seed(seed)
+    with contextlib.redirect_stdout(io.StringIO()):
+        st = F.SpectralTransform(cin, cout, stride=2, upsample=True)
+    for m in st.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = momentum
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    return st.cuda().train()
+
+
+def _run(st, xs, fold, spill):
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.BN_FOLD, rt.FU_SPILL, rt.FU_PATH
+    rt.BN_FOLD, rt.FU_SPILL, rt.FU_PATH = fold, spill, "fused"
+    try:
+        with torch.no_grad():
+            outs = [st(x).clone() for x in xs]
+        torch.cuda.synchronize()
+    finally:
+        rt.BN_FOLD, rt.FU_SPILL, rt.FU_PATH = old
+    return outs, {k: v.detach().clone() for k, v in st.state_dict().items()}
+
+
+@pytest.mark.parametrize("momentum", [0.1, None])
+@pytest.mark.parametrize("cin,cout,hw,B", [(64, 64, 4, 12), (32, 32, 8, 5), (16, 16, 16, 3)])
+def test_fold_and_spill_match_separate_launches(momentum, cin, cout, hw, B):
+    base = _st(cin, cout, momentum, seed=cin + hw)
+    g = torch.Generator().manual_seed(hw)
+    xs = [torch.randn((B, cin, hw, hw), generator=g).cuda() for _ in range(3)]
+    ref_out, ref_sd = _run(copy.deepcopy(base), xs, False, False)
+    for fold, spill in [(True, False), (False, True), (True, True)]:
+        out, sd = _run(copy.deepcopy(base), xs, fold, spill)
+        for a, b in zip(out, ref_out):
+            assert normwise_err(a.double().cpu(), b.double().cpu()) <= 1e-6, (fold, spill)
+        for k, v in ref_sd.items():
+            if k.endswith("num_batches_tracked"):
+                assert int(sd[k]) == int(v), (k, fold, spill)
+            elif k.endswith("running_mean") or k.endswith("running_var"):
+                torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=f"{k} {fold} {spill}")
+
+
+def test_folded_path_deterministic():
+    base = _st(32, 32, 0.1, seed=3)
+    xs = [torch.randn((9, 32, 8, 8), generator=torch.Generator().manual_seed(2)).cuda()]
+    a, sa = _run(copy.deepcopy(base), xs, True, True)
+    b, sb = _run(copy.deepcopy(base), xs, True, True)
+    assert torch.equal(a[0], b[0])
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
