@@ -343,7 +343,8 @@ class ConvExec:
         if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and convq_cfg is not None:
             pp = _plan.plan_convq_job(B, M, segs, convq_cfg) or pp   # the launch group's common cfg
         elif USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and (
-                CONVQ_FORCE or pp is None or pp.npb * (-(-M // 32)) <= CONVQ_MAX_CONVP_TILES):
+                CONVQ_FORCE or pp is None or pp.npb * (-(-M // 32)) <= CONVQ_MAX_CONVP_TILES or
+                _plan.job_signature(B, M, segs) in _plan.convq_tuned()[0]):   # measured faster there
             pp = _plan.pick_convq_cfg(B, M, segs) or pp
         if pw_ok and pw_only and PW_KERNEL == "pw":
             self.kind, self.plan = "pw", _plan.plan_job(B, M, segs)

@@ -466,9 +466,13 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #endif
             return;   // no barrier follows
         }
-        Split3 anext[MT];   // tap 0's A of the coming chunk
+        // A of the current chunk, refilled tap by tap with the next chunk's right after the tap's
+        // MFMAs: every A load has a whole chunk of MFMAs to arrive in (L2 latency under load is
+        // ~1-2K cycles; loading taps 1-3 at the chunk start exposed it), in the same registers
+        Split3 a[4][MT];
         compute_setup(cs);
-        load_A(kseg + cch * 4, anext);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) load_A(kseg + cch * 4 + 16 * t, a[t]);
 #ifdef FFC_TRACE_Q
         QSTAMP(tq_a);
 #endif
@@ -489,17 +493,9 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
                 do { ++cn; } while (J.seg[cn].direct);
                 chn = 0;
             }
-            Split3 a[4][MT];
-            const int kc = kseg + cch * 4;   // chunk-major, then tap, then channel
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) a[0][mt] = anext[mt];
-#ifdef FFC_QPROBE_NOA
-            if (ci == 0)
-#endif
-#pragma unroll
-            for (int t = 1; t < 4; ++t) load_A(kc + 16 * t, a[t]);
-            // next chunk's tap 0 (the last chunk reloads its own: no branch around the load)
-            load_A(more ? P.kseg[cn] + chn * 4 : kc, anext);
+            // K base of the next chunk (chunk-major, then tap, then channel); the last chunk reloads
+            // its own: no branch around the loads
+            const int kn = more ? P.kseg[cn] + chn * 4 : kseg + cch * 4;
             __builtin_amdgcn_sched_barrier(0);
 #ifdef FFC_TRACE_Q
             QSTAMP(tq_b);
@@ -530,12 +526,12 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = mfma_split3(a[t][mt], b, acc[mt][nt]);
                 }
+                load_A(kn + 16 * t, a[t]);   // refill: the next chunk's tap t
                 // keep the next tap's reads ahead of this tap's MFMAs (the scheduler otherwise sinks
-                // each read to just before its first use and waits on it)
-                if (t + 1 < 4) {
-                    __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTW, 0);    // DS_READ
-                    __builtin_amdgcn_sched_group_barrier(0x8, 6 * NTW * MT, 0); // MFMA
-                }
+                // each read to just before its first use and waits on it), the refill after them
+                if (t + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTW, 0);   // DS_READ
+                __builtin_amdgcn_sched_group_barrier(0x8, 6 * NTW * MT, 0);                // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x20, 3 * MT, 0);                     // VMEM_READ
                 __builtin_amdgcn_sched_barrier(0);
             }
 #endif

@@ -103,10 +103,22 @@ __device__ __forceinline__ float apply_act(float v, int act, float p) {
 }
 
 // Sum over the 32 lanes of each half-wave (lanes l and l^k, k < 32).
+// Sum over each 32-lane half of the wave, in every lane: DPP butterflies inside the 16-lane rows
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: VALU, no LDS) and one
+// v_permlane16_swap across the rows of a half (gfx950).  Symmetric steps: all 32 lanes hold the
+// bit-identical sum.  (xor __shfl chains compile to ds_bpermute: an LDS round trip per step.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_full(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float half_wave_sum(float v) {
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += dpp_full<0xB1>(v);
+    v += dpp_full<0x4E>(v);
+    v += dpp_full<0x141>(v);
+    v += dpp_full<0x140>(v);
+    const int iv = __builtin_bit_cast(int, v);
+    const auto sw = __builtin_amdgcn_permlane16_swap(iv, iv, false, false);
+    return __builtin_bit_cast(float, (int)sw[0]) + __builtin_bit_cast(float, (int)sw[1]);
 }
 
 // DPP lane moves (no LDS round trip).  CTRL: 0x111..0x11F row_shr:1..15, 0xB1 quad_perm [1,0,3,2]

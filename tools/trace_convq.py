@@ -27,7 +27,7 @@ L = P.rt.lib()
 read = L.ffc_debug_trace_read_q
 read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 read.restype = ctypes.c_int
-ntiles = int(keys.split(":")[-1])
+ntiles = int(keys.split(":")[-2])
 buf = np.zeros((ntiles, 16), dtype=np.uint64)
 assert read(buf.ctypes.data, buf.nbytes) == 0
 rt0, rt1 = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64)
