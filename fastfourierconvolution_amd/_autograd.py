@@ -320,8 +320,7 @@ class _BNActFn(torch.autograd.Function):
         use_batch, update = rt.bn_mode(bn)
         if bn.num_features != C:
             raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
-        if use_batch and rt._sync_group() is not None:
-            raise NotImplementedError("SyncBN on the training path (sharded backward) is not supported")
+        grp = rt._sync_group() if use_batch else None   # SyncBN: global-batch statistics
         L = rt.lib()
         dev, stream = x.device, _stream(x)
         scale = torch.empty(C, device=dev, dtype=torch.float32)
@@ -339,6 +338,9 @@ class _BNActFn(torch.autograd.Function):
             moments = torch.empty((C, 3), device=dev, dtype=torch.float64)
             with rt.observe("bn_moments", bytes=4.0 * x.numel()):
                 check(L.ffc_channel_moments(ptr(x), B, C, HW, ptr(ws), S, ptr(moments), stream), "ffc_channel_moments")
+            if grp is not None:
+                from .distributed import merge_moments
+                merge_moments(moments, group=grp)
             check(L.ffc_bn_finalize(ptr(moments), C, ptr(g), ptr(b), ptr(rm), ptr(rv), ptr(nbt), 1, int(update),
                                     momentum, float(bn.eps), 1.0, ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
         else:
@@ -356,6 +358,7 @@ class _BNActFn(torch.autograd.Function):
                               rstats[1] if rstats[1] is not None else torch.empty(0),
                               g if g is not None else torch.empty(0))
         ctx.use_batch = use_batch
+        ctx.grp = grp
         return y
 
     @staticmethod
@@ -371,6 +374,27 @@ class _BNActFn(torch.autograd.Function):
         dgamma = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.has_gamma else None
         dbeta = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.has_beta else None
         dx = torch.empty_like(x) if ctx.needs_input_grad[3] else None
+        if ctx.grp is not None:
+            # torch.nn.SyncBatchNorm backward: dx from the all-reduced {sum g, sum g*x}, this rank's
+            # own sums for dgamma / dbeta (the caller's data-parallel wrapper reduces parameter grads)
+            import torch.distributed as dist
+            stream = _stream(x)
+            sums = torch.empty((C, 2), device=x.device, dtype=torch.float64)
+            with rt.observe("bn_bwd", bytes=8.0 * x.numel()):
+                check(L.ffc_bn_bwd_sums(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), ctx.act, float(ctx.param),
+                                        ptr(ws), S, ptr(sums), stream), "ffc_bn_bwd_sums")
+            gsums = sums.clone()
+            dist.all_reduce(gsums, group=ctx.grp)
+            g = ptr(gamma) if ctx.has_gamma else None
+            check(L.ffc_bn_bwd_coeff(ptr(sums), C, ptr(moments), ctx.eps, g, ptr(coef), ptr(dgamma), ptr(dbeta),
+                                     stream), "ffc_bn_bwd_coeff")
+            check(L.ffc_bn_bwd_coeff(ptr(gsums), C, ptr(moments), ctx.eps, g, ptr(coef), None, None, stream),
+                  "ffc_bn_bwd_coeff")
+            if dx is not None:
+                with rt.observe("bn_bwd", bytes=12.0 * x.numel()):
+                    check(L.ffc_bn_bwd_apply(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), ctx.act,
+                                             float(ctx.param), ptr(coef), ptr(dx), stream), "ffc_bn_bwd_apply")
+            return None, None, None, dx, dgamma, dbeta
         with rt.observe("bn_bwd", bytes=12.0 * x.numel()):
             check(L.ffc_bn_bwd(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), ctx.act, float(ctx.param),
                                ptr(moments) if ctx.use_batch else None,

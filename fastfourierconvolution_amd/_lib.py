@@ -147,6 +147,12 @@ SIGNATURES = [
     ("ffc_act_bwd", c_int, [c_void_p, c_void_p, c_void_p, c_longlong, c_int, c_float, c_void_p]),
     ("ffc_reduce_splits", c_int, [c_int, c_int, c_int]),
     ("ffc_channel_moments", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_bn_bwd_sums", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float,
+                                c_void_p, c_int, c_void_p, c_void_p]),
+    ("ffc_bn_bwd_coeff", c_int, [c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p]),
+    ("ffc_bn_bwd_apply", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float,
+                                 c_void_p, c_void_p, c_void_p]),
     ("ffc_bn_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_float, c_void_p,
                            c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p]),

@@ -682,6 +682,52 @@ extern "C" int ffc_channel_moments(const float* x, int B, int C, int HW, double*
     return ffc::launch_status("ffc_channel_moments");
 }
 
+namespace {
+// ws[S][C][2] -> sums[C][2] in split order (fixed: deterministic)
+__global__ void bn_bwd_sums_kernel(const double* __restrict__ ws, int S, int C, double* __restrict__ sums) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double a = 0.0, b = 0.0;
+    for (int s = 0; s < S; ++s) {
+        a += ws[((size_t)s * C + c) * 2];
+        b += ws[((size_t)s * C + c) * 2 + 1];
+    }
+    sums[2 * c] = a;
+    sums[2 * c + 1] = b;
+}
+}  // namespace
+
+// SyncBN backward in three steps (the caller all-reduces the sums in between)
+extern "C" int ffc_bn_bwd_sums(const float* x, const float* dy, int B, int C, int HW, const float* scale,
+                               const float* shift, int act, float act_param, double* ws, int S, double* sums,
+                               void* stream) {
+    FFC_CHECK_ARG(x && dy && scale && shift && ws && sums && B > 0 && C > 0 && HW > 0 && S > 0,
+                  "ffc_bn_bwd_sums: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(C, S), dim3(256), 0, s, x, dy, B, C, HW, S, scale, shift, act,
+                       act_param, ws);
+    hipLaunchKernelGGL(bn_bwd_sums_kernel, dim3((C + 255) / 256), dim3(256), 0, s, ws, S, C, sums);
+    return ffc::launch_status("ffc_bn_bwd_sums");
+}
+
+extern "C" int ffc_bn_bwd_coeff(const double* sums, int C, const double* moments, float eps, const float* gamma,
+                                float* coef, float* dgamma, float* dbeta, void* stream) {
+    FFC_CHECK_ARG(sums && moments && coef && C > 0, "ffc_bn_bwd_coeff: bad args");
+    hipLaunchKernelGGL(bn_bwd_coeff_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sums, 1, C,
+                       moments, nullptr, nullptr, eps, gamma, coef, dgamma, dbeta);
+    return ffc::launch_status("ffc_bn_bwd_coeff");
+}
+
+extern "C" int ffc_bn_bwd_apply(const float* x, const float* dy, int B, int C, int HW, const float* scale,
+                                const float* shift, int act, float act_param, const float* coef, float* dx,
+                                void* stream) {
+    FFC_CHECK_ARG(x && dy && scale && shift && coef && dx && B > 0 && C > 0 && HW > 0, "ffc_bn_bwd_apply: bad args");
+    const long long total = (long long)B * C * HW;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, dy, C, HW,
+                       total, scale, shift, act, act_param, coef, dx);
+    return ffc::launch_status("ffc_bn_bwd_apply");
+}
+
 extern "C" int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW, const float* scale,
                           const float* shift, int act, float act_param, const double* moments, const float* rmean,
                           const float* rvar, float eps, const float* gamma, double* ws, int S, float* coef,

@@ -416,6 +416,17 @@ int ffc_bn_bwd(const float* x, const float* dy, int B, int C, int HW, const floa
                int act, float act_param, const double* moments, const float* rmean, const float* rvar, float eps,
                const float* gamma, double* ws, int S, float* coef, float* dgamma, float* dbeta, float* dx,
                void* stream);
+/* The same backward split for SyncBN (sharded training, torch.nn.SyncBatchNorm semantics):
+ * ffc_bn_bwd_sums -> sums[C][2] = {sum g, sum g*x} of this rank (fp64, fixed order); the caller
+ * all-reduces a copy; ffc_bn_bwd_coeff(global sums, global moments) -> coef for dx, and
+ * ffc_bn_bwd_coeff(local sums, ...) -> this rank's dgamma / dbeta (coef scratch); then
+ * ffc_bn_bwd_apply -> dx. */
+int ffc_bn_bwd_sums(const float* x, const float* dy, int B, int C, int HW, const float* scale, const float* shift,
+                    int act, float act_param, double* ws, int S, double* sums, void* stream);
+int ffc_bn_bwd_coeff(const double* sums, int C, const double* moments, float eps, const float* gamma, float* coef,
+                     float* dgamma, float* dbeta, void* stream);
+int ffc_bn_bwd_apply(const float* x, const float* dy, int B, int C, int HW, const float* scale, const float* shift,
+                     int act, float act_param, const float* coef, float* dx, void* stream);
 /* Weight gradient of nn.Conv2d / nn.ConvTranspose2d / 1x1 conv / nn.Linear (ffc.py:45-70,
  * ffc_transpose.py:48-86, spectral_transform.py:23-28,52-71, fourier_unity.py:20-23):
  *   dW[m][n][kh][kw] = sum_b sum_q U[b][m][q] * V[b][n][qy*stride - pad + kh*dil][qx*stride - pad + kw*dil]

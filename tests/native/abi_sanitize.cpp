@@ -162,6 +162,9 @@ static void validation_paths() {
     EXPECT_INVALID(ffc_fu2d_c2r_rows(cp, 1, 4, 16, 16, cp, 1, nullptr, nullptr, 0, 0, p, nullptr), "unsupported plane");
     // --- training path (train_kernels.hip)
     EXPECT_INVALID(ffc_act_bwd(cp, cp, p, 16, 9, 0.f, nullptr), "ffc_act_bwd");
+    EXPECT_INVALID(ffc_bn_bwd_sums(cp, cp, 1, 4, 16, cp, cp, 0, 0.f, dbuf, 0, dbuf, nullptr), "ffc_bn_bwd_sums");
+    EXPECT_INVALID(ffc_bn_bwd_coeff(dbuf, 4, nullptr, 1e-5f, nullptr, p, nullptr, nullptr, nullptr), "ffc_bn_bwd_coeff");
+    EXPECT_INVALID(ffc_bn_bwd_apply(cp, cp, 1, 4, 16, cp, cp, 0, 0.f, cp, nullptr, nullptr), "ffc_bn_bwd_apply");
     EXPECT_INVALID(ffc_channel_moments(cp, 1, 4, 16, dbuf, 0, dbuf, nullptr), "ffc_channel_moments");
     EXPECT_INVALID(ffc_bn_bwd(cp, cp, 1, 4, 16, cp, cp, 0, 0.f, nullptr, nullptr, nullptr, 1e-5f, cp, dbuf, 1, p,
                               nullptr, nullptr, p, nullptr), "need batch moments");
