@@ -73,6 +73,12 @@ class BnFold(ctypes.Structure):
                 ("scale_out", c_void_p), ("shift_out", c_void_p)]
 
 
+class InTf(ctypes.Structure):
+    """ffc_in_tf: a producer's BN + activation (+ NoiseInjection) applied by the consuming conv"""
+    _fields_ = [("scale", c_void_p), ("shift", c_void_p), ("act", c_int), ("act_param", c_float),
+                ("noise_w", c_void_p), ("noise", c_void_p)]
+
+
 # (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
 SIGNATURES = [
     ("ffc_last_error", ctypes.c_char_p, []),
@@ -130,10 +136,15 @@ SIGNATURES = [
                                   c_int, c_void_p, c_void_p]),
     ("ffc_fu2d_c2r", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                              c_int, c_void_p, c_void_p]),
+    ("ffc_fu2d_c2r_bn", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),
     ("ffc_conv3x3_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                    c_int, c_int, c_void_p, c_int, c_float, c_void_p]),
+    ("ffc_conv3x3_smallm_tf", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
+                                      c_int, c_int, c_void_p, c_int, c_float, ctypes.POINTER(InTf),
+                                      ctypes.POINTER(InTf), c_void_p]),
     ("ffc_pw_gate_blocks", c_int, [c_int]),
     ("ffc_pw_gate_lds_bytes", c_size_t, [c_int, c_int]),
     ("ffc_pw_gate_conv", c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
@@ -193,10 +204,11 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (c_int * 7)()
-        lib.ffc_struct_sizes(sizes, 7)
+        sizes = (c_int * 8)()
+        lib.ffc_struct_sizes(sizes, 8)
         want = (ctypes.sizeof(ConvSeg), ctypes.sizeof(ConvPhase), ctypes.sizeof(ConvJob),
-                ctypes.sizeof(ConvPSeg), ctypes.sizeof(ConvPPhase), ctypes.sizeof(ConvPJob), ctypes.sizeof(BnFold))
+                ctypes.sizeof(ConvPSeg), ctypes.sizeof(ConvPPhase), ctypes.sizeof(ConvPJob), ctypes.sizeof(BnFold),
+                ctypes.sizeof(InTf))
         if tuple(sizes) != want:
             raise FFCError(f"ABI struct layout mismatch: library {tuple(sizes)} vs binding {want}")
         _lib = lib

@@ -247,6 +247,51 @@ def bn_act_noise_apply(x, scale, shift, act, param, noise_mod, noise=None):
     return x
 
 
+class PendingAct:
+    """A branch output whose BN + activation (+ NoiseInjection) has not been applied yet: the consumer
+    applies it while staging its operand (ffc_in_tf), so the separate read + write pass of the whole
+    tensor disappears.  ``materialize()`` runs that pass instead (for consumers without the option).
+    The noise is drawn when the pending value is created, in the order the eager path draws it."""
+
+    def __init__(self, raw, scale, shift, act, param, noise_mod=None, noise=None):
+        B, C, H, W = raw.shape
+        self.raw, self.scale, self.shift, self.act, self.param = raw, scale, shift, int(act), float(param)
+        self.noise_w = self.noise = None
+        if noise_mod is not None:
+            if noise is None:
+                noise = raw.new_empty(B, 1, H, W).normal_()
+            noise = require(noise, "noise")
+            if tuple(noise.shape) != (B, 1, H, W):
+                raise RuntimeError(f"noise must be {(B, 1, H, W)}, got {tuple(noise.shape)}")
+            w = require(noise_mod.weight.detach(), "NoiseInjection.weight")
+            if w.numel() != C:
+                raise RuntimeError(f"NoiseInjection has {w.numel()} channels, tensor has {C}")
+            self.noise_w, self.noise = w, noise
+        self.shape = raw.shape
+
+    def struct(self):
+        from ._lib import InTf
+        return InTf(ptr(self.scale), ptr(self.shift), self.act, self.param, ptr(self.noise_w), ptr(self.noise))
+
+    def materialize(self):
+        x = self.raw
+        if self.noise is not None:
+            with observe("bn_act_noise", bytes=8.0 * x.numel() + 4.0 * self.noise.numel()):
+                B, C, H, W = x.shape
+                check(lib().ffc_bn_act_noise_apply(ptr(x), ptr(x), B, C, H * W, ptr(self.scale), ptr(self.shift),
+                                                   self.act, self.param, ptr(self.noise_w), ptr(self.noise),
+                                                   stream_of(x)), "ffc_bn_act_noise_apply")
+            return x
+        return bn_act_apply(x, self.scale, self.shift, self.act, self.param)
+
+
+def materialize(x):
+    """PendingAct -> tensor (other values unchanged); tuples element-wise"""
+    if type(x) is tuple:
+        return tuple(materialize(v) for v in x)
+    return x.materialize() if isinstance(x, PendingAct) else x
+
+
 # --------------------------------------------------------------------------- convolution jobs
 def _wkey(ts):
     return tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)
@@ -309,6 +354,9 @@ FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU a
 FU_PATH = __import__("os").environ.get("FFC_FU_PATH", "auto")
 FU_FUSED_MIN_BATCH = 128
 FU_COLS = True      # staged FU: inverse column FFT fused into mix pass 1, rows-only C2R (H in 32..128)
+# staged FU, batch-statistics BN: pass 0 spills the raw Y and the whole-plane C2R applies BN + ReLU on
+# load (no second mix); FFC_FU2D_SPILL=0 keeps the two-pass mix
+FU2D_SPILL = __import__("os").environ.get("FFC_FU2D_SPILL", "1") != "0"
 # Run SpectralTransform's kernels on a side stream beside the local-branch GEMM of the same FFC
 # layer ("gemm-first" / "spectral-first": which is issued first).  Off by default: measured on
 # MI355X (B=256 generator) 10-18 % slower than one launch pairing the local and global GEMMs,

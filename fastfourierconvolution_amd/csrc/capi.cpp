@@ -36,5 +36,6 @@ extern "C" int ffc_struct_sizes(int* out, int n) {
     out[4] = (int)sizeof(ffc_convp_phase);
     out[5] = (int)sizeof(ffc_convp_job);
     if (n >= 7) out[6] = (int)sizeof(ffc_bn_fold);
+    if (n >= 8) out[7] = (int)sizeof(ffc_in_tf);
     return FFC_OK;
 }

@@ -38,6 +38,7 @@ struct SmallMArgs {
     int nty, ntx;
     int act;
     float act_param;
+    ffc_in_tf tf[2];     // conv3x3_smallm_kernel<MM, true>: deferred BN + act (+ noise) of segment s
 };
 
 // ---- ConvTranspose2d k4 s2 p1, M <= 4: 32x32 input tile (64x64 outputs) per workgroup.
@@ -282,7 +283,11 @@ constexpr int GT3 = (G3 + 255) / 256;       // groups per thread
 constexpr int PB3 = G3 * 4;                 // floats per patch buffer
 constexpr int CMAX3 = 256;                  // channels (both segments) whose weights fit the LDS slot
 
-template <int MM>
+// TF: each segment is read through its deferred transform a.tf[s] (ffc_in_tf): the producer's
+// BN + activation + NoiseInjection applied as the patch goes to LDS, on in-image groups only (the
+// zero padding belongs to the transformed tensor).  Same expression as bn_act_plane_kernel, so the
+// result is bit-identical to the separate pass; the noise float4 rides with the patch loads.
+template <int MM, bool TF>
 __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int half = threadIdx.x >> 8, tid = threadIdx.x & 255;
@@ -315,21 +320,56 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         }
     }
 
-    auto load = [&](int ci, float4 (&r)[GT3]) {
+    auto inimg = [&](int j) {
+        const int n = j * 256 + tid;
+        const int g = n % (S3 / 4), pr = n / (S3 / 4);
+        const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
+        return n < G3 && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
+    };
+    auto load = [&](int ci, float4 (&r)[GT3], float4 (&nz)[TF ? GT3 : 1]) {
         const int s = ci < a.C[0] ? 0 : 1;
         const int c = s == 0 ? ci : ci - a.C[0];
         const float* x = a.x[s] + ((size_t)b * a.C[s] + c) * a.IH * a.IW;
+        const float* npl = TF && a.tf[s].noise ? a.tf[s].noise + (size_t)b * a.IH * a.IW : nullptr;
 #pragma unroll
         for (int j = 0; j < GT3; ++j) {
             const int n = j * 256 + tid;
             const int g = n % (S3 / 4), pr = n / (S3 / 4);
             const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
             r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (n < G3 && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW)
-                r[j] = *reinterpret_cast<const float4*>(x + (size_t)iy * a.IW + ix);
+            if (inimg(j)) r[j] = *reinterpret_cast<const float4*>(x + (size_t)iy * a.IW + ix);
+            if constexpr (TF) {
+                nz[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (npl && inimg(j)) nz[j] = *reinterpret_cast<const float4*>(npl + (size_t)iy * a.IW + ix);
+            }
         }
     };
-    auto put = [&](float* dst, const float4 (&r)[GT3]) {
+    auto put = [&](float* dst, float4 (&r)[GT3], const float4 (&nz)[TF ? GT3 : 1], int ci) {
+        if constexpr (TF) {
+            const int s = ci < a.C[0] ? 0 : 1;
+            const int c = s == 0 ? ci : ci - a.C[0];
+            const ffc_in_tf& t = a.tf[s];
+            if (t.scale) {
+                const float sc = t.scale[c], sh = t.shift[c];
+                const float nw = t.noise ? t.noise_w[c] : 0.0f;
+                const int act = t.act;
+                const float p = t.act_param;
+#pragma unroll
+                for (int j = 0; j < GT3; ++j) {
+                    if (!inimg(j)) continue;
+                    float4 v = r[j];
+                    v = make_float4(ffc::apply_act(fmaf(v.x, sc, sh), act, p), ffc::apply_act(fmaf(v.y, sc, sh), act, p),
+                                    ffc::apply_act(fmaf(v.z, sc, sh), act, p), ffc::apply_act(fmaf(v.w, sc, sh), act, p));
+                    if (t.noise) {
+                        v.x = fmaf(nw, nz[j].x, v.x);
+                        v.y = fmaf(nw, nz[j].y, v.y);
+                        v.z = fmaf(nw, nz[j].z, v.z);
+                        v.w = fmaf(nw, nz[j].w, v.w);
+                    }
+                    r[j] = v;
+                }
+            }
+        }
 #pragma unroll
         for (int j = 0; j < GT3; ++j) {
             const int n = j * 256 + tid;
@@ -385,16 +425,17 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
     // one channel of prefetch in registers: channel k+1's loads are in flight under channel k's FMAs
     // (a second register set measured slower: 196 VGPRs, same occupancy)
     float4 r[GT3];
+    float4 nzr[TF ? GT3 : 1];
     if (half < nchunks) {
-        load(half, r);
-        put(buf(0), r);
+        load(half, r, nzr);
+        put(buf(0), r, nzr, half);
     }
     __syncthreads();
     for (int k = 0; k < nsteps; ++k) {
         const int cn = 2 * (k + 1) + half;
-        if (cn < nchunks) load(cn, r);
+        if (cn < nchunks) load(cn, r, nzr);
         compute(k);
-        if (cn < nchunks) put(buf(k + 1), r);
+        if (cn < nchunks) put(buf(k + 1), r, nzr, cn);
         __syncthreads();
     }
     // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
@@ -528,9 +569,10 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     return ffc::launch_status("ffc_convt_k4s2_smallm");
 }
 
-extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
-                                  const float* w1, const float* bias, int B, int H, int W, int M, float* out,
-                                  int act, float act_param, void* stream) {
+static int conv3x3_smallm_launch(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                                 const float* w1, const float* bias, int B, int H, int W, int M, float* out,
+                                 int act, float act_param, const ffc_in_tf* tf0, const ffc_in_tf* tf1,
+                                 void* stream) {
     FFC_CHECK_ARG(x0 && w0 && out && B > 0 && H > 0 && W > 0 && C0 > 0, "ffc_conv3x3_smallm: bad args");
     FFC_CHECK_ARG(M >= 1 && M <= 4, "ffc_conv3x3_smallm: 1 <= M <= 4");
     FFC_CHECK_ARG(!x1 || (w1 && C1 > 0), "ffc_conv3x3_smallm: second segment");
@@ -556,20 +598,50 @@ extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, cons
     a.act = act;
     a.act_param = act_param;
     FFC_CHECK_ARG(C0 + (x1 ? C1 : 0) <= CMAX3, "ffc_conv3x3_smallm: at most 256 input channels");
+    const ffc_in_tf none = {nullptr, nullptr, 0, 0.0f, nullptr, nullptr};
+    const ffc_in_tf* tfs[2] = {tf0, x1 ? tf1 : nullptr};
+    const bool tf = tfs[0] || tfs[1];
+    for (int s = 0; s < 2; ++s) {
+        const ffc_in_tf* t = tfs[s];
+        FFC_CHECK_ARG(!t || (t->scale && t->shift && (!t->noise || t->noise_w)),
+                      "ffc_conv3x3_smallm_tf: a transform needs scale, shift (and noise_w with noise)");
+        FFC_CHECK_ARG(!t || !t->noise || (reinterpret_cast<uintptr_t>(t->noise) & 15) == 0,
+                      "ffc_conv3x3_smallm_tf: noise not 16-B aligned");
+        a.tf[s] = t ? *t : none;
+    }
     const size_t lds = (CMAX3 * 48 + 4 * (size_t)PB3) * sizeof(float);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
-    auto k = M == 1 ? conv3x3_smallm_kernel<1> : M == 2 ? conv3x3_smallm_kernel<2>
-           : M == 3 ? conv3x3_smallm_kernel<3> : conv3x3_smallm_kernel<4>;
-    static bool raised[5] = {false, false, false, false, false};
-    if (!raised[M]) {
+    typedef void (*C3Kernel)(SmallMArgs);
+    static const C3Kernel kernels[2][4] = {
+        {conv3x3_smallm_kernel<1, false>, conv3x3_smallm_kernel<2, false>, conv3x3_smallm_kernel<3, false>,
+         conv3x3_smallm_kernel<4, false>},
+        {conv3x3_smallm_kernel<1, true>, conv3x3_smallm_kernel<2, true>, conv3x3_smallm_kernel<3, true>,
+         conv3x3_smallm_kernel<4, true>}};
+    auto k = kernels[tf ? 1 : 0][M - 1];
+    static bool raised[2][5] = {};
+    if (!raised[tf][M]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) {
             ffc::set_error("ffc_conv3x3_smallm: hipFuncSetAttribute failed");
             return FFC_E_LAUNCH;
         }
-        raised[M] = true;
+        raised[tf][M] = true;
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_conv3x3_smallm");
+}
+
+extern "C" int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                                  const float* w1, const float* bias, int B, int H, int W, int M, float* out,
+                                  int act, float act_param, void* stream) {
+    return conv3x3_smallm_launch(x0, C0, w0, x1, C1, w1, bias, B, H, W, M, out, act, act_param, nullptr, nullptr,
+                                 stream);
+}
+
+extern "C" int ffc_conv3x3_smallm_tf(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                                     const float* w1, const float* bias, int B, int H, int W, int M, float* out,
+                                     int act, float act_param, const ffc_in_tf* tf0, const ffc_in_tf* tf1,
+                                     void* stream) {
+    return conv3x3_smallm_launch(x0, C0, w0, x1, C1, w1, bias, B, H, W, M, out, act, act_param, tf0, tf1, stream);
 }

@@ -251,6 +251,8 @@ struct C2rArgs {
     float* out;
     int C, in_relu, residual;
     float norm;
+    const float* bn_scale;   // optional [2C]: Y is the raw mix output, relu(Y*bn_scale + bn_shift) on load
+    const float* bn_shift;
 };
 
 template <int H, int W, int UP>
@@ -264,9 +266,13 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     const int ch = plane % a.C;
     const int tid = threadIdx.x;
 
-    // 1. Y plane -> LDS rows of stride ZS (16 float2 loads in flight per thread per batch)
+    // 1. Y plane -> LDS rows of stride ZS (16 float2 loads in flight per thread per batch); a raw
+    //    (spilled) Y gets the FU's BN + ReLU here, the same expression as mix pass 1
     {
         const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)plane * H * WP;
+        const bool bn = a.bn_scale != nullptr;
+        const float bsr = bn ? a.bn_scale[2 * ch] : 1.0f, bhr = bn ? a.bn_shift[2 * ch] : 0.0f;
+        const float bsi = bn ? a.bn_scale[2 * ch + 1] : 1.0f, bhi = bn ? a.bn_shift[2 * ch + 1] : 0.0f;
         for (int i0 = 0; i0 < H * WP; i0 += 16 * FU2_THREADS) {
             float2 v[16];
 #pragma unroll
@@ -279,6 +285,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                 const int i = i0 + u * FU2_THREADS + tid;
                 if (i < H * WP) {
                     const int r = i / WP, k = i - r * WP;
+                    if (bn) v[u] = make_float2(fmaxf(fmaf(v[u].x, bsr, bhr), 0.0f), fmaxf(fmaf(v[u].y, bsi, bhi), 0.0f));
                     Z[r * ZS + k] = v[u];
                 }
             }
@@ -648,6 +655,16 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
         floatx16 acc[MT];
         mix_tile<MT, CC, F16>(acc, g, A, n, C, hh, col);
         if constexpr (PASS == 0) {
+            if (a.Y) {   // spill: the raw mix output, BN + ReLU applied by the C2R that reads it
+                float2* Yb = reinterpret_cast<float2*>(a.Y) + (size_t)b * C * NB;
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {
+                        const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even: Re, o+1: Im
+                        if (valid && o < C2) Yb[(size_t)(o >> 1) * NB + n] = make_float2(acc[mt][r], acc[mt][r + 1]);
+                    }
+            }
             const int nv = min(32, NB - tile * 32);
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
@@ -1123,15 +1140,17 @@ extern "C" int ffc_fu2d_mix_f16(const float* T, int B, int C, int H, int W, int 
     return ffc::launch_status("ffc_fu2d_mix_f16");
 }
 
-extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
-                            const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
-                            void* stream) {
+static int fu2d_c2r_launch(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                           const float* in_scale, const float* in_shift, int in_relu, int residual,
+                           const float* bn_scale, const float* bn_shift, float* out, void* stream) {
     FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_c2r: B and C must be positive");
+    FFC_CHECK_ARG((bn_scale == nullptr) == (bn_shift == nullptr), "ffc_fu2d_c2r: bn_scale/bn_shift pairing");
     FFC_CHECK_ARG(Y && out, "ffc_fu2d_c2r: null pointer");
     FFC_CHECK_ARG(!residual || t, "ffc_fu2d_c2r: residual needs t");
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu2d_c2r: up must be 1 or 2");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
-    C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W))};
+    C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
+              bn_scale, bn_shift};
     C2rKernel k = pick_c2r(H, W, up);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [16, 128])");
     const size_t lds = c2r_lds(H, W);
@@ -1139,6 +1158,21 @@ extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const fl
     if (rc) return rc;
     hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r");
+}
+
+extern "C" int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                            const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
+                            void* stream) {
+    return fu2d_c2r_launch(Y, B, C, H, W, t, up, in_scale, in_shift, in_relu, residual, nullptr, nullptr, out,
+                           stream);
+}
+
+extern "C" int ffc_fu2d_c2r_bn(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                               const float* in_scale, const float* in_shift, int in_relu, int residual,
+                               const float* bn_scale, const float* bn_shift, float* out, void* stream) {
+    FFC_CHECK_ARG(bn_scale && bn_shift, "ffc_fu2d_c2r_bn: bn_scale and bn_shift required");
+    return fu2d_c2r_launch(Y, B, C, H, W, t, up, in_scale, in_shift, in_relu, residual, bn_scale, bn_shift, out,
+                           stream);
 }
 
 extern "C" int ffc_fu2d_cols_supported(int C, int H, int W, int up, int f16) {
@@ -1187,7 +1221,8 @@ extern "C" int ffc_fu2d_c2r_rows(const float* Yc, int B, int C, int H, int W, co
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r_rows: unsupported plane (square, 32..128)");
     const int RB = H < 64 ? H : 64;
     const size_t lds = (size_t)RB * zstride(W / 2 + 1) * 8;
-    C2rArgs a{Yc, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W))};
+    C2rArgs a{Yc, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
+              nullptr, nullptr};
     hipLaunchKernelGGL(k, dim3(B * C * (H / RB)), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r_rows");
 }

@@ -8,6 +8,8 @@ with the FFC_BN_ACT activation fused into the epilogue (or BN partials, then one
 BN+activation pass when norm_layer is BatchNorm2d).  ``nn.Identity`` sub-convs keep the
 reference semantics: they return their input (usually the int 0 of the tuple protocol).
 """
+import ctypes
+
 import torch
 import torch.nn as nn
 
@@ -44,10 +46,17 @@ class _FFCExec:
                 raise NotImplementedError(f"{type(mod).__name__} in an FFC branch")
         return segs, weights, inputs, addends
 
-    def _run(self, x, y=None, act_l=(0, 0.0), act_g=(0, 0.0), bn_l=None, bn_g=None, noise=None):
+    def _run(self, x, y=None, act_l=(0, 0.0), act_g=(0, 0.0), bn_l=None, bn_g=None, noise=None, defer=False):
         """noise: optional {"l"|"g": (NoiseInjection, noise tensor or None)} applied after the branch's
-        BN + activation in the same pass (FFC_BN_ACT followed by the fgan128 NoiseInjection)"""
+        BN + activation in the same pass (FFC_BN_ACT followed by the fgan128 NoiseInjection).
+        defer: return rt.PendingAct outputs instead of running that pass (the consumer applies it).
+        Inputs may be PendingAct: a consumer that cannot apply them materializes them first."""
         x_l, x_g = x if type(x) is tuple else (x, 0)
+        if isinstance(x_l, rt.PendingAct) or isinstance(x_g, rt.PendingAct):
+            out = self._run_pending(x_l, x_g, y, act_l, act_g, bn_l, bn_g, noise)
+            if out is not None:
+                return out
+            x_l, x_g = rt.materialize(x_l), rt.materialize(x_g)
         if ag.wants_grad(self, x_l, x_g):
             return self._run_train(x_l, x_g, y, act_l, act_g, bn_l, bn_g, noise)
         if isinstance(x_l, torch.Tensor):
@@ -113,7 +122,24 @@ class _FFCExec:
             M = self.convl2g.out_channels if isinstance(self.convl2g, (nn.Conv2d, nn.ConvTranspose2d)) else (
                 self.convg2g.conv2.out_channels if isinstance(self.convg2g, SpectralTransform) else None)
             branches.append(("g", segs, w, inp, add, act_g, bn_g, M))
-        return self._launch_branches(branches, B, dev, stream, noise)
+        return self._launch_branches(branches, B, dev, stream, noise, defer)
+
+    def _run_pending(self, x_l, x_g, y, act_l, act_g, bn_l, bn_g, noise):
+        """Inputs with deferred BN + activation (+ noise): the direct 3x3 head (fgan128 conv7: local output
+        only, no BN, both inputs convs) reads them through ffc_in_tf.  -> (out_l, 0) or None (not fusable)"""
+        if y is not None or noise or bn_l is not None or self.ratio_gout != 0 or ag.wants_grad(self, x_l, x_g):
+            return None
+        parts = [(self.convl2l, x_l), (self.convg2l, x_g)]
+        if not all(isinstance(m, nn.Conv2d) and isinstance(t, (torch.Tensor, rt.PendingAct)) for m, t in parts):
+            return None
+        raw = [t.raw if isinstance(t, rt.PendingAct) else rt.require(t, "x") for _, t in parts]
+        segs, w, inp, add = self._branch([(m, r) for (m, _), r in zip(parts, raw)])
+        M = self.convl2l.out_channels
+        if self._smallm_kind(segs, w, None, None, M) != "conv3":
+            return None
+        tfs = [t if isinstance(t, rt.PendingAct) else None for _, t in parts]
+        return self._smallm("conv3", segs, w, inp, act_l, M, raw[0].shape[0], raw[0].device,
+                            rt.stream_of(raw[0]), tfs=tfs), 0
 
     def _run_train(self, x_l, x_g, y, act_l, act_g, bn_l, bn_g, noise):
         """training path (autograd recording): the layer's local convs and ST conv2 as one
@@ -180,9 +206,10 @@ class _FFCExec:
                 res[name] = ag.bn_act(bn, yv, act) if bn is not None else yv
         return res["l"], res["g"]
 
-    def _launch_branches(self, branches, B, dev, stream, noise=None):
+    def _launch_branches(self, branches, B, dev, stream, noise=None, defer=False):
         """plan / pack / launch the GEMM(s) of the given branches (one launch per kernel kind),
-        then BN statistics and BN+activation passes.  -> (out_l, out_g)"""
+        then BN statistics and BN+activation passes (defer: PendingAct outputs instead of those
+        passes).  -> (out_l, out_g)"""
         outs = {"l": 0, "g": 0}
         execs, jobs, post, built = [], [], [], []
         jb_name = {}
@@ -278,6 +305,10 @@ class _FFCExec:
                     continue
                 sc = torch.ones(C, device=dev, dtype=torch.float32)
                 sh = torch.zeros(C, device=dev, dtype=torch.float32)
+            if defer:
+                outs[name] = rt.PendingAct(out, sc, sh, act[0], act[1], *(nz if nz is not None else (None, None)))
+                done.add(name)
+                continue
             if nz is not None and out.shape[2] * out.shape[3] % 4 == 0:
                 mod, n = nz
                 rt.bn_act_noise_apply(out, sc, sh, act[0], act[1], mod, n)
@@ -372,7 +403,7 @@ class _FFCExec:
             return "conv3"
         return None
 
-    def _smallm(self, kind, segs, w, inp, act, M, B, dev, stream):
+    def _smallm(self, kind, segs, w, inp, act, M, B, dev, stream, tfs=None):
         IH, IW = segs[0].IH, segs[0].IW
         x1 = inp[1][0] if len(inp) > 1 else None
         w1 = w[1][0] if len(w) > 1 else None
@@ -403,6 +434,16 @@ class _FFCExec:
                                    [x for x, _ in inp], act=act)
         out = torch.empty((B, M, IH, IW), device=dev, dtype=torch.float32)
         flops = 2.0 * B * M * sum(sg.C for sg in segs) * 9 * IH * IW
+        if tfs is not None and any(t is not None for t in tfs):
+            st = [t.struct() if t is not None else None for t in tfs] + [None]
+            with rt.observe("conv3_smallm", flops=flops):
+                rt.check(rt.lib().ffc_conv3x3_smallm_tf(inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(),
+                                                        rt.ptr(x1), C1, rt.ptr(w1), rt.ptr(bias), B, IH, IW, M,
+                                                        out.data_ptr(), act[0], act[1],
+                                                        None if st[0] is None else ctypes.byref(st[0]),
+                                                        None if st[1] is None else ctypes.byref(st[1]), stream),
+                         "ffc_conv3x3_smallm_tf")
+            return out
         with rt.observe("conv3_smallm", flops=flops):
             rt.check(rt.lib().ffc_conv3x3_smallm(inp[0][0].data_ptr(), segs[0].C, w[0][0].data_ptr(), rt.ptr(x1), C1,
                                                  rt.ptr(w1), rt.ptr(bias), B, IH, IW, M, out.data_ptr(),

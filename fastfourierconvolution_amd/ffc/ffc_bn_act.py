@@ -61,3 +61,12 @@ class FFC_BN_ACT(nn.Module):
         bn_l, bn_g = self._norm(self.bn_l), self._norm(self.bn_g)
         return self.ffc._run(x, None, rt.act_code(self.act_l), rt.act_code(self.act_g), bn_l, bn_g,
                              noise={"l": noise_l, "g": noise_g})
+
+    def forward_deferred(self, x, noise_l=None, noise_g=None):
+        """forward (plus NoiseInjection when noise_* are given, as forward_noise) whose outputs are
+        rt.PendingAct: BN + activation + noise are left to the consuming layer, which applies them
+        while it stages its operands (or materializes them).  Not for autograd."""
+        bn_l, bn_g = self._norm(self.bn_l), self._norm(self.bn_g)
+        noise = {k: v for k, v in (("l", noise_l), ("g", noise_g)) if v is not None}
+        return self.ffc._run(x, None, rt.act_code(self.act_l), rt.act_code(self.act_g), bn_l, bn_g,
+                             noise=noise or None, defer=True)

@@ -139,23 +139,33 @@ class FourierUnitSN(nn.Module):
         with rt.observe("fu2d_r2c", bytes=4.0 * t.numel() + 8.0 * nT):
             check(L.ffc_fu2d_r2c(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(T), stream),
                   "ffc_fu2d_r2c")
+        out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
+        c2r_bytes = 8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)
         if use_batch:
             rows = L.ffc_fu2d_slab_rows(B, C, H, W)
             slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
-            with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT):
-                check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, None, stream),
+            # spill: pass 0 stores the raw Y and the C2R applies BN + ReLU on load (one mix instead of
+            # two, and the statistics are taken from exactly the values they normalise)
+            Y = torch.empty((B, C, H, W // 2 + 1, 2), device=dev, dtype=torch.float32) if rt.FU2D_SPILL else None
+            with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT + (8.0 * nY if Y is not None else 0.0)):
+                check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, ptr(Y), stream),
                       "ffc_fu2d_mix(pass 0)")
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
+            if Y is not None:
+                with rt.observe("fu2d_c2r", bytes=c2r_bytes):
+                    check(L.ffc_fu2d_c2r_bn(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
+                                            int(in_relu), int(residual), ptr(sc), ptr(sh), ptr(out), stream),
+                          "ffc_fu2d_c2r_bn")
+                return out
         else:
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
-        out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         if rt.FU_COLS and L.ffc_fu2d_cols_supported(C, H, W, up, int(f16)):
             # pass 1 with the inverse column FFT fused in (column-major Yc), then rows-only C2R
             Yc = torch.empty((B, C, W // 2 + 1, H, 2), device=dev, dtype=torch.float32)
             with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
                 check(L.ffc_fu2d_mix_cols(ptr(T), B, C, H, W, up, ptr(mixT), int(f16), ptr(sc), ptr(sh), ptr(Yc),
                                           stream), "ffc_fu2d_mix_cols")
-            with rt.observe("fu2d_c2r", bytes=8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)):
+            with rt.observe("fu2d_c2r", bytes=c2r_bytes):
                 check(L.ffc_fu2d_c2r_rows(ptr(Yc), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
                                           int(in_relu), int(residual), ptr(out), stream), "ffc_fu2d_c2r_rows")
             return out
@@ -163,7 +173,7 @@ class FourierUnitSN(nn.Module):
         with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
             check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 1, None, ptr(sc), ptr(sh), ptr(Y), stream),
                   "ffc_fu2d_mix(pass 1)")
-        with rt.observe("fu2d_c2r", bytes=8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)):
+        with rt.observe("fu2d_c2r", bytes=c2r_bytes):
             check(L.ffc_fu2d_c2r(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift), int(in_relu),
                                  int(residual), ptr(out), stream), "ffc_fu2d_c2r")
         return out

@@ -17,6 +17,12 @@ from .config import Config
 from .ffc import FFC_BN_ACT
 from .layers_misc import NoiseInjection, Print, Resizer, debug_print
 
+# FGenerator conv6 -> conv7 hand-off with the BN + GELU + noise pass deferred into the head's operand
+# staging (FFC_DEFER_HEAD=1).  Off by default: measured slower on MI355X -- the VALU-bound head pays
+# more for GELU on every staged element than the HBM pass it removes (B = 512: head 1.36 -> 4.05 ms,
+# pass 2.36 -> 0.78 ms; profiles/r02/ab1_*)
+DEFER_HEAD_INPUT = os.environ.get("FFC_DEFER_HEAD", "0") == "1"
+
 
 class FFCModel(nn.Module):
     def __init__(self, debug=False, inplanes=None):
@@ -178,14 +184,18 @@ class FGenerator(FFCModel):
         """FGenerator.forward up to the float image (:491-515): the eval-mode uint8 quantization of
         :516-521 is left out"""
         fake = self._noise_to_feature(z)                                     # :491-494
+        grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         for i, n in enumerate((2, 3, 4, 5, 6)):                              # :496-515
             conv = getattr(self, f"conv{n}")
+            # conv6 -> conv7: conv6's BN + GELU (+ noise) is applied by the 3x3 head as it stages its
+            # input (ffc_conv3x3_smallm_tf), no separate pass over the 128x128 activations
+            defer = n == 6 and not grad and DEFER_HEAD_INPUT
             if self.training:   # NoiseInjection fused into conv{n}'s BN + GELU pass
                 nl, ng = noises[i] if noises is not None else (None, None)
-                fake = conv.forward_noise(fake, (getattr(self, f"lcl_noise{n}"), nl),
-                                          (getattr(self, f"glb_noise{n}"), ng))
+                nzl, nzg = (getattr(self, f"lcl_noise{n}"), nl), (getattr(self, f"glb_noise{n}"), ng)
+                fake = conv.forward_deferred(fake, nzl, nzg) if defer else conv.forward_noise(fake, nzl, nzg)
             else:
-                fake = conv(fake)
+                fake = conv.forward_deferred(fake) if defer else conv(fake)
         return self.resizer(self.conv7(fake))
 
     def forward(self, z, noises=None):

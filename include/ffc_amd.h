@@ -41,7 +41,7 @@ extern "C" {
 const char* ffc_last_error(void);
 int ffc_abi_version(void);
 /* sizeof(ffc_conv_seg), (ffc_conv_phase), (ffc_conv_job), (ffc_convp_seg), (ffc_convp_phase),
- * (ffc_convp_job) -> out[0..5]; n >= 7: sizeof(ffc_bn_fold) -> out[6] */
+ * (ffc_convp_job) -> out[0..5]; n >= 7: sizeof(ffc_bn_fold) -> out[6]; n >= 8: sizeof(ffc_in_tf) -> out[7] */
 int ffc_struct_sizes(int* out, int n);
 
 /* ------------------------------------------------------------------ local branch
@@ -294,6 +294,29 @@ int ffc_conv3x3_smallm(const float* x0, int C0, const float* w0, const float* x1
                        const float* w1, const float* bias, int B, int H, int W, int M, float* out,
                        int act, float act_param, void* stream);
 
+/* Deferred input transform of one conv input segment: the producing FFC_BN_ACT's BatchNorm2d +
+ * activation and the NoiseInjection that follows it (ffc_bn_act.py:80-83 then
+ * noise_injection.py:25-32; fgan128_complete.py:509-513), applied while the consumer stages its
+ * operand instead of in a separate pass:
+ *   x' = act(x*scale[c] + shift[c]) [+ noise_w[c] * noise[b, y, x]]   (zero padding stays zero)
+ * noise: (B, 1, H, W) or NULL (then noise_w is ignored). */
+typedef struct ffc_in_tf {
+    const float* scale;
+    const float* shift;
+    int act;
+    float act_param;
+    const float* noise_w;
+    const float* noise;
+} ffc_in_tf;
+
+/* ffc_conv3x3_smallm over deferred inputs: segment s is read through tf_s (NULL: as stored).
+ * Replaces the producer's ffc_bn_act_noise_apply pass + ffc_conv3x3_smallm (the fgan128 conv6 ->
+ * conv7 hand-off); results are bit-identical to that pair. */
+int ffc_conv3x3_smallm_tf(const float* x0, int C0, const float* w0, const float* x1, int C1,
+                          const float* w1, const float* bias, int B, int H, int W, int M, float* out,
+                          int act, float act_param, const ffc_in_tf* tf0, const ffc_in_tf* tf1,
+                          void* stream);
+
 /* Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56), fused per sample:
  *   s   = in_relu ? relu(t*in_scale + in_shift) : t, nearest-upsampled by `up` (1|2)
  *         (SpectralTransform's bn1/act1 + Upsample, spectral_transform.py:44-45,79,89)
@@ -354,6 +377,8 @@ int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int up, const 
  *                 Y = Wmix Z (Z: X's interleaved Re/Im channels, :40-45);
  *                 pass 0: BN partial slab [ffc_fu2d_slab_rows()][2C] float4 {n, mean, M2}
  *                 pass 1: Y = relu(Y*bn_scale + bn_shift) -> (B, C, H, W/2+1) complex64
+ *                 pass 0 with Y != NULL also stores the raw Y (no BN) there, for ffc_fu2d_c2r_bn:
+ *                 the statistics and the values they normalise are then the same numbers
  *   ffc_fu2d_c2r: out = irfftn(Y, s=(H, W), ortho) (+ s when residual) -> (B, C, H, W)
  * wmixT as for ffc_fu_forward. */
 int ffc_fu2d_supported(int C, int H, int W, int up);
@@ -382,6 +407,11 @@ int ffc_fu2d_c2r_rows(const float* Yc, int B, int C, int H, int W, const float* 
 int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int up,
                  const float* in_scale, const float* in_shift, int in_relu, int residual, float* out,
                  void* stream);
+/* ffc_fu2d_c2r from pass 0's raw Y: relu(Y*bn_scale[2c|2c+1] + bn_shift[..]) (fourier_unity.py:46-49)
+ * applied as each plane is loaded, so the two-pass mix becomes one mix + this C2R. */
+int ffc_fu2d_c2r_bn(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                    const float* in_scale, const float* in_shift, int in_relu, int residual,
+                    const float* bn_scale, const float* bn_shift, float* out, void* stream);
 
 /* ------------------------------------------------------------------ fgan128 caller ops
  * NoiseInjection.forward(x, noise) (layers/noise_injection.py:25-32): out = x + weight[c]*noise[b]
