@@ -99,6 +99,7 @@ SIGNATURES = [
     ("ffc_conv_pack", c_int, [ctypes.POINTER(ConvJob), ctypes.POINTER(c_void_p), ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_void_p),
                               c_void_p, c_void_p, c_void_p]),
+    ("ffc_bn_reduce_ws_doubles", c_size_t, [c_int, c_int]),
     ("ffc_bn_reduce", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_bn_finalize", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                 c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),

@@ -132,17 +132,19 @@ def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: flo
     rv = ptr(bn.running_var) if bn.running_var is not None else None
     nbt = ptr(bn.num_batches_tracked) if bn.num_batches_tracked is not None else None
     if use_batch:
-        moments = torch.empty((C, 3), device=device, dtype=torch.float64)
+        # [C][3] moments + the large-slab scratch behind them (ffc_bn_reduce_ws_doubles)
+        mbuf = torch.empty(3 * C + L.ffc_bn_reduce_ws_doubles(nrows, C), device=device, dtype=torch.float64)
+        moments = mbuf[:3 * C].view(C, 3)
         grp = _sync_group()
         if grp is None:
             with observe("bn_stats"):
-                check(L.ffc_bn_reduce_finalize(ptr(slab), nrows, C, ptr(moments), gamma, beta, rm, rv, nbt,
+                check(L.ffc_bn_reduce_finalize(ptr(slab), nrows, C, ptr(mbuf), gamma, beta, rm, rv, nbt,
                                                int(update), momentum, float(bn.eps), float(count_mult), ptr(scale),
                                                ptr(shift), stream), "ffc_bn_reduce_finalize")
         else:
             from .distributed import merge_moments
             with observe("bn_stats"):
-                check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(moments), stream), "ffc_bn_reduce")
+                check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(mbuf), stream), "ffc_bn_reduce")
                 merge_moments(moments, group=grp)
                 check(L.ffc_bn_finalize(ptr(moments), C, gamma, beta, rm, rv, nbt, 1, int(update), momentum,
                                         float(bn.eps), float(count_mult), ptr(scale), ptr(shift), stream),

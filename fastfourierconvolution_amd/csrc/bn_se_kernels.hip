@@ -6,6 +6,8 @@
 // SE: SELayer (layers/ffc/spectral_transform.py:12-28).
 #include "ffc_internal.h"
 
+#include <algorithm>
+
 #include <cmath>
 
 namespace {
@@ -300,10 +302,128 @@ __global__ void se_fc_kernel(const float* means, int C, const float* __restrict_
     }
 }
 
+// ---- two-level reduction of large slabs (thousands of rows: the fgan128 layers at B = 512).  The
+// one-block-per-channel kernel above reads one float4 per lane from a different row (a 16-byte
+// piece of 64 cache lines per load) and runs C blocks; here a block takes 16 channels x a row range
+// (lane = 16 rg + oc: every load is 4 rows x 256 contiguous bytes) and ~512 blocks cover the slab,
+// writing fp64 partials {n, sum, sumsq} to the scratch behind `moments`; the second kernel merges the
+// S partials of a channel in a fixed order (lane-strided sums, one shuffle tree) and finalizes.
+constexpr int RED2_MIN_ROWS = 1024;
+
+__global__ __launch_bounds__(256) void bn_partial16_kernel(const float4* __restrict__ slab, int nrows, int C, int S,
+                                                           double* __restrict__ ws) {
+    const int cg = blockIdx.x, sp = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int oc = lane & 15, rgb = wave * 4 + (lane >> 4);   // 16 row groups per block
+    const int c = cg * 16 + oc;
+    const int cc = c < C ? c : C - 1;
+    const int r_lo = (int)((long long)sp * nrows / S), r_hi = (int)((long long)(sp + 1) * nrows / S);
+    double n = 0.0, s = 0.0, q = 0.0;
+    int r = r_lo + rgb;
+    for (; r + 48 < r_hi; r += 64) {   // four rows in flight per lane
+        float4 e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = slab[(size_t)(r + 16 * u) * C + cc];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double en = e[u].x, em = e[u].y;
+            n += en;
+            s += en * em;
+            q += (double)e[u].z + en * em * em;
+        }
+    }
+    for (; r < r_hi; r += 16) {
+        const float4 e = slab[(size_t)r * C + cc];
+        const double en = e.x, em = e.y;
+        n += en;
+        s += en * em;
+        q += (double)e.z + en * em * em;
+    }
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {
+        n += __shfl_xor(n, m, 64);
+        s += __shfl_xor(s, m, 64);
+        q += __shfl_xor(q, m, 64);
+    }
+    __shared__ double sh[4][16][3];
+    if (lane < 16) {
+        sh[wave][oc][0] = n;
+        sh[wave][oc][1] = s;
+        sh[wave][oc][2] = q;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16 && c < C) {
+        double m3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) m3[i] += sh[w][threadIdx.x][i];
+        double* d = ws + ((size_t)sp * C + c) * 3;
+        d[0] = m3[0];
+        d[1] = m3[1];
+        d[2] = m3[2];
+    }
+}
+
+// one wave per channel: the S partials in a fixed order -> moments (+ finalize)
+__global__ __launch_bounds__(64) void bn_merge_kernel(const double* __restrict__ ws, int S, int C, double* moments,
+                                                      int finalize, FinalizeArgs a) {
+    const int c = blockIdx.x, lane = threadIdx.x;
+    FinalizeIn in = {};
+    if (finalize && lane == 0) in = finalize_load(c, a);
+    double n = 0.0, s = 0.0, q = 0.0;
+    for (int sp = lane; sp < S; sp += 64) {
+        const double* d = ws + ((size_t)sp * C + c) * 3;
+        n += d[0];
+        s += d[1];
+        q += d[2];
+    }
+    n = wave_sum_f64(n);
+    s = wave_sum_f64(s);
+    q = wave_sum_f64(q);
+    if (lane == 0) {
+        double* m = moments + 3 * c;
+        m[0] = n;
+        m[1] = s;
+        m[2] = q;
+        if (finalize) {
+            const double m3[3] = {n, s, q};
+            finalize_channel(m3, c, a, in);
+            if (a.bump_here && c == 0) *a.nbt += 1;
+        }
+    }
+}
+
+int red2_splits(int nrows, int C) {
+    if (nrows < RED2_MIN_ROWS) return 0;
+    const int ncg = (C + 15) / 16;
+    return std::max(1, std::min(nrows / 64, (512 + ncg - 1) / ncg));
+}
+
 }  // namespace
+
+extern "C" size_t ffc_bn_reduce_ws_doubles(int nrows, int C) {
+    if (nrows <= 0 || C <= 0) return 0;
+    return (size_t)red2_splits(nrows, C) * (size_t)C * 3;
+}
+
+// large slabs: partials into the scratch behind moments, then the merge (finalize when fa != null)
+static void bn_reduce2(const float* slab, int nrows, int C, double* moments, const FinalizeArgs* fa,
+                       hipStream_t stream) {
+    const int S = red2_splits(nrows, C);
+    double* ws = moments + 3 * (size_t)C;
+    hipLaunchKernelGGL(bn_partial16_kernel, dim3((C + 15) / 16, S), dim3(256), 0, stream,
+                       reinterpret_cast<const float4*>(slab), nrows, C, S, ws);
+    FinalizeArgs a = fa ? *fa : FinalizeArgs{};
+    hipLaunchKernelGGL(bn_merge_kernel, dim3(C), dim3(64), 0, stream, ws, S, C, moments, fa ? 1 : 0, a);
+}
 
 extern "C" int ffc_bn_reduce(const float* slab, int nrows, int C, double* moments, void* stream) {
     FFC_CHECK_ARG(slab && moments && nrows > 0 && C > 0, "ffc_bn_reduce: bad args");
+    if (red2_splits(nrows, C)) {
+        bn_reduce2(slab, nrows, C, moments, nullptr, (hipStream_t)stream);
+        return ffc::launch_status("ffc_bn_reduce");
+    }
     hipLaunchKernelGGL(bn_reduce_kernel, dim3(C), dim3(RED_THREADS), 0, (hipStream_t)stream,
                        reinterpret_cast<const float4*>(slab), nrows, C, moments);
     return ffc::launch_status("ffc_bn_reduce");
@@ -357,8 +477,11 @@ extern "C" int ffc_bn_reduce_finalize(const float* slab, int nrows, int C, doubl
                   "ffc_bn_reduce_finalize: update needs running buffers");
     FinalizeArgs a = make_finalize(gamma, beta, running_mean, running_var, num_batches_tracked, 1, update_running,
                                    momentum, eps, count_mult, scale, shift);
-    hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(C), dim3(RED_THREADS), 0, (hipStream_t)stream,
-                       reinterpret_cast<const float4*>(slab), nrows, C, moments, a);
+    if (red2_splits(nrows, C))
+        bn_reduce2(slab, nrows, C, moments, &a, (hipStream_t)stream);
+    else
+        hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(C), dim3(RED_THREADS), 0, (hipStream_t)stream,
+                           reinterpret_cast<const float4*>(slab), nrows, C, moments, a);
     if (update_running && !a.bump_here)
         hipLaunchKernelGGL(bn_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, num_batches_tracked);
     return ffc::launch_status("ffc_bn_reduce_finalize");

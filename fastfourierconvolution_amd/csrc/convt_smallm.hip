@@ -26,6 +26,21 @@ namespace {
 
 constexpr int SM_THREADS = 512;   // conv3x3_smallm_kernel: two halves of 256
 
+// exact GELU x * Phi(x) (nn.GELU(approximate='none')) with erf from Abramowitz & Stegun 7.1.26
+// (|erf error| <= 1.5e-7, so |GELU error| <= 0.75e-7 |x|): one reciprocal, one exp and five FMAs on
+// a single branch-free path
+__device__ __forceinline__ float gelu_as(float v) {
+    const float z = fabsf(v) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+    float q = fmaf(t, 1.061405429f, -1.453152027f);
+    q = fmaf(q, t, 1.421413741f);
+    q = fmaf(q, t, -0.284496736f);
+    q = fmaf(q, t, 0.254829592f);
+    const float e = q * t * __expf(-z * z);    // erfc(z)
+    const float h = 0.5f * v * e;
+    return v >= 0.0f ? v - h : h;
+}
+
 struct SmallMArgs {
     const float* x[2];
     const float* w[2];   // Conv2d (M, C_s, 3, 3) weights (conv3x3_smallm_kernel)
@@ -69,8 +84,20 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 // MM output channels: pairs (m, m+1) run as v_pk_fma_f32, one input value against the two
 // channels' weights (LDS weight layout [channel][tap][m 0..3]); an odd last channel is scalar.
-template <int MM, bool VEC>   // VEC: IW % 4 == 0, every float4 group wholly inside or outside a row
-__global__ __launch_bounds__(CT_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void convt_smallm_kernel(SmallMArgs a) {
+// TR_ / NQ_: input tile rows and channel quarters.  The default 16 x 4 (512 threads) tiles large
+// batches; 8 x 8 (same 512 threads, half the rows, the channels split 8 ways) doubles the workgroups
+// when the grid would leave CUs idle (the small per-rank batches of strong scaling).
+template <int MM, bool VEC, int TR_ = CT_TR, int NQ_ = CT_NQ>   // VEC: IW % 4 == 0 (whole float4 groups)
+__global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgpu_waves_per_eu(4))) void convt_smallm_kernel(SmallMArgs a) {
+    constexpr int CT_TR = TR_, CT_NQ = NQ_;
+    constexpr int CT_QT = (CT_TT / 2) * (CT_TR / 2);
+    constexpr int CT_PR = CT_TR + 2;
+    constexpr int CT_G = CT_PR * (CT_PS / 4);
+    constexpr int CT_GT = (CT_CPQ * CT_G + CT_QT - 1) / CT_QT;
+    constexpr int CT_PB = CT_PR * CT_PS;
+    constexpr int CT_THREADS = CT_QT * CT_NQ;
+    constexpr int CT_WOFF = 2 * CT_NQ * CT_CPQ * CT_PB;
+    static_assert(CT_QT % 64 == 0 && CT_QT * 16 * 4 <= CT_WOFF, "quarters of whole waves; combine area fits");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x / CT_QT), tid = threadIdx.x % CT_QT;
     int bid = blockIdx.x;
@@ -285,8 +312,8 @@ constexpr int CMAX3 = 256;                  // channels (both segments) whose we
 
 // TF: each segment is read through its deferred transform a.tf[s] (ffc_in_tf): the producer's
 // BN + activation + NoiseInjection applied as the patch goes to LDS, on in-image groups only (the
-// zero padding belongs to the transformed tensor).  Same expression as bn_act_plane_kernel, so the
-// result is bit-identical to the separate pass; the noise float4 rides with the patch loads.
+// zero padding belongs to the transformed tensor).  The head is VALU-bound, so GELU uses the
+// branch-free gelu_as below instead of erff (whose two ranges diverge within a wave).
 template <int MM, bool TF>
 __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -326,11 +353,10 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
         return n < G3 && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
     };
-    auto load = [&](int ci, float4 (&r)[GT3], float4 (&nz)[TF ? GT3 : 1]) {
+    auto load = [&](int ci, float4 (&r)[GT3]) {
         const int s = ci < a.C[0] ? 0 : 1;
         const int c = s == 0 ? ci : ci - a.C[0];
         const float* x = a.x[s] + ((size_t)b * a.C[s] + c) * a.IH * a.IW;
-        const float* npl = TF && a.tf[s].noise ? a.tf[s].noise + (size_t)b * a.IH * a.IW : nullptr;
 #pragma unroll
         for (int j = 0; j < GT3; ++j) {
             const int n = j * 256 + tid;
@@ -338,36 +364,52 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
             const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
             r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             if (inimg(j)) r[j] = *reinterpret_cast<const float4*>(x + (size_t)iy * a.IW + ix);
-            if constexpr (TF) {
-                nz[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (npl && inimg(j)) nz[j] = *reinterpret_cast<const float4*>(npl + (size_t)iy * a.IW + ix);
-            }
         }
     };
-    auto put = [&](float* dst, float4 (&r)[GT3], const float4 (&nz)[TF ? GT3 : 1], int ci) {
+    // TF: this thread's noise float4s sit at the same patch positions for every channel of a segment,
+    // so they are loaded once per segment (each half switches segment once)
+    float4 nzr[TF ? GT3 : 1];
+    int nz_seg = -1;
+    auto put = [&](float* dst, float4 (&r)[GT3], int ci) {
         if constexpr (TF) {
             const int s = ci < a.C[0] ? 0 : 1;
             const int c = s == 0 ? ci : ci - a.C[0];
             const ffc_in_tf& t = a.tf[s];
+            if (s != nz_seg) {
+                const float* npl = t.noise ? t.noise + (size_t)b * a.IH * a.IW : nullptr;
+#pragma unroll
+                for (int j = 0; j < GT3; ++j) {
+                    const int n = j * 256 + tid;
+                    const int g = n % (S3 / 4), pr = n / (S3 / 4);
+                    const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
+                    nzr[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    if (npl && inimg(j)) nzr[j] = *reinterpret_cast<const float4*>(npl + (size_t)iy * a.IW + ix);
+                }
+                nz_seg = s;
+            }
             if (t.scale) {
                 const float sc = t.scale[c], sh = t.shift[c];
                 const float nw = t.noise ? t.noise_w[c] : 0.0f;
                 const int act = t.act;
                 const float p = t.act_param;
+                auto tf4 = [&](auto actf) {
 #pragma unroll
-                for (int j = 0; j < GT3; ++j) {
-                    if (!inimg(j)) continue;
-                    float4 v = r[j];
-                    v = make_float4(ffc::apply_act(fmaf(v.x, sc, sh), act, p), ffc::apply_act(fmaf(v.y, sc, sh), act, p),
-                                    ffc::apply_act(fmaf(v.z, sc, sh), act, p), ffc::apply_act(fmaf(v.w, sc, sh), act, p));
-                    if (t.noise) {
-                        v.x = fmaf(nw, nz[j].x, v.x);
-                        v.y = fmaf(nw, nz[j].y, v.y);
-                        v.z = fmaf(nw, nz[j].z, v.z);
-                        v.w = fmaf(nw, nz[j].w, v.w);
+                    for (int j = 0; j < GT3; ++j) {
+                        if (!inimg(j)) continue;
+                        float4 v = r[j];
+                        v = make_float4(actf(fmaf(v.x, sc, sh)), actf(fmaf(v.y, sc, sh)), actf(fmaf(v.z, sc, sh)),
+                                        actf(fmaf(v.w, sc, sh)));
+                        v.x = fmaf(nw, nzr[j].x, v.x);   // nzr is zero without noise
+                        v.y = fmaf(nw, nzr[j].y, v.y);
+                        v.z = fmaf(nw, nzr[j].z, v.z);
+                        v.w = fmaf(nw, nzr[j].w, v.w);
+                        r[j] = v;
                     }
-                    r[j] = v;
-                }
+                };
+                if (act == FFC_ACT_GELU)
+                    tf4([](float v) { return gelu_as(v); });
+                else
+                    tf4([act, p](float v) { return ffc::apply_act(v, act, p); });
             }
         }
 #pragma unroll
@@ -425,17 +467,16 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
     // one channel of prefetch in registers: channel k+1's loads are in flight under channel k's FMAs
     // (a second register set measured slower: 196 VGPRs, same occupancy)
     float4 r[GT3];
-    float4 nzr[TF ? GT3 : 1];
     if (half < nchunks) {
-        load(half, r, nzr);
-        put(buf(0), r, nzr, half);
+        load(half, r);
+        put(buf(0), r, half);
     }
     __syncthreads();
     for (int k = 0; k < nsteps; ++k) {
         const int cn = 2 * (k + 1) + half;
-        if (cn < nchunks) load(cn, r, nzr);
+        if (cn < nchunks) load(cn, r);
         compute(k);
-        if (cn < nchunks) put(buf(k + 1), r, nzr, cn);
+        if (cn < nchunks) put(buf(k + 1), r, cn);
         __syncthreads();
     }
     // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
@@ -540,32 +581,40 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     a.IH = IH;
     a.IW = IW;
     a.M = M;
-    a.nty = (IH + CT_TR - 1) / CT_TR;
+    // fewer workgroups than CUs with 16-row tiles: 8-row tiles over 8 channel quarters
+    const bool small = (long long)B * ((IH + CT_TR - 1) / CT_TR) * ((IW + CT_TT - 1) / CT_TT) < 256 && IH > 8;
+    const int tr = small ? 8 : CT_TR, nq = small ? 8 : CT_NQ;
+    a.nty = (IH + tr - 1) / tr;
     a.ntx = (IW + CT_TT - 1) / CT_TT;
     a.act = act;
     a.act_param = act_param;
 
-    const size_t lds = ((size_t)CT_WOFF + (size_t)(C0 + (x1 ? C1 : 0)) * 64) * sizeof(float);
+    const size_t woff = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PS;
+    const size_t lds = (woff + (size_t)(C0 + (x1 ? C1 : 0)) * 64) * sizeof(float);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
     typedef void (*CtKernel)(SmallMArgs);
-    static const CtKernel kernels[2][4] = {
-        {convt_smallm_kernel<1, false>, convt_smallm_kernel<2, false>, convt_smallm_kernel<3, false>,
-         convt_smallm_kernel<4, false>},
-        {convt_smallm_kernel<1, true>, convt_smallm_kernel<2, true>, convt_smallm_kernel<3, true>,
-         convt_smallm_kernel<4, true>}};
+    static const CtKernel kernels[2][2][4] = {
+        {{convt_smallm_kernel<1, false>, convt_smallm_kernel<2, false>, convt_smallm_kernel<3, false>,
+          convt_smallm_kernel<4, false>},
+         {convt_smallm_kernel<1, true>, convt_smallm_kernel<2, true>, convt_smallm_kernel<3, true>,
+          convt_smallm_kernel<4, true>}},
+        {{convt_smallm_kernel<1, false, 8, 8>, convt_smallm_kernel<2, false, 8, 8>, convt_smallm_kernel<3, false, 8, 8>,
+          convt_smallm_kernel<4, false, 8, 8>},
+         {convt_smallm_kernel<1, true, 8, 8>, convt_smallm_kernel<2, true, 8, 8>, convt_smallm_kernel<3, true, 8, 8>,
+          convt_smallm_kernel<4, true, 8, 8>}}};
     const int vec = IW % 4 == 0 ? 1 : 0;
-    auto k = kernels[vec][M - 1];
-    static bool raised[2][5] = {};
-    if (!raised[vec][M]) {
+    auto k = kernels[small][vec][M - 1];
+    static bool raised[2][2][5] = {};
+    if (!raised[small][vec][M]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) {
             ffc::set_error("ffc_convt_k4s2_smallm: hipFuncSetAttribute failed");
             return FFC_E_LAUNCH;
         }
-        raised[vec][M] = true;
+        raised[small][vec][M] = true;
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(CT_THREADS), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k, dim3(grid), dim3((CT_TT / 2) * (tr / 2) * nq), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_convt_k4s2_smallm");
 }
 

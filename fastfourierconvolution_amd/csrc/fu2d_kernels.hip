@@ -293,9 +293,28 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     }
     __syncthreads();
 
-    // 2. inverse columns (length H)
+    // 2. inverse columns (length H).  The row C2R keeps only Re of columns 0 and W/2 after this pass,
+    //    and Re(IFFT(a)) = IFFT(a_h) with a_h[k] = (a[k] + conj(a[-k])) / 2 (real), so those two
+    //    columns run as ONE complex IFFT of z = a_h + i b_h placed in the pad column WP: W/2 lines
+    //    instead of W/2 + 1 (whole rounds of the column pass: 128^2 3 -> 2, 64^2 2 -> 1).
+    static_assert(ZS > WP, "pad column for the packed DC / Nyquist column");
+    for (int r = tid; r < H; r += FU2_THREADS) {
+        const int rm = (H - r) & (H - 1);
+        const float2 a0 = Z[r * ZS], a1 = Z[rm * ZS], b0 = Z[r * ZS + W / 2], b1 = Z[rm * ZS + W / 2];
+        const float ahx = 0.5f * (a0.x + a1.x), ahy = 0.5f * (a0.y - a1.y);
+        const float bhx = 0.5f * (b0.x + b1.x), bhy = 0.5f * (b0.y - b1.y);
+        Z[r * ZS + WP] = make_float2(ahx - bhy, ahy + bhx);
+    }
+    __syncthreads();
 #ifndef FFC_C2R_SKIP_COL   // timing probes only (tools/build_variant.sh): results are wrong without it
-    column_pass<H, true>(Z, ZS, WP, tid);
+    {
+        constexpr int N1c = Split<H>::N1, LPR = FU2_THREADS / N1c;
+        const int jj = tid % N1c;
+        for (int l0 = 0; l0 < W / 2; l0 += LPR) {
+            const int l = l0 + tid / N1c;
+            if (l < W / 2) line_fft<H, true>(Z + (l == 0 ? WP : l), ZS, jj);
+        }
+    }
 #endif
     __syncthreads();
 
@@ -319,13 +338,13 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                 for (int m = 0; m < N2; ++m) {
                     const int k = jj + N1 * m;
                     float2 A, B;
-                    if (k <= W / 2) {
+                    if (k == 0 || k == W / 2) {   // Re parts from the packed column (step 2)
+                        const float2 za = ra[WP], zb = rb[WP];
+                        A = make_float2(k == 0 ? za.x : za.y, 0.0f);
+                        B = make_float2(k == 0 ? zb.x : zb.y, 0.0f);
+                    } else if (k < W / 2) {
                         A = ra[k];
                         B = rb[k];
-                        if (k == 0 || k == W / 2) {
-                            A.y = 0.0f;
-                            B.y = 0.0f;
-                        }
                     } else {
                         A = ra[W - k];
                         B = rb[W - k];

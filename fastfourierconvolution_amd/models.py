@@ -18,10 +18,10 @@ from .ffc import FFC_BN_ACT
 from .layers_misc import NoiseInjection, Print, Resizer, debug_print
 
 # FGenerator conv6 -> conv7 hand-off with the BN + GELU + noise pass deferred into the head's operand
-# staging (FFC_DEFER_HEAD=1).  Off by default: measured slower on MI355X -- the VALU-bound head pays
-# more for GELU on every staged element than the HBM pass it removes (B = 512: head 1.36 -> 4.05 ms,
-# pass 2.36 -> 0.78 ms; profiles/r02/ab1_*)
-DEFER_HEAD_INPUT = os.environ.get("FFC_DEFER_HEAD", "0") == "1"
+# staging (FFC_DEFER_HEAD=0: the separate pass, for A/B runs).  The head is VALU-bound, so the
+# deferred GELU uses a branch-free erf: B = 512 head 1.36 -> 2.46 ms, BN/act/noise pass 2.36 -> 0.79 ms,
+# step 18.11 -> 17.61 ms (with erff the head took 4.05 ms: profiles/r02/ab1, s4)
+DEFER_HEAD_INPUT = os.environ.get("FFC_DEFER_HEAD", "1") != "0"
 
 
 class FFCModel(nn.Module):

@@ -228,7 +228,11 @@ int ffc_dense_forward(const float* A, const float* Wt, const float* bias, int B,
  * num_batches_tracked += 1, momentum<0 means cumulative average; eval: running stats).
  * Used for SpectralTransform.bn1 (spectral_transform.py:57,89), FourierUnitSN.bn
  * (fourier_unity.py:28,49) and FFC_BN_ACT.bn_l/bn_g (ffc_bn_act.py:49-60,73-81). */
-/* merge a partial slab [nrows][C] float4 {n, mean, M2} into moments[C][3] = {n, sum, sumsq} (fp64) */
+/* merge a partial slab [nrows][C] float4 {n, mean, M2} into moments[C][3] = {n, sum, sumsq} (fp64).
+ * ffc_bn_reduce and ffc_bn_reduce_finalize need ffc_bn_reduce_ws_doubles(nrows, C) more doubles of
+ * scratch right behind moments[C][3] (nonzero for large slabs, >= 1024 rows, which are merged in two
+ * coalesced launches: 16-channel x row-range partials, then a fixed-order merge per channel). */
+size_t ffc_bn_reduce_ws_doubles(int nrows, int C);
 int ffc_bn_reduce(const float* slab, int nrows, int C, double* moments, void* stream);
 /* moments (possibly all-reduced across ranks) -> scale/shift; updates running stats */
 int ffc_bn_finalize(const double* moments, int C, const float* gamma, const float* beta,

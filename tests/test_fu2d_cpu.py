@@ -124,3 +124,24 @@ def test_upsample_identity(n, up):
     s = np.repeat(np.repeat(t, up, 0), up, 1)
     np.testing.assert_allclose(mix_rebuild(np.fft.rfft2(t), n, n, up), np.fft.rfft2(s, norm="ortho"),
                                rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("H", [16, 32, 64, 128])
+def test_c2r_packed_dc_nyquist_columns(H):
+    """fu2d_c2r_kernel step 2: columns 0 and W/2 (whose Im the row C2R drops after the column IFFT) run
+    as ONE complex IFFT of z = a_h + i b_h, a_h[k] = (a[k] + conj(a[-k])) / 2 -- numpy emulation
+    against irfftn(Y, s=(H, W)) (torch's C2R semantics ignore Im of bins 0 and W/2)"""
+    W = H
+    rng = np.random.default_rng(H)
+    Y = rng.standard_normal((H, W // 2 + 1)) + 1j * rng.standard_normal((H, W // 2 + 1))
+    cols = np.fft.ifft(Y, axis=0) * H                      # unnormalised inverse column FFT
+    a, b = Y[:, 0], Y[:, W // 2]
+    neg = (-np.arange(H)) % H
+    z = 0.5 * (a + np.conj(a[neg])) + 1j * 0.5 * (b + np.conj(b[neg]))
+    zc = np.fft.ifft(z) * H
+    cols[:, 0] = zc.real
+    cols[:, W // 2] = zc.imag                                # only the Re parts are used below
+    rows = np.fft.irfft(cols.real * (np.arange(W // 2 + 1) % (W // 2) == 0) + cols * (np.arange(W // 2 + 1) % (W // 2) != 0),
+                        n=W, axis=1) * W
+    ref = np.fft.irfftn(Y, s=(H, W)) * H * W
+    np.testing.assert_allclose(rows, ref, rtol=0, atol=1e-9 * np.abs(ref).max())

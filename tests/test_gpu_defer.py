@@ -2,9 +2,10 @@
 hand-off where the 3x3 head applies conv6's BatchNorm2d + GELU + noise (ffc_bn_act.py:80-83,
 noise_injection.py:25-32, fgan128_complete.py:509-514) while staging its input.
 
-The deferred path evaluates the same expression as the separate pass, so the tests ask for
-bit-identical results against that pass (and the fp64 oracle through test_gpu_fu2d.py's
-fgan128 stack tests, which run the deferred path by default)."""
+The deferred path evaluates the same BN / noise expression as the separate pass; GELU uses a
+branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7) instead of erff, so the tests
+ask for <= 2e-6 normwise against that pass (bit-identical running statistics) and <= 1e-4
+against the fp64 oracle."""
 import contextlib
 import io
 
@@ -43,9 +44,9 @@ def _sd64(mod):
 
 @pytest.mark.parametrize("train", [True, False])
 @pytest.mark.parametrize("cin,H,W,B", [(32, 32, 32, 3), (16, 16, 16, 2), (128, 64, 64, 2)])
-def test_deferred_head_bit_identical(train, cin, H, W, B):
+def test_deferred_head_matches_separate_pass(train, cin, H, W, B):
     """producer FFC_BN_ACT(cin, cin, 3, 0.5, 0.5, BN, GELU) + NoiseInjection on both branches, consumer
-    FFC_BN_ACT(cin, 3, 3, 0.5, 0, Tanh): deferred == separate pass, bit for bit; and vs the oracle"""
+    FFC_BN_ACT(cin, 3, 3, 0.5, 0, Tanh): deferred vs the separate pass and vs the oracle"""
     import fastfourierconvolution_amd as F
     from fastfourierconvolution_amd import _runtime as rt
     gen = torch.Generator().manual_seed(cin + H + train)
@@ -86,7 +87,7 @@ def test_deferred_head_bit_identical(train, cin, H, W, B):
         torch.cuda.synchronize()
     summ = obs.summary()
     assert og == 0 and "conv3_smallm" in summ and "bn_act_noise" not in summ and "bn_act" not in summ
-    assert torch.equal(out, ref_out)
+    assert normwise_err(out.cpu(), ref_out.cpu()) <= 2e-6
     for k, v in prod.state_dict().items():   # running stats advanced exactly as on the eager path
         assert torch.equal(v, after[k]), k
     cfg_p = dict(in_channels=cin, out_channels=cin, kernel_size=3, ratio_gin=0.5, ratio_gout=0.5, stride=1,
@@ -122,7 +123,7 @@ def test_pending_materializes_for_other_consumers():
 
 @pytest.mark.parametrize("train", [True, False])
 def test_fgan128_deferred_head_matches_eager(train):
-    """FGenerator.forward_float with conv6 -> conv7 deferred (default) == the separate-pass path, bit for bit"""
+    """FGenerator.forward_float with conv6 -> conv7 deferred == the separate-pass path (GELU erf within 2e-6)"""
     import fastfourierconvolution_amd as F
     from fastfourierconvolution_amd import models
     gen = torch.Generator().manual_seed(11)
@@ -144,7 +145,7 @@ def test_fgan128_deferred_head_matches_eager(train):
             b = g.forward_float(z, noises if train else None)
     finally:
         models.DEFER_HEAD_INPUT = old
-    assert torch.equal(a, b)
+    assert normwise_err(a.cpu(), b.cpu()) <= 2e-6
 
 
 def test_conv3x3_smallm_tf_abi_validation():
