@@ -420,13 +420,16 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
     };
     auto buf = [&](int k) { return pbuf + ((k & 1) * 2 + half) * PB3; };
 
-    float acc[MM][4][4];
+    // accumulators as column pairs (j, j+1): the FMAs run as v_pk_fma_f32 (two output columns against
+    // one broadcast weight), half the VALU issue of scalar FMAs
+    f2 acc2[MM][4][2];
 #pragma unroll
     for (int m = 0; m < MM; ++m)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[m][i][j] = 0.0f;
+            for (int j = 0; j < 2; ++j) acc2[m][i][j] = f2{0.0f, 0.0f};
+#define ACC(m, i, j) (((j) & 1) ? acc2[m][i][(j) >> 1].y : acc2[m][i][(j) >> 1].x)
 
     const int nsteps = (nchunks + 1) / 2;   // half h takes chunks 2k + h (its k-th channel)
     auto compute = [&](int k) {
@@ -454,13 +457,17 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float s2 = acc[m][i][j];
+                for (int jp = 0; jp < 2; ++jp) {
+                    f2 s2 = acc2[m][i][jp];
 #pragma unroll
                     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-                        for (int kx = 0; kx < 3; ++kx) s2 = fmaf(v[i + ky][j + kx], k9[ky * 3 + kx], s2);
-                    acc[m][i][j] = s2;
+                        for (int kx = 0; kx < 3; ++kx) {
+                            const float w = k9[ky * 3 + kx];
+                            s2 = __builtin_elementwise_fma(f2{v[i + ky][2 * jp + kx], v[i + ky][2 * jp + kx + 1]},
+                                                           f2{w, w}, s2);
+                        }
+                    acc2[m][i][jp] = s2;
                 }
         }
     };
@@ -487,7 +494,7 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * 256 + tid] = acc[m][i][j];
+                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * 256 + tid] = ACC(m, i, j);
     }
     __syncthreads();
     if (half == 1) return;
@@ -496,7 +503,9 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[m][i][j] += part[((m * 4 + i) * 4 + j) * 256 + tid];
+            for (int jp = 0; jp < 2; ++jp)
+                acc2[m][i][jp] += f2{part[((m * 4 + i) * 4 + 2 * jp) * 256 + tid],
+                                     part[((m * 4 + i) * 4 + 2 * jp + 1) * 256 + tid]};
     const int oy0 = y0 + qy, ox0 = x0 + qx;
     const bool xin = ox0 + 3 < a.IW;
     auto store = [&](auto actf) {
@@ -510,12 +519,12 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
                 if (oy >= a.IH) continue;
                 float* row = a.out + (((size_t)b * M + m) * a.IH + oy) * a.IW + ox0;
                 if (xin) {
-                    *reinterpret_cast<float4*>(row) = make_float4(actf(acc[m][i][0] + bv), actf(acc[m][i][1] + bv),
-                                                                  actf(acc[m][i][2] + bv), actf(acc[m][i][3] + bv));
+                    *reinterpret_cast<float4*>(row) = make_float4(actf(ACC(m, i, 0) + bv), actf(ACC(m, i, 1) + bv),
+                                                                  actf(ACC(m, i, 2) + bv), actf(ACC(m, i, 3) + bv));
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (ox0 + j < a.IW) row[j] = actf(acc[m][i][j] + bv);
+                        if (ox0 + j < a.IW) row[j] = actf(ACC(m, i, j) + bv);
                 }
             }
         }
@@ -530,6 +539,7 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         default: store([](float v) { return v; }); break;
     }
 }
+#undef ACC
 
 }  // namespace
 
