@@ -509,6 +509,67 @@ class _Up2Fn(torch.autograd.Function):
         return _pool2(dy.contiguous(), 1.0)
 
 
+# --------------------------------------------------------------------------- NoiseInjection, Linear
+class _NoiseFn(torch.autograd.Function):
+    """NoiseInjection.forward (layers/noise_injection.py:25-32): x + weight * noise; backward
+    dx = g, dweight[c] = sum g[:, c] * noise (ffc_noise_wgrad)"""
+
+    @staticmethod
+    def forward(ctx, x, weight, noise):
+        B, C, H, W = x.shape
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        with rt.observe("noise_inject", bytes=8.0 * x.numel() + 4.0 * noise.numel()):
+            check(rt.lib().ffc_noise_inject(ptr(x), ptr(weight.detach().contiguous()), ptr(noise), ptr(out), B, C,
+                                            H * W, _stream(x)), "ffc_noise_inject")
+        ctx.save_for_backward(noise)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (noise,) = ctx.saved_tensors
+        g = g.contiguous()
+        dw = None
+        if ctx.needs_input_grad[1]:
+            B, C, H, W = g.shape
+            dw = torch.empty(C, device=g.device, dtype=torch.float32)
+            check(rt.lib().ffc_noise_wgrad(ptr(g), ptr(noise), B, C, H * W, ptr(dw), _stream(g)), "ffc_noise_wgrad")
+            dw = dw.view(1, C, 1, 1)
+        return (g if ctx.needs_input_grad[0] else None), dw, None
+
+
+def noise_inject(mod, x, noise=None):
+    """NoiseInjection ``mod`` applied to x on the training path (noise drawn with normal_() as the
+    reference does when not given)"""
+    B, C, H, W = x.shape
+    if noise is None:
+        noise = x.new_empty(B, 1, H, W).normal_()
+    noise = rt.require(noise, "noise").contiguous()
+    if tuple(noise.shape) != (B, 1, H, W) or (H * W) % 4:
+        raise NotImplementedError("NoiseInjection: noise must be (B, 1, H, W) with H*W % 4 == 0")
+    if mod.weight.numel() != C:
+        raise RuntimeError(f"NoiseInjection has {mod.weight.numel()} channels, tensor has {C}")
+    return _NoiseFn.apply(x, mod.weight, noise)
+
+
+class _LinearAs1x1:
+    """nn.Linear(K, N) seen by conv_layer as a 1x1 Conv2d on a 1x1 input: weight (N, K, 1, 1) is a view
+    of the Linear's weight, so its gradient flows back to the parameter"""
+
+    def __init__(self, lin: nn.Linear):
+        self.weight = lin.weight.view(lin.out_features, lin.in_features, 1, 1)
+        self.bias = lin.bias
+        self.out_channels = lin.out_features
+
+
+def linear(owner_cache, lin: nn.Linear, z):
+    """nn.Linear forward + backward (fgan128_complete.py:453-455 noise_to_feature) -> (B, N)"""
+    B, K = z.shape
+    (y,) = conv_layer(owner_cache, B, [(lin.out_features, 0, 0.0)], [(0, 0, _plan.Seg("pw", K, 1, 1), _LinearAs1x1(lin))],
+                      [z.reshape(B, K, 1, 1)])
+    return y.reshape(B, lin.out_features)
+
+
 # --------------------------------------------------------------------------- FFTs
 def _rfft2(x, iscale):
     B, C, H, W = x.shape
@@ -564,8 +625,8 @@ def fourier_unit(fu, x, residual: bool):
     if fu.mix_precision != "fp32":
         raise NotImplementedError("the training path computes the spectral mix in fp32 only (config 5's fp16 "
                                   "mix is forward-only)")
-    if H > 64 or W > 64:
-        raise NotImplementedError("training-path Fourier unit: planes up to 64x64")
+    if (H > 64 or W > 64) and not (H == W and H in (128,)):
+        raise NotImplementedError("training-path Fourier unit: planes up to 64x64, or square 128x128")
     Z = _RFFT2Fn.apply(x)
     cache = fu.__dict__.setdefault("_train_cache", {})
     seg = _plan.Seg("pw", 2 * C, H, W // 2 + 1)

@@ -140,6 +140,7 @@ SIGNATURES = [
     ("ffc_fu2d_c2r_bn", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                 c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    ("ffc_noise_wgrad", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),
     ("ffc_conv3x3_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                    c_int, c_int, c_void_p, c_int, c_float, c_void_p]),

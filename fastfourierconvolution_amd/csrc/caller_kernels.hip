@@ -34,6 +34,29 @@ __global__ void quantize_u8_kernel(const float4* __restrict__ x, unsigned int* _
     }
 }
 
+// NoiseInjection backward, weight: dw[c] = sum_{b, hw} g[b, c, hw] * noise[b, hw].  One block per
+// channel, fp64 per-thread sums over (b, hw) in a fixed stride, a fixed shuffle tree, the waves in
+// order: deterministic.
+__global__ __launch_bounds__(256) void noise_wgrad_kernel(const float4* __restrict__ g, const float4* __restrict__ noise,
+                                                          int B, int C, int HW4, float* __restrict__ dw) {
+    const int c = blockIdx.x;
+    double acc = 0.0;
+    for (int b = 0; b < B; ++b) {
+        const float4* gp = g + ((size_t)b * C + c) * HW4;
+        const float4* np = noise + (size_t)b * HW4;
+        for (int i = threadIdx.x; i < HW4; i += 256) {
+            const float4 u = gp[i], n = np[i];
+            acc += (double)u.x * n.x + (double)u.y * n.y + (double)u.z * n.z + (double)u.w * n.w;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    __shared__ double part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) dw[c] = (float)(((part[0] + part[1]) + part[2]) + part[3]);
+}
+
 int grid_for(long long n4) {
     const long long g = (n4 + 255) / 256;
     return (int)(g < 8192 ? (g > 0 ? g : 1) : 8192);
@@ -58,4 +81,12 @@ extern "C" int ffc_quantize_u8(const float* x, unsigned char* out, long long n, 
     hipLaunchKernelGGL(quantize_u8_kernel, dim3(grid_for(n4)), dim3(256), 0, (hipStream_t)stream,
                        reinterpret_cast<const float4*>(x), reinterpret_cast<unsigned int*>(out), n4);
     return ffc::launch_status("ffc_quantize_u8");
+}
+
+extern "C" int ffc_noise_wgrad(const float* g, const float* noise, int B, int C, int HW, float* dw, void* stream) {
+    FFC_CHECK_ARG(g && noise && dw, "ffc_noise_wgrad: null pointer");
+    FFC_CHECK_ARG(B > 0 && C > 0 && HW > 0 && HW % 4 == 0, "ffc_noise_wgrad: HW must be a positive multiple of 4");
+    hipLaunchKernelGGL(noise_wgrad_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(g), reinterpret_cast<const float4*>(noise), B, C, HW / 4, dw);
+    return ffc::launch_status("ffc_noise_wgrad");
 }

@@ -82,6 +82,10 @@ __device__ __forceinline__ floatx4 buf_ld4(__amdgpu_buffer_rsrc_t r, unsigned of
 
 void set_error(const std::string& msg);
 int launch_status(const char* what);  // FFC_OK or FFC_E_LAUNCH after checking hipGetLastError
+// the training path's planar 2-D real transforms on the fu2d line FFTs (fu2d_kernels.hip): square
+// power-of-two planes up to 128; return 1 when the plane is not handled there (direct DFT instead)
+int fft_planes_r2c(const float* x, int P, int H, int W, float iscale, float* Z, void* stream);
+int fft_planes_c2r(const float* Z, int P, int H, int W, float iscale, const float* addend, float* y, void* stream);
 
 #define FFC_CHECK_ARG(cond, msg)              \
     do {                                      \

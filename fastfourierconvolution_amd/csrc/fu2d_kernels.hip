@@ -141,11 +141,15 @@ struct R2cArgs {
     const float* in_shift;
     float* T;
     int C, in_relu;
+    float oscale, iscale;   // PLANAR: every bin x oscale, bins with a Hermitian mirror x iscale too
 };
 
 // ---------------------------------------------------------------- stage 1: R2C of the t planes
 // LDS: real plane R (h rows, stride w+4: conflict-free row-pair reads), complex plane Z (h x WPt).
-template <int h, int w>
+// PLANAR (the training path's ffc_rfft2_planes): T is the interleaved channel-plane layout of
+// fourier_unity.py:40-42 -- Re of plane p at T + 2p*h*WPt, Im at T + (2p+1)*h*WPt -- scaled by
+// oscale (1/sqrt(hw): rfftn ortho) and, on bins 0 < kw < w/2, iscale (2: the adjoint of irfftn).
+template <int h, int w, bool PLANAR = false>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     constexpr int WPt = w / 2 + 1;
     constexpr int ZS = zstride(WPt);
@@ -234,11 +238,23 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     column_pass<h, false>(Z, ZS, WPt, tid);
     __syncthreads();
 
-    // 4. Z -> T (contiguous h x WPt float2)
-    float2* dst = reinterpret_cast<float2*>(a.T) + (size_t)plane * h * WPt;
-    for (int i = tid; i < h * WPt; i += FU2_THREADS) {
-        const int r = i / WPt, k = i - r * WPt;
-        dst[i] = Z[r * ZS + k];
+    // 4. Z -> T (contiguous h x WPt float2, or the two planes of PLANAR)
+    if constexpr (PLANAR) {
+        float* re = a.T + (size_t)plane * 2 * h * WPt;
+        float* im = re + h * WPt;
+        for (int i = tid; i < h * WPt; i += FU2_THREADS) {
+            const int r = i / WPt, k = i - r * WPt;
+            const float sc = (k == 0 || 2 * k == w) ? a.oscale : a.oscale * a.iscale;
+            const float2 v = Z[r * ZS + k];
+            re[i] = v.x * sc;
+            im[i] = v.y * sc;
+        }
+    } else {
+        float2* dst = reinterpret_cast<float2*>(a.T) + (size_t)plane * h * WPt;
+        for (int i = tid; i < h * WPt; i += FU2_THREADS) {
+            const int r = i / WPt, k = i - r * WPt;
+            dst[i] = Z[r * ZS + k];
+        }
     }
 }
 
@@ -253,9 +269,12 @@ struct C2rArgs {
     float norm;
     const float* bn_scale;   // optional [2C]: Y is the raw mix output, relu(Y*bn_scale + bn_shift) on load
     const float* bn_shift;
+    float iscale;            // PLANAR: bins 0 < kw < W/2 x iscale (0.5: the adjoint of rfftn)
 };
 
-template <int H, int W, int UP>
+// PLANAR (the training path's ffc_irfft2_planes): Y in the interleaved channel-plane layout (Re of
+// plane p at Y + 2p*H*WP, Im at Y + (2p+1)*H*WP), interior bins x iscale; UP = 1, residual = addend.
+template <int H, int W, int UP, bool PLANAR = false>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     constexpr int WP = W / 2 + 1;
     constexpr int ZS = zstride(WP);
@@ -270,6 +289,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     //    (spilled) Y gets the FU's BN + ReLU here, the same expression as mix pass 1
     {
         const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)plane * H * WP;
+        const float* pre = a.Y + (size_t)plane * 2 * H * WP;   // PLANAR: Re plane, Im plane behind it
         const bool bn = a.bn_scale != nullptr;
         const float bsr = bn ? a.bn_scale[2 * ch] : 1.0f, bhr = bn ? a.bn_shift[2 * ch] : 0.0f;
         const float bsi = bn ? a.bn_scale[2 * ch + 1] : 1.0f, bhi = bn ? a.bn_shift[2 * ch + 1] : 0.0f;
@@ -278,7 +298,15 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int i = i0 + u * FU2_THREADS + tid;
-                if (i < H * WP) v[u] = src[i];
+                if (i < H * WP) {
+                    if constexpr (PLANAR) {
+                        const int k = i % WP;
+                        const float sc = (k == 0 || 2 * k == W) ? 1.0f : a.iscale;
+                        v[u] = make_float2(pre[i] * sc, pre[H * WP + i] * sc);
+                    } else {
+                        v[u] = src[i];
+                    }
+                }
             }
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
@@ -1079,7 +1107,7 @@ extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const fl
     FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_fu2d_r2c: plane exceeds LDS");
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c");
     if (rc) return rc;
-    R2cArgs a{t, in_scale, in_shift, T, C, in_relu};
+    R2cArgs a{t, in_scale, in_shift, T, C, in_relu, 1.0f, 1.0f};
     hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_r2c");
 }
@@ -1169,7 +1197,7 @@ static int fu2d_c2r_launch(const float* Y, int B, int C, int H, int W, const flo
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu2d_c2r: up must be 1 or 2");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
     C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
-              bn_scale, bn_shift};
+              bn_scale, bn_shift, 1.0f};
     C2rKernel k = pick_c2r(H, W, up);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [16, 128])");
     const size_t lds = c2r_lds(H, W);
@@ -1241,7 +1269,63 @@ extern "C" int ffc_fu2d_c2r_rows(const float* Yc, int B, int C, int H, int W, co
     const int RB = H < 64 ? H : 64;
     const size_t lds = (size_t)RB * zstride(W / 2 + 1) * 8;
     C2rArgs a{Yc, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
-              nullptr, nullptr};
+              nullptr, nullptr, 1.0f};
     hipLaunchKernelGGL(k, dim3(B * C * (H / RB)), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r_rows");
 }
+
+// ---- the training path's planar transforms (ffc_rfft2_planes / ffc_irfft2_planes, train_kernels.hip)
+// on the line FFTs above: square power-of-two planes 8..128 (r2c) / 16..128 (c2r); 0 = handled,
+// 1 = not supported here (the caller falls back to its direct DFT, planes <= 64).
+namespace {
+template <int N>
+R2cKernel pick_r2c_planar_n() { return fu2d_r2c_kernel<N, N, true>; }
+R2cKernel pick_r2c_planar(int H, int W) {
+    if (H != W) return nullptr;
+    switch (H) {
+        case 8: return pick_r2c_planar_n<8>();
+        case 16: return pick_r2c_planar_n<16>();
+        case 32: return pick_r2c_planar_n<32>();
+        case 64: return pick_r2c_planar_n<64>();
+        case 128: return pick_r2c_planar_n<128>();
+    }
+    return nullptr;
+}
+C2rKernel pick_c2r_planar(int H, int W) {
+    if (H != W) return nullptr;
+    switch (H) {
+        case 16: return fu2d_c2r_kernel<16, 16, 1, true>;
+        case 32: return fu2d_c2r_kernel<32, 32, 1, true>;
+        case 64: return fu2d_c2r_kernel<64, 64, 1, true>;
+        case 128: return fu2d_c2r_kernel<128, 128, 1, true>;
+    }
+    return nullptr;
+}
+}  // namespace
+
+namespace ffc {
+int fft_planes_r2c(const float* x, int P, int H, int W, float iscale, float* Z, void* stream) {
+    R2cKernel k = pick_r2c_planar(H, W);
+    if (!k) return 1;
+    const size_t lds = r2c_lds(H, W);
+    if (lds > 160 * 1024) return 1;
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_rfft2_planes");
+    if (rc) return rc;
+    R2cArgs a{x, nullptr, nullptr, Z, 1, 0, (float)(1.0 / std::sqrt((double)H * (double)W)), iscale};
+    hipLaunchKernelGGL(k, dim3(P), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return launch_status("ffc_rfft2_planes");
+}
+
+int fft_planes_c2r(const float* Z, int P, int H, int W, float iscale, const float* addend, float* y, void* stream) {
+    C2rKernel k = pick_c2r_planar(H, W);
+    if (!k) return 1;
+    const size_t lds = c2r_lds(H, W);
+    if (lds > 160 * 1024) return 1;
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_irfft2_planes");
+    if (rc) return rc;
+    C2rArgs a{Z, addend, nullptr, nullptr, y, 1, 0, addend ? 1 : 0,
+              (float)(1.0 / std::sqrt((double)H * (double)W)), nullptr, nullptr, iscale};
+    hipLaunchKernelGGL(k, dim3(P), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
+    return launch_status("ffc_irfft2_planes");
+}
+}  // namespace ffc

@@ -795,8 +795,14 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
 }
 
 extern "C" int ffc_rfft2_planes(const float* x, int P, int H, int W, float interior_scale, float* Z, void* stream) {
-    FFC_CHECK_ARG(x && Z && P > 0 && H >= 1 && W >= 2 && H <= DFT_MAXN && W <= DFT_MAXN,
-                  "ffc_rfft2_planes: planes up to 64x64");
+    FFC_CHECK_ARG(x && Z && P > 0 && H >= 1 && W >= 2, "ffc_rfft2_planes: bad args");
+    // square power-of-two planes 8..128: line FFTs (fu2d_kernels.hip); others: direct DFT up to 64
+    if (H >= 8 && H == W && (H & (H - 1)) == 0) {
+        const int rc = ffc::fft_planes_r2c(x, P, H, W, interior_scale, Z, stream);
+        if (rc != 1) return rc;
+    }
+    FFC_CHECK_ARG(H <= DFT_MAXN && W <= DFT_MAXN,
+                  "ffc_rfft2_planes: planes up to 64x64 (square powers of two up to 128x128)");
     const int npw = dft_npw(H, W);
     hipLaunchKernelGGL(rfft2_kernel, dim3((P + npw - 1) / npw), dim3(256), dft_lds(H, W, npw, false),
                        (hipStream_t)stream, x, P, H, W, npw, interior_scale, Z);
@@ -805,8 +811,13 @@ extern "C" int ffc_rfft2_planes(const float* x, int P, int H, int W, float inter
 
 extern "C" int ffc_irfft2_planes(const float* Z, int P, int H, int W, float interior_scale, const float* addend,
                                  float* y, void* stream) {
-    FFC_CHECK_ARG(Z && y && P > 0 && H >= 1 && W >= 2 && H <= DFT_MAXN && W <= DFT_MAXN,
-                  "ffc_irfft2_planes: planes up to 64x64");
+    FFC_CHECK_ARG(Z && y && P > 0 && H >= 1 && W >= 2, "ffc_irfft2_planes: bad args");
+    if (H >= 16 && H == W && (H & (H - 1)) == 0) {
+        const int rc = ffc::fft_planes_c2r(Z, P, H, W, interior_scale, addend, y, stream);
+        if (rc != 1) return rc;
+    }
+    FFC_CHECK_ARG(H <= DFT_MAXN && W <= DFT_MAXN,
+                  "ffc_irfft2_planes: planes up to 64x64 (square powers of two up to 128x128)");
     const int npw = dft_npw(H, W);
     hipLaunchKernelGGL(irfft2_kernel, dim3((P + npw - 1) / npw), dim3(256), dft_lds(H, W, npw, true),
                        (hipStream_t)stream, Z, P, H, W, npw, interior_scale, addend, y);

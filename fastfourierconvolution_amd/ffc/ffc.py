@@ -149,8 +149,6 @@ class _FFCExec:
         if y is not None:
             raise TypeError("FFC: the conditional (y) path is not supported (the reference raises in "
                             "FourierUnitSN, fourier_unity.py:46-47)")
-        if noise:
-            raise NotImplementedError("NoiseInjection on the training path")
         for t, n in ((x_l, "x_l"), (x_g, "x_g")):
             if isinstance(t, torch.Tensor):
                 rt.require(t, n)
@@ -204,6 +202,9 @@ class _FFCExec:
             ys = ag.conv_layer(self._ffc_cache(), B, outs, edges, inputs)
             for (name, act, bn), yv in zip(names, ys):
                 res[name] = ag.bn_act(bn, yv, act) if bn is not None else yv
+        for name, (mod, n) in (noise or {}).items():   # fgan128's NoiseInjection after FFC_BN_ACT
+            if isinstance(res[name], torch.Tensor):
+                res[name] = ag.noise_inject(mod, res[name], n)
         return res["l"], res["g"]
 
     def _launch_branches(self, branches, B, dev, stream, noise=None, defer=False):

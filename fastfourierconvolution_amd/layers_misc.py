@@ -67,6 +67,9 @@ class NoiseInjection(nn.Module):
         noise = rt.require(noise, "noise")
         if tuple(noise.shape) != (batch, 1, height, width) or (height * width) % 4:
             raise NotImplementedError("NoiseInjection: noise must be (B, 1, H, W) with H*W % 4 == 0")
+        from . import _autograd as ag
+        if ag.wants_grad(self, x):   # training path: weight gradient through ffc_noise_wgrad
+            return ag.noise_inject(self, x, noise)
         w = rt.require(self.weight.detach(), "weight")
         out = torch.empty_like(x)
         with rt.observe("noise_inject", bytes=8.0 * x.numel() + 4.0 * noise.numel()):

@@ -11,6 +11,7 @@ import os
 import torch
 import torch.nn as nn
 
+from . import _autograd as ag
 from . import _runtime as rt
 from ._lib import check, ptr
 from .config import Config
@@ -158,6 +159,7 @@ class FGenerator(FFCModel):
         self.conv7 = FFC_BN_ACT(ngf, 3, 3, ratio_g, 0.0, stride=1, padding=1, activation_layer=nn.Tanh,
                                 norm_layer=nn.Identity, upsampling=False, uses_noise=True, uses_sn=True)
         self._lin = {}
+        self._lin_train = {}
 
     def _noise_to_feature(self, z):
         """nn.Linear(z_size, 16*1024) (fgan128_complete.py:453-455) on the HIP dense GEMM"""
@@ -166,6 +168,8 @@ class FGenerator(FFCModel):
         if z.dim() != 2 or z.shape[1] != lin.in_features:
             raise RuntimeError(f"FGenerator: z must be (B, {lin.in_features}), got {tuple(z.shape)}")
         B = z.shape[0]
+        if ag.wants_grad(self.noise_to_feature, z):   # training path: Linear as a 1x1 conv job with autograd
+            return ag.linear(self._lin_train, lin, z).view(B, -1, self.mg, self.mg)
         w = rt.require(lin.weight.detach(), "noise_to_feature.0.weight")
         b = rt.require(lin.bias.detach(), "noise_to_feature.0.bias") if lin.bias is not None else None
         key = (w.data_ptr(), w._version)

@@ -422,6 +422,9 @@ int ffc_fu2d_c2r_bn(const float* Y, int B, int C, int H, int W, const float* t, 
  * x, out (B, C, H, W); weight (C); noise (B, 1, H, W); HW % 4 == 0; in place allowed. */
 int ffc_noise_inject(const float* x, const float* weight, const float* noise, float* out, int B, int C,
                      int HW, void* stream);
+/* NoiseInjection backward (training path): dweight[c] = sum over b, hw of dout[b, c, hw] * noise[b, hw]
+ * (dx = dout needs no kernel).  dout (B, C, H, W), noise (B, 1, H, W), HW % 4 == 0; deterministic. */
+int ffc_noise_wgrad(const float* dout, const float* noise, int B, int C, int HW, float* dweight, void* stream);
 /* eval-mode output of fgan128 FGenerator (fgan128_complete.py:516-521): out = uint8(255*(x*0.5+0.5))
  * (the reference's clamp to the tensor's own min/max is the identity); n % 4 == 0 */
 int ffc_quantize_u8(const float* x, unsigned char* out, long long n, void* stream);
@@ -475,11 +478,13 @@ int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const float* V, int N
 /* rfftn(x, dim=(-2,-1), norm="ortho") of P planes (P, H, W) into the interleaved Re/Im planes of
  * fourier_unity.py:38-42: Re of plane p at Z[2p], Im at Z[2p+1], each H x (W/2+1).  Bins with a
  * Hermitian mirror (0 < kw, 2kw != W) are multiplied by interior_scale (2: the adjoint of irfftn).
- * H, W <= 64. */
+ * Square power-of-two planes 8..128 run on the line FFTs of the staged Fourier unit; other planes
+ * (H, W <= 64) on direct DFTs. */
 int ffc_rfft2_planes(const float* x, int P, int H, int W, float interior_scale, float* Z, void* stream);
 /* irfftn(X, s=(H,W), dim=(-2,-1), norm="ortho") (fourier_unity.py:51-56) from interleaved planes,
  * Im of the kw = 0 and kw = W/2 bins ignored, mirrored bins x interior_scale (0.5: the adjoint of
- * rfftn), + addend (P, H, W) when not NULL (SpectralTransform's x + fu(x), :108). H, W <= 64. */
+ * rfftn), + addend (P, H, W) when not NULL (SpectralTransform's x + fu(x), :108).  Square
+ * power-of-two planes 16..128 on line FFTs, other planes (H, W <= 64) on direct DFTs. */
 int ffc_irfft2_planes(const float* Z, int P, int H, int W, float interior_scale, const float* addend, float* y,
                       void* stream);
 /* SELayer backward (spectral_transform.py:23-28), one workgroup per sample: dx, plus the

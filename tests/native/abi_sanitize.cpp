@@ -68,6 +68,13 @@ static void validation_paths() {
     EXPECT_INVALID(ffc_se_gate(cp, 1, 4, 4, 4, 0, nullptr, nullptr, -1, p, nullptr), "ffc_se_gate");
     EXPECT_INVALID(ffc_noise_inject(cp, cp, cp, p, 1, 4, 6, nullptr), "multiple of 4");
     EXPECT_INVALID(ffc_noise_inject(cp, nullptr, cp, p, 1, 4, 8, nullptr), "null pointer");
+    EXPECT_INVALID(ffc_noise_wgrad(cp, cp, 1, 4, 6, p, nullptr), "multiple of 4");
+    EXPECT_INVALID(ffc_noise_wgrad(nullptr, cp, 1, 4, 8, p, nullptr), "null pointer");
+    if (ffc_bn_reduce_ws_doubles(100, 64) != 0 || ffc_bn_reduce_ws_doubles(0, 64) != 0 ||
+        ffc_bn_reduce_ws_doubles(1 << 30, 1 << 12) == 0) {
+        std::fprintf(stderr, "FAIL ffc_bn_reduce_ws_doubles\n");
+        ++g_fail;
+    }
     EXPECT_INVALID(ffc_quantize_u8(cp, reinterpret_cast<unsigned char*>(p), 6, nullptr), "ffc_quantize_u8");
     // --- convolution jobs (conv_kernels.hip, convp_kernels.hip, pw_gemm.hip, dense.hip, convt_smallm.hip)
     ffc_conv_job job;
@@ -117,6 +124,13 @@ static void validation_paths() {
                    "second segment");
     EXPECT_INVALID(ffc_conv3x3_smallm(cp, 4, cp, nullptr, 0, nullptr, nullptr, 1, 8, 6, 3, p, 0, 0.f, nullptr),
                    "ffc_conv3x3_smallm");
+    {
+        const ffc_in_tf bad = {nullptr, nullptr, 0, 0.f, nullptr, nullptr};
+        EXPECT_INVALID(ffc_conv3x3_smallm_tf(cp, 4, cp, nullptr, 0, nullptr, nullptr, 1, 8, 8, 3, p, 0, 0.f, &bad,
+                                             nullptr, nullptr), "scale");
+        EXPECT_INVALID(ffc_fu2d_c2r_bn(cp, 1, 4, 32, 32, cp, 2, nullptr, nullptr, 0, 1, nullptr, nullptr, p, nullptr),
+                       "bn_scale");
+    }
     // --- spectral branch (st_prologue.hip, st_pw.hip, fu_kernels.hip, fu2d_kernels.hip)
     EXPECT_INVALID(ffc_st_prologue(cp, 1, 4096, 64, 64, 0, nullptr, nullptr, 0, cp, 4, p, p, nullptr, nullptr),
                    "does not fit");
@@ -169,7 +183,7 @@ static void validation_paths() {
     EXPECT_INVALID(ffc_bn_bwd(cp, cp, 1, 4, 16, cp, cp, 0, 0.f, nullptr, nullptr, nullptr, 1e-5f, cp, dbuf, 1, p,
                               nullptr, nullptr, p, nullptr), "need batch moments");
     EXPECT_INVALID(ffc_conv_wgrad(cp, 4, 4, 4, cp, 4, 4, 4, 1, 3, 1, 1, 1, 2, nullptr, p, 0, nullptr), "workspace");
-    EXPECT_INVALID(ffc_rfft2_planes(cp, 1, 128, 128, 1.f, p, nullptr), "ffc_rfft2_planes");
+    EXPECT_INVALID(ffc_rfft2_planes(cp, 1, 128, 96, 1.f, p, nullptr), "ffc_rfft2_planes");
     EXPECT_INVALID(ffc_irfft2_planes(cp, 1, 8, 1, 1.f, nullptr, p, nullptr), "ffc_irfft2_planes");
     EXPECT_INVALID(ffc_se_bwd(cp, cp, 1, 4, 4, 4, nullptr, nullptr, 40, p, p, p, p, p, nullptr), "ffc_se_bwd");
     EXPECT_INVALID(ffc_conv_full_smallm(cp, 16, cp, nullptr, 0, nullptr, nullptr, 1, 9, p, 0, 0.f, nullptr),
