@@ -26,7 +26,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <map>
 #include <mutex>
 #include <set>
 
@@ -271,7 +270,6 @@ struct C2rArgs {
     const float* bn_scale;   // optional [2C]: Y is the raw mix output, relu(Y*bn_scale + bn_shift) on load
     const float* bn_shift;
     float iscale;            // PLANAR: bins 0 < kw < W/2 x iscale (0.5: the adjoint of rfftn)
-    int nplanes;             // fu2d_c2r_kernel: planes (B * C); the grid may be smaller (persistent)
 };
 
 // PLANAR (the training path's ffc_irfft2_planes): Y in the interleaved channel-plane layout (Re of
@@ -283,53 +281,45 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     constexpr int N1 = Split<W>::N1, N2 = Split<W>::N2, Q = Split<W>::Q;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float2* Z = reinterpret_cast<float2*>(smem);
-    const int tid = threadIdx.x;
-    // Persistent: the grid is what fits on the chip at once and a workgroup walks planes blockIdx.x,
-    // + gridDim.x, ...; the NEXT plane's Y is loaded into registers right after the current one is
-    // in LDS, so its HBM latency runs under this plane's column FFTs (the C2R's data movement and its
-    // in-LDS FFT work no longer add up).
-    constexpr int NYT = (H * WP + FU2_THREADS - 1) / FU2_THREADS;   // float2 per thread
-    float2 yv[NYT];
-    auto fetch = [&](int pl) {
-        const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)pl * H * WP;
-        const float* pre = a.Y + (size_t)pl * 2 * H * WP;   // PLANAR: Re plane, Im plane behind it
-#pragma unroll
-        for (int u = 0; u < NYT; ++u) {
-            const int i = u * FU2_THREADS + tid;
-            if (i < H * WP) {
-                if constexpr (PLANAR) {
-                    const int k = i % WP;
-                    const float sc = (k == 0 || 2 * k == W) ? 1.0f : a.iscale;
-                    yv[u] = make_float2(pre[i] * sc, pre[H * WP + i] * sc);
-                } else {
-                    yv[u] = src[i];
-                }
-            }
-        }
-    };
-    if (blockIdx.x < a.nplanes) fetch(blockIdx.x);
-    for (int plane = blockIdx.x; plane < a.nplanes; plane += gridDim.x) {
+    const int plane = blockIdx.x;
     const int ch = plane % a.C;
+    const int tid = threadIdx.x;
 
-    // 1. Y plane (registers) -> LDS rows of stride ZS; a raw (spilled) Y gets the FU's BN + ReLU here,
-    //    the same expression as mix pass 1
+    // 1. Y plane -> LDS rows of stride ZS (16 float2 loads in flight per thread per batch); a raw
+    //    (spilled) Y gets the FU's BN + ReLU here, the same expression as mix pass 1
     {
+        const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)plane * H * WP;
+        const float* pre = a.Y + (size_t)plane * 2 * H * WP;   // PLANAR: Re plane, Im plane behind it
         const bool bn = a.bn_scale != nullptr;
         const float bsr = bn ? a.bn_scale[2 * ch] : 1.0f, bhr = bn ? a.bn_shift[2 * ch] : 0.0f;
         const float bsi = bn ? a.bn_scale[2 * ch + 1] : 1.0f, bhi = bn ? a.bn_shift[2 * ch + 1] : 0.0f;
+        for (int i0 = 0; i0 < H * WP; i0 += 16 * FU2_THREADS) {
+            float2 v[16];
 #pragma unroll
-        for (int u = 0; u < NYT; ++u) {
-            const int i = u * FU2_THREADS + tid;
-            if (i < H * WP) {
-                const int r = i / WP, k = i - r * WP;
-                float2 v = yv[u];
-                if (bn) v = make_float2(fmaxf(fmaf(v.x, bsr, bhr), 0.0f), fmaxf(fmaf(v.y, bsi, bhi), 0.0f));
-                Z[r * ZS + k] = v;
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * FU2_THREADS + tid;
+                if (i < H * WP) {
+                    if constexpr (PLANAR) {
+                        const int k = i % WP;
+                        const float sc = (k == 0 || 2 * k == W) ? 1.0f : a.iscale;
+                        v[u] = make_float2(pre[i] * sc, pre[H * WP + i] * sc);
+                    } else {
+                        v[u] = src[i];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int i = i0 + u * FU2_THREADS + tid;
+                if (i < H * WP) {
+                    const int r = i / WP, k = i - r * WP;
+                    if (bn) v[u] = make_float2(fmaxf(fmaf(v[u].x, bsr, bhr), 0.0f), fmaxf(fmaf(v[u].y, bsi, bhi), 0.0f));
+                    Z[r * ZS + k] = v[u];
+                }
             }
         }
     }
     __syncthreads();
-    if (plane + (int)gridDim.x < a.nplanes) fetch(plane + gridDim.x);   // in flight under the FFTs
 
     // 2. inverse columns (length H).  The row C2R keeps only Re of columns 0 and W/2 after this pass,
     //    and Re(IFFT(a)) = IFFT(a_h) with a_h[k] = (a[k] + conj(a[-k])) / 2 (real), so those two
@@ -447,8 +437,6 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                 }
             }
         }
-    }
-    __syncthreads();   // Z is rewritten by the next plane
     }
 }
 
@@ -1084,28 +1072,6 @@ int raise_lds(const void* k, size_t lds, const char* what) {
     return FFC_OK;
 }
 
-// grid of the persistent C2R: the workgroups that fit on the device at once (occupancy of this
-// kernel at this LDS size x CUs, cached per kernel), at most one per plane
-int c2r_grid(const void* k, size_t lds, int planes) {
-    static std::mutex mu;
-    static std::map<std::pair<const void*, size_t>, int> cache;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = cache.find({k, lds});
-    int fit = 0;
-    if (it != cache.end()) {
-        fit = it->second;
-    } else {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, FU2_THREADS, lds) == hipSuccess && cus > 0 &&
-            per > 0)
-            fit = cus * per;
-        cache[{k, lds}] = fit;
-    }
-    return fit > 0 ? std::min(planes, fit) : planes;
-}
-
 // workgroups per sample: ~MIX_TILES_PER_WG bin tiles each (2 per wave), but enough workgroups
 // (>= ~1024) to fill the chip when the batch is small, down to one tile per workgroup
 int mix_nsplit(int B, int H, int W) {
@@ -1231,14 +1197,13 @@ static int fu2d_c2r_launch(const float* Y, int B, int C, int H, int W, const flo
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu2d_c2r: up must be 1 or 2");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
     C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
-              bn_scale, bn_shift, 1.0f, B * C};
+              bn_scale, bn_shift, 1.0f};
     C2rKernel k = pick_c2r(H, W, up);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [16, 128])");
     const size_t lds = c2r_lds(H, W);
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_c2r");
     if (rc) return rc;
-    hipLaunchKernelGGL(k, dim3(c2r_grid(reinterpret_cast<const void*>(k), lds, B * C)), dim3(FU2_THREADS), lds,
-                       (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r");
 }
 
@@ -1304,7 +1269,7 @@ extern "C" int ffc_fu2d_c2r_rows(const float* Yc, int B, int C, int H, int W, co
     const int RB = H < 64 ? H : 64;
     const size_t lds = (size_t)RB * zstride(W / 2 + 1) * 8;
     C2rArgs a{Yc, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
-              nullptr, nullptr, 1.0f, B * C};
+              nullptr, nullptr, 1.0f};
     hipLaunchKernelGGL(k, dim3(B * C * (H / RB)), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_c2r_rows");
 }
@@ -1359,9 +1324,8 @@ int fft_planes_c2r(const float* Z, int P, int H, int W, float iscale, const floa
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_irfft2_planes");
     if (rc) return rc;
     C2rArgs a{Z, addend, nullptr, nullptr, y, 1, 0, addend ? 1 : 0,
-              (float)(1.0 / std::sqrt((double)H * (double)W)), nullptr, nullptr, iscale, P};
-    hipLaunchKernelGGL(k, dim3(c2r_grid(reinterpret_cast<const void*>(k), lds, P)), dim3(FU2_THREADS), lds,
-                       (hipStream_t)stream, a);
+              (float)(1.0 / std::sqrt((double)H * (double)W)), nullptr, nullptr, iscale};
+    hipLaunchKernelGGL(k, dim3(P), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return launch_status("ffc_irfft2_planes");
 }
 }  // namespace ffc
