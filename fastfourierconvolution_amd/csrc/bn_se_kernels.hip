@@ -7,6 +7,7 @@
 #include "ffc_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <cmath>
 
@@ -308,7 +309,14 @@ __global__ void se_fc_kernel(const float* means, int C, const float* __restrict_
 // (lane = 16 rg + oc: every load is 4 rows x 256 contiguous bytes) and ~512 blocks cover the slab,
 // writing fp64 partials {n, sum, sumsq} to the scratch behind `moments`; the second kernel merges the
 // S partials of a channel in a fixed order (lane-strided sums, one shuffle tree) and finalizes.
-constexpr int RED2_MIN_ROWS = 1024;
+constexpr int RED2_MIN_ROWS = 1024;   // FFC_BN_RED2_MIN overrides (A/B runs)
+int red2_min_rows() {
+    static const int v = [] {
+        const char* e = std::getenv("FFC_BN_RED2_MIN");
+        return e && *e ? std::max(1, std::atoi(e)) : RED2_MIN_ROWS;
+    }();
+    return v;
+}
 
 __global__ __launch_bounds__(256) void bn_partial16_kernel(const float4* __restrict__ slab, int nrows, int C, int S,
                                                            double* __restrict__ ws) {
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(64) void bn_merge_kernel(const double* __restrict__
 }
 
 int red2_splits(int nrows, int C) {
-    if (nrows < RED2_MIN_ROWS) return 0;
+    if (nrows < red2_min_rows()) return 0;
     const int ncg = (C + 15) / 16;
     return std::max(1, std::min(nrows / 64, (512 + ncg - 1) / ncg));
 }
