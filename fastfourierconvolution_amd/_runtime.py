@@ -155,6 +155,49 @@ def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: flo
     return scale, shift
 
 
+def bn_scale_shift_many(items, device, stream):
+    """bn_scale_shift for several BNs whose slabs are ready together (an FFC layer's bn_l and bn_g,
+    ffc_bn_act.py:80-83).  items: [(bn, C, slab, nrows, count_mult)] -> [(scale, shift)].  Under
+    SyncBN their raw moments travel in ONE all-reduce (one collective per layer instead of one per
+    BN: the per-rank step of strong scaling is latency-bound, each collective a round trip)."""
+    grp = _sync_group()
+    batch = [it for it in items if it[2] is not None and bn_mode(it[0])[0]]
+    if grp is None or len(batch) < 2:
+        return [bn_scale_shift(bn, C, slab, nrows, cm, device, stream) for bn, C, slab, nrows, cm in items]
+    from .distributed import merge_moments
+    L = lib()
+    Cs = [it[1] for it in batch]
+    # moments of every BN back to back ([sum C][3]); each reduce's scratch lies behind its own
+    # moments (the later BNs' moments included: they are reduced afterwards, in stream order)
+    offs = [3 * sum(Cs[:i]) for i in range(len(batch))]
+    need = max(offs[i] + 3 * Cs[i] + L.ffc_bn_reduce_ws_doubles(batch[i][3], Cs[i]) for i in range(len(batch)))
+    mbuf = torch.empty(need, device=device, dtype=torch.float64)
+    with observe("bn_stats"):
+        for (bn, C, slab, nrows, _), o in zip(batch, offs):
+            if bn.num_features != C:
+                raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
+            check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(mbuf[o:]), stream), "ffc_bn_reduce")
+        tot = 3 * sum(Cs)
+        merge_moments(mbuf[:tot].view(-1, 3), group=grp)
+    res = {}
+    for (bn, C, slab, nrows, cm), o in zip(batch, offs):
+        use_batch, update = bn_mode(bn)
+        scale = torch.empty(C, device=device, dtype=torch.float32)
+        shift = torch.empty(C, device=device, dtype=torch.float32)
+        momentum = -1.0 if bn.momentum is None else float(bn.momentum)
+        with observe("bn_stats"):
+            check(L.ffc_bn_finalize(ptr(mbuf[o:]), C, ptr(bn.weight.detach()) if bn.weight is not None else None,
+                                    ptr(bn.bias.detach()) if bn.bias is not None else None,
+                                    ptr(bn.running_mean) if bn.running_mean is not None else None,
+                                    ptr(bn.running_var) if bn.running_var is not None else None,
+                                    ptr(bn.num_batches_tracked) if bn.num_batches_tracked is not None else None,
+                                    1, int(update), momentum, float(bn.eps), float(cm), ptr(scale), ptr(shift), stream),
+                  "ffc_bn_finalize")
+        res[id(bn)] = (scale, shift)
+    return [res[id(it[0])] if id(it[0]) in res else bn_scale_shift(it[0], it[1], it[2], it[3], it[4], device, stream)
+            for it in items]
+
+
 # Train-mode BNs whose consumer kernel finalizes them in-kernel (ffc_bn_fold) instead of a
 # separate ffc_bn_reduce_finalize launch: single rank only (SyncBN all-reduces the moments between
 # the merge and the finalize).  FFC_BN_FOLD=0 restores the separate launch (A/B measurements).

@@ -295,12 +295,19 @@ class _FFCExec:
             lp.launch(structs, stream, flops=sum(j[0].flops for j in gjobs))
         noise = noise or {}
         done = set()
+        # the layer's slab-backed BNs (bn_l, bn_g) finalized together: one SyncBN all-reduce for both
+        slab_bns = [(bn, out.shape[1], slab, nrows, 1.0) for _, out, _, bn, slab, nrows in post
+                    if bn is not None and slab is not None]
+        ss = dict(zip((id(it[0]) for it in slab_bns), rt.bn_scale_shift_many(slab_bns, dev, stream)))
         for name, out, act, bn, slab, nrows in post:
             C = out.shape[1]
             nz = noise.get(name)
             if bn is not None:
-                sc, sh = rt.bn_scale_shift(bn, C, slab, nrows, 1.0, dev, stream) if slab is not None or \
-                    not rt.bn_mode(bn)[0] else self._bn_from_tensor(bn, out, stream)
+                if slab is not None:
+                    sc, sh = ss[id(bn)]
+                else:
+                    sc, sh = rt.bn_scale_shift(bn, C, slab, nrows, 1.0, dev, stream) if not rt.bn_mode(bn)[0] \
+                        else self._bn_from_tensor(bn, out, stream)
             else:
                 if act[0] == 0 and nz is None:
                     continue

@@ -151,8 +151,10 @@ def test_unsupported_plane_raises():
             fu(torch.randn(1, 4, 48, 48, device="cuda"))     # not a power of two
         with pytest.raises(NotImplementedError):
             fu(torch.randn(1, 4, 64, 128, device="cuda"))    # staged FU: square planes only
-    with pytest.raises(NotImplementedError):             # training path: direct DFTs up to 64 x 64
-        fu(torch.randn(1, 4, 128, 128, device="cuda"))
+    with pytest.raises(NotImplementedError):             # training path: line FFTs on square planes
+        fu(torch.randn(1, 4, 128, 64, device="cuda"))        # up to 128^2, direct DFTs up to 64^2
+    y = fu(torch.randn(1, 4, 128, 128, device="cuda"))      # 128^2 trains (tests/test_gpu_fgan_train.py)
+    assert y.shape == (1, 4, 128, 128) and y.requires_grad
 
 
 def test_conditional_path_raises_like_reference():

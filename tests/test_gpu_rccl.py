@@ -97,3 +97,42 @@ def test_syncbn_generator_graph_over_rccl(rccl_world1):
         graph.replay()
         torch.cuda.synchronize()
     torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_paired_syncbn_one_collective(rccl_world1):
+    """an FFC layer's bn_l and bn_g under SyncBN share ONE all-reduce (_runtime.bn_scale_shift_many):
+    same scale / shift and running statistics, bit for bit, as the per-BN single-rank path -- a small
+    slab (one-block-per-channel merge) beside a large one (two-level merge, scratch behind moments)"""
+    import torch.nn as nn
+    from fastfourierconvolution_amd import _runtime as rt, distributed as D
+    g = torch.Generator().manual_seed(5)
+    items, twins = [], []
+    for C, nrows in ((64, 300), (32, 2000)):
+        n = torch.randint(1, 64, (nrows, C), generator=g).float()
+        slab = torch.stack([n, torch.randn((nrows, C), generator=g), torch.rand((nrows, C), generator=g) * n,
+                            torch.zeros_like(n)], -1).cuda()
+        bn = nn.BatchNorm2d(C).cuda().train()
+        with torch.no_grad():
+            bn.weight.copy_(1 + 0.1 * torch.randn(C, generator=g))
+            bn.bias.copy_(0.1 * torch.randn(C, generator=g))
+        twin = nn.BatchNorm2d(C).cuda().train()
+        twin.load_state_dict(bn.state_dict())
+        items.append((bn, C, slab, nrows, 1.0))
+        twins.append((twin, C, slab, nrows, 1.0))
+    ref = [rt.bn_scale_shift(b, C, s, n, cm, torch.device("cuda"), rt.stream_of(s)) for b, C, s, n, cm in twins]
+    calls = []
+    orig = D.merge_moments
+    D.merge_moments = lambda m, group=None: calls.append(m.shape) or orig(m, group=group)
+    try:
+        D.enable_sync_bn(even_world1=True)
+        got = rt.bn_scale_shift_many(items, torch.device("cuda"), torch.cuda.current_stream().cuda_stream)
+    finally:
+        D.merge_moments = orig
+        D.disable_sync_bn()
+    torch.cuda.synchronize()
+    assert calls == [torch.Size([96, 3])]
+    for (s0, h0), (s1, h1) in zip(ref, got):
+        assert torch.equal(s0, s1) and torch.equal(h0, h1)
+    for (b, *_), (t, *_) in zip(items, twins):
+        for k, v in b.state_dict().items():
+            assert torch.equal(v, t.state_dict()[k]), k
