@@ -79,6 +79,20 @@ class InTf(ctypes.Structure):
                 ("noise_w", c_void_p), ("noise", c_void_p)]
 
 
+class BnRfItem(ctypes.Structure):
+    """ffc_bn_rf_item: one BN of ffc_bn_reduce_finalize_batch"""
+    _fields_ = [("slab", c_void_p), ("nrows", c_int), ("C", c_int), ("moments", c_void_p), ("gamma", c_void_p),
+                ("beta", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
+                ("num_batches_tracked", c_void_p), ("update_running", c_int), ("momentum", c_float), ("eps", c_float),
+                ("count_mult", c_float), ("scale", c_void_p), ("shift", c_void_p)]
+
+
+class BnApplyItem(ctypes.Structure):
+    """ffc_bn_apply_item: one tensor of ffc_bn_act_apply_batch"""
+    _fields_ = [("x", c_void_p), ("y", c_void_p), ("B", c_int), ("C", c_int), ("HW", c_int), ("scale", c_void_p),
+                ("shift", c_void_p), ("act", c_int), ("act_param", c_float), ("noise_w", c_void_p), ("noise", c_void_p)]
+
+
 # (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
 SIGNATURES = [
     ("ffc_last_error", ctypes.c_char_p, []),
@@ -100,6 +114,8 @@ SIGNATURES = [
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_void_p),
                               c_void_p, c_void_p, c_void_p]),
     ("ffc_bn_reduce_ws_doubles", c_size_t, [c_int, c_int]),
+    ("ffc_bn_reduce_finalize_batch", c_int, [ctypes.POINTER(BnRfItem), c_int, c_void_p]),
+    ("ffc_bn_act_apply_batch", c_int, [ctypes.POINTER(BnApplyItem), c_int, c_void_p]),
     ("ffc_bn_reduce", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_bn_finalize", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                 c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
@@ -206,11 +222,11 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (c_int * 8)()
-        lib.ffc_struct_sizes(sizes, 8)
+        sizes = (c_int * 10)()
+        lib.ffc_struct_sizes(sizes, 10)
         want = (ctypes.sizeof(ConvSeg), ctypes.sizeof(ConvPhase), ctypes.sizeof(ConvJob),
                 ctypes.sizeof(ConvPSeg), ctypes.sizeof(ConvPPhase), ctypes.sizeof(ConvPJob), ctypes.sizeof(BnFold),
-                ctypes.sizeof(InTf))
+                ctypes.sizeof(InTf), ctypes.sizeof(BnRfItem), ctypes.sizeof(BnApplyItem))
         if tuple(sizes) != want:
             raise FFCError(f"ABI struct layout mismatch: library {tuple(sizes)} vs binding {want}")
         _lib = lib

@@ -155,6 +155,50 @@ def bn_scale_shift(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: flo
     return scale, shift
 
 
+def _bn_finalize_batch(items, batch, device, stream):
+    """single rank: the batch's reduce + finalize in one launch (ffc_bn_reduce_finalize_batch)"""
+    from ._lib import BnRfItem
+    L = lib()
+    arr = (BnRfItem * len(batch))()
+    res, keep = {}, []
+    for k, (bn, C, slab, nrows, cm) in enumerate(batch):
+        if bn.num_features != C:
+            raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
+        _, update = bn_mode(bn)
+        scale = torch.empty(C, device=device, dtype=torch.float32)
+        shift = torch.empty(C, device=device, dtype=torch.float32)
+        mbuf = torch.empty(3 * C + L.ffc_bn_reduce_ws_doubles(nrows, C), device=device, dtype=torch.float64)
+        keep.append(mbuf)
+        arr[k] = BnRfItem(ptr(slab), nrows, C, ptr(mbuf), ptr(bn.weight.detach()) if bn.weight is not None else None,
+                          ptr(bn.bias.detach()) if bn.bias is not None else None,
+                          ptr(bn.running_mean) if bn.running_mean is not None else None,
+                          ptr(bn.running_var) if bn.running_var is not None else None,
+                          ptr(bn.num_batches_tracked) if bn.num_batches_tracked is not None else None,
+                          int(update), -1.0 if bn.momentum is None else float(bn.momentum), float(bn.eps), float(cm),
+                          ptr(scale), ptr(shift))
+        res[id(bn)] = (scale, shift)
+    with observe("bn_stats"):
+        check(L.ffc_bn_reduce_finalize_batch(arr, len(batch), stream), "ffc_bn_reduce_finalize_batch")
+    return [res[id(it[0])] if id(it[0]) in res else bn_scale_shift(it[0], it[1], it[2], it[3], it[4], device, stream)
+            for it in items]
+
+
+def bn_act_apply_batch(items):
+    """[(x, scale, shift, act, param, noise_w or None, noise or None)]: y = x in place, one launch
+    (ffc_bn_act_apply_batch; the l and g outputs of an FFC_BN_ACT, with fgan128's NoiseInjection)"""
+    from ._lib import BnApplyItem
+    arr = (BnApplyItem * len(items))()
+    nbytes = 0.0
+    for k, (x, sc, sh, act, param, nw, nz) in enumerate(items):
+        B, C = x.shape[:2]
+        HW = x.numel() // (B * C)
+        arr[k] = BnApplyItem(ptr(x), ptr(x), B, C, HW, ptr(sc), ptr(sh), int(act), float(param), ptr(nw), ptr(nz))
+        nbytes += 8.0 * x.numel() + (4.0 * nz.numel() if nz is not None else 0.0)
+    label = "bn_act_noise" if any(it[6] is not None for it in items) else "bn_act"
+    with observe(label, bytes=nbytes):
+        check(lib().ffc_bn_act_apply_batch(arr, len(items), stream_of(items[0][0])), "ffc_bn_act_apply_batch")
+
+
 def bn_scale_shift_many(items, device, stream):
     """bn_scale_shift for several BNs whose slabs are ready together (an FFC layer's bn_l and bn_g,
     ffc_bn_act.py:80-83).  items: [(bn, C, slab, nrows, count_mult)] -> [(scale, shift)].  Under
@@ -162,8 +206,10 @@ def bn_scale_shift_many(items, device, stream):
     BN: the per-rank step of strong scaling is latency-bound, each collective a round trip)."""
     grp = _sync_group()
     batch = [it for it in items if it[2] is not None and bn_mode(it[0])[0]]
-    if grp is None or len(batch) < 2:
+    if len(batch) < 2 or len(batch) > 4:
         return [bn_scale_shift(bn, C, slab, nrows, cm, device, stream) for bn, C, slab, nrows, cm in items]
+    if grp is None:
+        return _bn_finalize_batch(items, batch, device, stream)
     from .distributed import merge_moments
     L = lib()
     Cs = [it[1] for it in batch]

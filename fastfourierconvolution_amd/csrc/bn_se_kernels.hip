@@ -408,6 +408,76 @@ int red2_splits(int nrows, int C) {
     return std::max(1, std::min(nrows / 64, (512 + ncg - 1) / ncg));
 }
 
+// ---- batched forms: one launch for the BNs of a layer (items located by block-index prefix sums)
+struct RfBatch {
+    const float4* slab[FFC_MAX_BN_BATCH];
+    double* moments[FFC_MAX_BN_BATCH];
+    FinalizeArgs fa[FFC_MAX_BN_BATCH];
+    int nrows[FFC_MAX_BN_BATCH], C[FFC_MAX_BN_BATCH];
+    int off[FFC_MAX_BN_BATCH + 1];
+    int n;
+};
+
+__global__ void bn_reduce_finalize_batch_kernel(RfBatch a) {
+    int it = 0;
+    while (it + 1 < a.n && (int)blockIdx.x >= a.off[it + 1]) ++it;
+    const int c = blockIdx.x - a.off[it];
+    FinalizeIn in = {};
+    if (threadIdx.x == 0) in = finalize_load(c, a.fa[it]);
+    double m[3];
+    reduce_channel(a.slab[it], a.nrows[it], a.C[it], c, a.moments[it] + 3 * c, m);
+    if (threadIdx.x == 0) finalize_channel(m, c, a.fa[it], in);
+    if (a.fa[it].bump_here && c == 0 && threadIdx.x == 0) *a.fa[it].nbt += 1;
+}
+
+struct ApplyBatch {
+    const float4* x[FFC_MAX_BN_BATCH];
+    float4* y[FFC_MAX_BN_BATCH];
+    const float* scale[FFC_MAX_BN_BATCH];
+    const float* shift[FFC_MAX_BN_BATCH];
+    const float* noise_w[FFC_MAX_BN_BATCH];
+    const float4* noise[FFC_MAX_BN_BATCH];
+    int C[FFC_MAX_BN_BATCH], HW4[FFC_MAX_BN_BATCH], chunks[FFC_MAX_BN_BATCH], act[FFC_MAX_BN_BATCH];
+    float p[FFC_MAX_BN_BATCH];
+    int off[FFC_MAX_BN_BATCH + 1];
+    int n;
+};
+
+// bn_act_plane_kernel over several tensors: block -> (item, plane, chunk)
+__global__ __launch_bounds__(256) void bn_act_plane_batch_kernel(ApplyBatch a) {
+    int it = 0;
+    while (it + 1 < a.n && (int)blockIdx.x >= a.off[it + 1]) ++it;
+    const int bid = blockIdx.x - a.off[it];
+    const int chunks = a.chunks[it], HW4 = a.HW4[it];
+    const int plane = bid / chunks, chunk = bid - plane * chunks;
+    const int c = plane % a.C[it], b = plane / a.C[it];
+    const float sc = a.scale[it][c], sh = a.shift[it][c];
+    const float nw = a.noise_w[it] ? a.noise_w[it][c] : 0.0f;
+    const int act = a.act[it];
+    const float p = a.p[it];
+    const size_t base = (size_t)plane * HW4;
+    const float4* nz = a.noise[it] ? a.noise[it] + (size_t)b * HW4 : nullptr;
+    const float4* x = a.x[it];
+    float4* y = a.y[it];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = chunk * PLANE_CHUNK4 + u * 256 + threadIdx.x;
+        if (i < HW4) {
+            const float4 v = x[base + i];
+            float4 r = make_float4(ffc::apply_act(fmaf(v.x, sc, sh), act, p), ffc::apply_act(fmaf(v.y, sc, sh), act, p),
+                                   ffc::apply_act(fmaf(v.z, sc, sh), act, p), ffc::apply_act(fmaf(v.w, sc, sh), act, p));
+            if (nz) {
+                const float4 n = nz[i];
+                r.x = fmaf(nw, n.x, r.x);
+                r.y = fmaf(nw, n.y, r.y);
+                r.z = fmaf(nw, n.z, r.z);
+                r.w = fmaf(nw, n.w, r.w);
+            }
+            y[base + i] = r;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" size_t ffc_bn_reduce_ws_doubles(int nrows, int C) {
@@ -552,4 +622,85 @@ extern "C" int ffc_bn_act_noise_apply(const float* x, float* y, int B, int C, in
                        reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), C, HW4, chunks, scale, shift,
                        act, act_param, noise_w, reinterpret_cast<const float4*>(noise));
     return ffc::launch_status("ffc_bn_act_noise_apply");
+}
+
+extern "C" int ffc_bn_reduce_finalize_batch(const ffc_bn_rf_item* items, int n, void* stream) {
+    FFC_CHECK_ARG(items && n >= 1 && n <= FFC_MAX_BN_BATCH, "ffc_bn_reduce_finalize_batch: 1 <= n <= 4 items");
+    RfBatch a = {};
+    int blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const ffc_bn_rf_item& t = items[i];
+        FFC_CHECK_ARG(t.slab && t.moments && t.nrows > 0 && t.C > 0 && t.scale && t.shift,
+                      "ffc_bn_reduce_finalize_batch: bad item");
+        FFC_CHECK_ARG(!t.update_running || (t.running_mean && t.running_var && t.num_batches_tracked),
+                      "ffc_bn_reduce_finalize_batch: update needs running buffers");
+    }
+    for (int i = 0; i < n; ++i) {
+        const ffc_bn_rf_item& t = items[i];
+        if (red2_splits(t.nrows, t.C)) {   // large slab: its own two-level launches
+            const int rc = ffc_bn_reduce_finalize(t.slab, t.nrows, t.C, t.moments, t.gamma, t.beta, t.running_mean,
+                                                  t.running_var, t.num_batches_tracked, t.update_running, t.momentum,
+                                                  t.eps, t.count_mult, t.scale, t.shift, stream);
+            if (rc) return rc;
+            continue;
+        }
+        const int k = a.n++;
+        a.slab[k] = reinterpret_cast<const float4*>(t.slab);
+        a.moments[k] = t.moments;
+        a.fa[k] = make_finalize(t.gamma, t.beta, t.running_mean, t.running_var, t.num_batches_tracked, 1,
+                                t.update_running, t.momentum, t.eps, t.count_mult, t.scale, t.shift);
+        a.nrows[k] = t.nrows;
+        a.C[k] = t.C;
+        a.off[k] = blocks;
+        blocks += t.C;
+    }
+    if (a.n == 0) return FFC_OK;
+    a.off[a.n] = blocks;
+    hipLaunchKernelGGL(bn_reduce_finalize_batch_kernel, dim3(blocks), dim3(RED_THREADS), 0, (hipStream_t)stream, a);
+    for (int k = 0; k < a.n; ++k)   // momentum=None reads num_batches_tracked in every block: bump after
+        if (a.fa[k].update_running && !a.fa[k].bump_here)
+            hipLaunchKernelGGL(bn_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a.fa[k].nbt);
+    return ffc::launch_status("ffc_bn_reduce_finalize_batch");
+}
+
+extern "C" int ffc_bn_act_apply_batch(const ffc_bn_apply_item* items, int n, void* stream) {
+    FFC_CHECK_ARG(items && n >= 1 && n <= FFC_MAX_BN_BATCH, "ffc_bn_act_apply_batch: 1 <= n <= 4 items");
+    ApplyBatch a = {};
+    long long blocks = 0;
+    for (int i = 0; i < n; ++i) {
+        const ffc_bn_apply_item& t = items[i];
+        FFC_CHECK_ARG(t.x && t.y && t.scale && t.shift && t.B > 0 && t.C > 0 && t.HW > 0,
+                      "ffc_bn_act_apply_batch: bad item");
+        FFC_CHECK_ARG(!t.noise || t.noise_w, "ffc_bn_act_apply_batch: noise needs noise_w");
+        const bool plane = t.HW % 4 == 0 && t.HW >= 256 &&
+                           ((reinterpret_cast<uintptr_t>(t.x) | reinterpret_cast<uintptr_t>(t.y) |
+                             reinterpret_cast<uintptr_t>(t.noise)) & 15) == 0;
+        if (!plane) {   // the single forms' other paths
+            const int rc = t.noise ? ffc_bn_act_noise_apply(t.x, t.y, t.B, t.C, t.HW, t.scale, t.shift, t.act,
+                                                            t.act_param, t.noise_w, t.noise, stream)
+                                   : ffc_bn_act_apply(t.x, t.y, t.B, t.C, t.HW, t.scale, t.shift, t.act, t.act_param,
+                                                      stream);
+            if (rc) return rc;
+            continue;
+        }
+        const int k = a.n++;
+        a.x[k] = reinterpret_cast<const float4*>(t.x);
+        a.y[k] = reinterpret_cast<float4*>(t.y);
+        a.scale[k] = t.scale;
+        a.shift[k] = t.shift;
+        a.noise_w[k] = t.noise ? t.noise_w : nullptr;
+        a.noise[k] = reinterpret_cast<const float4*>(t.noise);
+        a.C[k] = t.C;
+        a.HW4[k] = t.HW / 4;
+        a.chunks[k] = (t.HW / 4 + PLANE_CHUNK4 - 1) / PLANE_CHUNK4;
+        a.act[k] = t.act;
+        a.p[k] = t.act_param;
+        a.off[k] = (int)blocks;
+        blocks += (long long)t.B * t.C * a.chunks[k];
+        FFC_CHECK_ARG(blocks < (1LL << 31), "ffc_bn_act_apply_batch: grid too large");
+    }
+    if (a.n == 0) return FFC_OK;
+    a.off[a.n] = (int)blocks;
+    hipLaunchKernelGGL(bn_act_plane_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    return ffc::launch_status("ffc_bn_act_apply_batch");
 }

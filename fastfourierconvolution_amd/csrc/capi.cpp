@@ -37,5 +37,9 @@ extern "C" int ffc_struct_sizes(int* out, int n) {
     out[5] = (int)sizeof(ffc_convp_job);
     if (n >= 7) out[6] = (int)sizeof(ffc_bn_fold);
     if (n >= 8) out[7] = (int)sizeof(ffc_in_tf);
+    if (n >= 10) {
+        out[8] = (int)sizeof(ffc_bn_rf_item);
+        out[9] = (int)sizeof(ffc_bn_apply_item);
+    }
     return FFC_OK;
 }

@@ -295,6 +295,7 @@ class _FFCExec:
             lp.launch(structs, stream, flops=sum(j[0].flops for j in gjobs))
         noise = noise or {}
         done = set()
+        applies = []
         # the layer's slab-backed BNs (bn_l, bn_g) finalized together: one SyncBN all-reduce for both
         slab_bns = [(bn, out.shape[1], slab, nrows, 1.0) for _, out, _, bn, slab, nrows in post
                     if bn is not None and slab is not None]
@@ -318,11 +319,14 @@ class _FFCExec:
                 done.add(name)
                 continue
             if nz is not None and out.shape[2] * out.shape[3] % 4 == 0:
-                mod, n = nz
-                rt.bn_act_noise_apply(out, sc, sh, act[0], act[1], mod, n)
+                # the noise drawn here, in branch order, as the single pass does; applied below
+                p = rt.PendingAct(out, sc, sh, act[0], act[1], *nz)
+                applies.append((out, sc, sh, act[0], act[1], p.noise_w, p.noise))
                 done.add(name)
             else:
-                rt.bn_act_apply(out, sc, sh, act[0], act[1])
+                applies.append((out, sc, sh, act[0], act[1], None, None))
+        if applies:   # the layer's BN + activation (+ noise) passes in one launch
+            rt.bn_act_apply_batch(applies)
         for name, (mod, n) in noise.items():   # branches without a BN/activation pass of their own
             if name not in done and isinstance(outs[name], torch.Tensor):
                 outs[name] = mod(outs[name], n)

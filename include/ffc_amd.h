@@ -41,7 +41,8 @@ extern "C" {
 const char* ffc_last_error(void);
 int ffc_abi_version(void);
 /* sizeof(ffc_conv_seg), (ffc_conv_phase), (ffc_conv_job), (ffc_convp_seg), (ffc_convp_phase),
- * (ffc_convp_job) -> out[0..5]; n >= 7: sizeof(ffc_bn_fold) -> out[6]; n >= 8: sizeof(ffc_in_tf) -> out[7] */
+ * (ffc_convp_job) -> out[0..5]; n >= 7: sizeof(ffc_bn_fold) -> out[6]; n >= 8: sizeof(ffc_in_tf) -> out[7];
+ * n >= 10: sizeof(ffc_bn_rf_item), sizeof(ffc_bn_apply_item) -> out[8], out[9] */
 int ffc_struct_sizes(int* out, int n);
 
 /* ------------------------------------------------------------------ local branch
@@ -253,6 +254,39 @@ int ffc_bn_act_apply(const float* x, float* y, int B, int C, int HW, const float
 int ffc_bn_act_noise_apply(const float* x, float* y, int B, int C, int HW, const float* scale,
                            const float* shift, int act, float act_param, const float* noise_w,
                            const float* noise, void* stream);
+
+/* Batched forms for the BNs of one FFC layer (bn_l and bn_g come out of the same conv launch,
+ * ffc_bn_act.py:80-83): up to FFC_MAX_BN_BATCH items per call, one launch for all of them where the
+ * single forms would launch once per item (launch latency dominates these small kernels).  Each item
+ * has the meaning of the single call's arguments. */
+#define FFC_MAX_BN_BATCH 4
+typedef struct ffc_bn_rf_item {       /* ffc_bn_reduce_finalize arguments */
+    const float* slab;
+    int nrows, C;
+    double* moments;                  /* [C][3] + ffc_bn_reduce_ws_doubles(nrows, C) */
+    const float* gamma;
+    const float* beta;
+    float* running_mean;
+    float* running_var;
+    int64_t* num_batches_tracked;
+    int update_running;
+    float momentum, eps, count_mult;
+    float* scale;
+    float* shift;
+} ffc_bn_rf_item;
+int ffc_bn_reduce_finalize_batch(const ffc_bn_rf_item* items, int n, void* stream);
+typedef struct ffc_bn_apply_item {    /* ffc_bn_act_noise_apply arguments (noise_w / noise may be NULL) */
+    const float* x;
+    float* y;
+    int B, C, HW;
+    const float* scale;
+    const float* shift;
+    int act;
+    float act_param;
+    const float* noise_w;
+    const float* noise;
+} ffc_bn_apply_item;
+int ffc_bn_act_apply_batch(const ffc_bn_apply_item* items, int n, void* stream);
 
 /* ------------------------------------------------------------------ spectral branch
  * SELayer gate (spectral_transform.py:12-28): gate[b][c] = sigmoid(W2 relu(W1 mean_hw x)),

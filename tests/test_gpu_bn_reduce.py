@@ -73,3 +73,70 @@ def test_bn_reduce_finalize_large(nrows, C, momentum):
     torch.testing.assert_close(rv.cpu().double(), (1 - f) * rv0.cpu().double() + f * var * n / (n - 1),
                                rtol=1e-5, atol=1e-6)
     assert int(nbt.item()) == 4
+
+
+def test_batched_finalize_and_apply_match_single_calls():
+    """ffc_bn_reduce_finalize_batch / ffc_bn_act_apply_batch (one launch for a layer's BNs) against the
+    single calls, bit for bit: a small slab, a large (two-level) slab and a momentum=None BN; apply
+    with and without noise, plus a tensor the plane kernel does not take (HW = 36)"""
+    import ctypes
+    from fastfourierconvolution_amd import _lib
+    L = _lib.load()
+    gen = torch.Generator().manual_seed(9)
+    specs = [(300, 64, 0.1), (2000, 32, 0.1), (50, 16, None)]
+    slabs = [_slab(n, C, gen)[0].cuda() for n, C, _ in specs]
+
+    def params(C):
+        return [t.cuda() for t in (1 + 0.1 * torch.randn(C, generator=gen), 0.1 * torch.randn(C, generator=gen),
+                                   0.1 * torch.randn(C, generator=gen), 0.5 + torch.rand(C, generator=gen))]
+    ps = [params(C) for _, C, _ in specs]
+    runs = []
+    for batched in (False, True):
+        st = [[t.clone() for t in p] + [torch.tensor(2, dtype=torch.int64, device="cuda")] for p in ps]
+        out = [(torch.empty(C, device="cuda"), torch.empty(C, device="cuda")) for _, C, _ in specs]
+        bufs = [torch.empty(3 * C + L.ffc_bn_reduce_ws_doubles(n, C), dtype=torch.float64, device="cuda")
+                for n, C, _ in specs]
+        args = [(slabs[i].data_ptr(), n, C, bufs[i].data_ptr(), *(t.data_ptr() for t in st[i]), 1,
+                 -1.0 if m is None else m, 1e-5, 1.0, out[i][0].data_ptr(), out[i][1].data_ptr())
+                for i, (n, C, m) in enumerate(specs)]
+        if batched:
+            arr = (_lib.BnRfItem * 3)(*[_lib.BnRfItem(*a) for a in args])
+            assert L.ffc_bn_reduce_finalize_batch(arr, 3, None) == 0, L.ffc_last_error()
+        else:
+            for a in args:
+                assert L.ffc_bn_reduce_finalize(*a, None) == 0, L.ffc_last_error()
+        torch.cuda.synchronize()
+        runs.append((out, st))
+    for (s0, h0), (s1, h1) in zip(runs[0][0], runs[1][0]):
+        assert torch.equal(s0, s1) and torch.equal(h0, h1)
+    for a, b in zip(runs[0][1], runs[1][1]):
+        for t0, t1 in zip(a, b):
+            assert torch.equal(t0, t1)
+    # apply
+    xs = [torch.randn((2, 8, 32, 32), generator=gen).cuda(), torch.randn((2, 4, 16, 16), generator=gen).cuda(),
+          torch.randn((3, 5, 6, 6), generator=gen).cuda()]
+    nzs = [torch.randn((2, 1, 32, 32), generator=gen).cuda(), None, None]
+    sc = [torch.rand(x.shape[1], generator=gen).cuda() + 0.5 for x in xs]
+    sh = [0.1 * torch.randn(x.shape[1], generator=gen).cuda() for x in xs]
+    nw = [torch.randn(x.shape[1], generator=gen).cuda() for x in xs]
+    acts = [5, 1, 2]
+    ref = [x.clone() for x in xs]
+    for i, x in enumerate(ref):
+        B, C, H, W = x.shape
+        if nzs[i] is not None:
+            rc = L.ffc_bn_act_noise_apply(x.data_ptr(), x.data_ptr(), B, C, H * W, sc[i].data_ptr(), sh[i].data_ptr(),
+                                          acts[i], 0.1, nw[i].data_ptr(), nzs[i].data_ptr(), None)
+        else:
+            rc = L.ffc_bn_act_apply(x.data_ptr(), x.data_ptr(), B, C, H * W, sc[i].data_ptr(), sh[i].data_ptr(),
+                                    acts[i], 0.1, None)
+        assert rc == 0
+    got = [x.clone() for x in xs]
+    arr = (_lib.BnApplyItem * 3)(*[_lib.BnApplyItem(x.data_ptr(), x.data_ptr(), x.shape[0], x.shape[1],
+                                                    x.shape[2] * x.shape[3], sc[i].data_ptr(), sh[i].data_ptr(),
+                                                    acts[i], 0.1, nw[i].data_ptr() if nzs[i] is not None else None,
+                                                    nzs[i].data_ptr() if nzs[i] is not None else None)
+                                   for i, x in enumerate(got)])
+    assert L.ffc_bn_act_apply_batch(arr, 3, None) == 0, L.ffc_last_error()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
