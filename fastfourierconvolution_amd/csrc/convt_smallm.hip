@@ -68,15 +68,10 @@ constexpr int CT_TR = FFC_CT_TR;             // input tile rows
 constexpr int CT_QT = (CT_TT / 2) * (CT_TR / 2);   // threads per channel quarter
 constexpr int CT_PR = CT_TR + 2;             // patch rows: iy = y0-1 .. y0+TR
 constexpr int CT_PS = CT_TT + 8;             // patch row: ix = x0-4 .. x0+35 (10 aligned float4 groups)
-// LDS row stride of a staged patch (floats): 48, so that the two patch rows a half-wave reads
-// (qy, qy + 2: 2 * 48 = 96 = 32 mod 64 banks) fall on disjoint banks; with the 40-float row the
-// lanes' even-bank reads overlapped 2-way (SQ_LDS_BANK_CONFLICT 3.7M cycles per gen64 step,
-// profiles/r02/pmc_sq_gen64_r02.txt)
-constexpr int CT_PSS = CT_PS + 8;
 constexpr int CT_G = CT_PR * (CT_PS / 4);    // float4 groups per channel
 constexpr int CT_CPQ = FFC_CT_CPQ;           // channels per quarter per step
 constexpr int CT_GT = (CT_CPQ * CT_G + CT_QT - 1) / CT_QT;   // groups per thread per step
-constexpr int CT_PB = CT_PR * CT_PSS;        // floats per channel patch (LDS)
+constexpr int CT_PB = CT_PR * CT_PS;         // floats per channel patch
 constexpr int CT_NQ = 4;                     // channel quarters
 constexpr int CT_THREADS = CT_QT * CT_NQ;
 constexpr int CT_CMAX = 256;                 // channels (both segments) whose weights fit in LDS
@@ -99,7 +94,7 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
     constexpr int CT_PR = CT_TR + 2;
     constexpr int CT_G = CT_PR * (CT_PS / 4);
     constexpr int CT_GT = (CT_CPQ * CT_G + CT_QT - 1) / CT_QT;
-    constexpr int CT_PB = CT_PR * CT_PSS;
+    constexpr int CT_PB = CT_PR * CT_PS;
     constexpr int CT_THREADS = CT_QT * CT_NQ;
     constexpr int CT_WOFF = 2 * CT_NQ * CT_CPQ * CT_PB;
     static_assert(CT_QT % 64 == 0 && CT_QT * 16 * 4 <= CT_WOFF, "quarters of whole waves; combine area fits");
@@ -161,11 +156,7 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
 #pragma unroll
         for (int j = 0; j < CT_GT; ++j) {
             const int n = j * CT_QT + tid;
-            if (n < CT_CPQ * CT_G) {
-                const int cl = n / CT_G, nn = n - cl * CT_G;
-                const int g = nn % (CT_PS / 4), pr = nn / (CT_PS / 4);
-                reinterpret_cast<float4*>(dst + cl * CT_PB + pr * CT_PSS)[g] = r[j];
-            }
+            if (n < CT_CPQ * CT_G) reinterpret_cast<float4*>(dst)[n] = r[j];
         }
     };
     auto buf = [&](int k) { return pbuf + ((k & 1) * CT_NQ + q) * CT_CPQ * CT_PB; };
@@ -198,15 +189,15 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
     auto compute = [&](int k, int cl) {
         const int ci = CT_CPQ * (CT_NQ * k + q) + cl;
         if (ci >= Ct) return;
-        const float* p = buf(k) + cl * CT_PB + qy * CT_PSS + qx + 3;   // input row qy-1, col qx-1
+        const float* p = buf(k) + cl * CT_PB + qy * CT_PS + qx + 3;   // input row qy-1, col qx-1
         float v[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const f2 mid = *reinterpret_cast<const f2*>(p + i * CT_PSS + 1);
-            v[i][0] = p[i * CT_PSS];
+            const f2 mid = *reinterpret_cast<const f2*>(p + i * CT_PS + 1);
+            v[i][0] = p[i * CT_PS];
             v[i][1] = mid.x;
             v[i][2] = mid.y;
-            v[i][3] = p[i * CT_PSS + 3];
+            v[i][3] = p[i * CT_PS + 3];
         }
         const fx4* wc = wlds + ci * 16;
 #pragma unroll
@@ -608,7 +599,7 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     a.act = act;
     a.act_param = act_param;
 
-    const size_t woff = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PSS;
+    const size_t woff = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PS;
     const size_t lds = (woff + (size_t)(C0 + (x1 ? C1 : 0)) * 64) * sizeof(float);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
