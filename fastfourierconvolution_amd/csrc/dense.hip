@@ -49,25 +49,26 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
         const bool ok = k < a.K && nv;
         wa[u] = ffc::buf_ld(rW, ok ? (unsigned)(((size_t)k * a.N + n) * 4) : ffc::OOB);
     }
-    constexpr int NA = DN_BM * 2 * KH / DN_THREADS;   // A elements per thread (K <= 2 KH)
+    // the 64 x K A tile: wave w stages rows 16w .. 16w+15, lane l columns l, l+64, .. (< 2 KH), zeros
+    // past K -- row / column come from the lane and loop indices (no per-element division by K)
+    constexpr int NC = 2 * KH / 64;                   // column groups of 64 (K <= 2 KH)
+    constexpr int NA = (DN_BM / 4) * NC;               // A elements per thread
     float v[NA];
 #pragma unroll
-    for (int u = 0; u < NA; ++u) {
-        const int i = u * DN_THREADS + tid;
-        const int r = i / a.K;
-        const bool ok = i < DN_BM * a.K && b0 + r < a.B;
-        v[u] = ffc::buf_ld(rA, ok ? (unsigned)(((size_t)b0 * a.K + i) * 4) : ffc::OOB);
-    }
+    for (int rr = 0; rr < DN_BM / 4; ++rr)
 #pragma unroll
-    for (int u = 0; u < NA; ++u) {
-        const int i = u * DN_THREADS + tid;
-        const int r = i / a.K, k = i - r * a.K;
-        if (i < DN_BM * a.K) As[r * KS + k] = v[u];
-    }
-    for (int i = tid; i < DN_BM * (KS - a.K); i += DN_THREADS) {   // zero the row tails
-        const int r = i / (KS - a.K), k = a.K + (i - r * (KS - a.K));
-        As[r * KS + k] = 0.0f;
-    }
+        for (int cg = 0; cg < NC; ++cg) {
+            const int r = wave * (DN_BM / 4) + rr, k = cg * 64 + lane;
+            const bool ok = k < a.K && b0 + r < a.B;
+            v[rr * NC + cg] = ffc::buf_ld(rA, ok ? (unsigned)(((size_t)(b0 + r) * a.K + k) * 4) : ffc::OOB);
+        }
+#pragma unroll
+    for (int rr = 0; rr < DN_BM / 4; ++rr)
+#pragma unroll
+        for (int cg = 0; cg < NC; ++cg) {
+            const int r = wave * (DN_BM / 4) + rr, k = cg * 64 + lane;
+            if (k < KS) As[r * KS + k] = v[rr * NC + cg];   // out-of-range loads read 0: the row tails
+        }
     __syncthreads();
     const float* ar = As + (wr * 32 + col) * KS;   // this lane's A row
     floatx16 acc;
