@@ -22,6 +22,8 @@
 // FMAs, written to the other LDS buffer after them).
 #include "ffc_internal.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int SM_THREADS = 512;   // conv3x3_smallm_kernel: two halves of 256
@@ -302,39 +304,54 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
 // any LDS read).  All weights are staged once, as [channel][m][12] (9 taps, padded).
 // Per channel a thread reads its 6x6 neighbourhood as 6 x (b32 + b128 + b32) and 3 x 3 broadcast
 // b128 of weights: 18 + 3M LDS reads feed 144M FMAs.
-constexpr int T3 = 64;                      // output tile side
-constexpr int R3 = T3 + 2;                  // patch rows (halo 1)
+constexpr int T3 = 64;                      // output tile columns
 constexpr int S3 = T3 + 8;                  // patch row: 18 float4 groups
-constexpr int G3 = R3 * (S3 / 4);           // float4 groups per channel
-constexpr int GT3 = (G3 + 255) / 256;       // groups per thread
-constexpr int PB3 = G3 * 4;                 // floats per patch buffer
-constexpr int CMAX3 = 256;                  // channels (both segments) whose weights fit the LDS slot
+constexpr int CMAX3 = 256;                  // channels (both segments)
+// TR3 output rows per tile: 64 (one 512-thread workgroup per CU, 124 KB of LDS) or 32 (256 threads,
+// ~64 KB with the weights sized to the channel count: two independent workgroups per CU, so one
+// stages / waits on its barrier while the other computes).  Threads per half: (TR3 / 4) x 16.
+template <int TR3>
+struct Head3 {
+    static constexpr int R3 = TR3 + 2;                        // patch rows (halo 1)
+    static constexpr int G3 = R3 * (S3 / 4);                  // float4 groups per channel
+    static constexpr int HT = (TR3 / 4) * 16;                 // threads per half
+    static constexpr int GT3 = (G3 + HT - 1) / HT;            // groups per thread
+    static constexpr int PB3 = G3 * 4;                        // floats per patch buffer
+    static_assert(HT * 4 * 16 <= 4 * PB3, "combine area fits in the patch buffers");
+};
+size_t head3_lds_bytes(int tr, int nchunks) {
+    const size_t w = ((size_t)nchunks * 48 + 63) / 64 * 64;
+    const size_t pb = (size_t)(tr + 2) * (S3 / 4) * 4;
+    return (w + 4 * pb) * sizeof(float);
+}
 
 // TF: each segment is read through its deferred transform a.tf[s] (ffc_in_tf): the producer's
 // BN + activation + NoiseInjection applied as the patch goes to LDS, on in-image groups only (the
 // zero padding belongs to the transformed tensor).  The head is VALU-bound, so GELU uses the
 // branch-free gelu_as below instead of erff (whose two ranges diverge within a wave).
-template <int MM, bool TF>
-__global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a) {
+template <int MM, bool TF, int TR3 = 64>
+__global__ __launch_bounds__(2 * Head3<TR3>::HT) void conv3x3_smallm_kernel(SmallMArgs a) {
+    constexpr int R3 = Head3<TR3>::R3, G3 = Head3<TR3>::G3, HT = Head3<TR3>::HT, GT3 = Head3<TR3>::GT3;
+    constexpr int PB3 = Head3<TR3>::PB3;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int half = threadIdx.x >> 8, tid = threadIdx.x & 255;
+    const int half = threadIdx.x / HT, tid = threadIdx.x % HT;
     int bid = blockIdx.x;
     const int tx = bid % a.ntx;
     bid /= a.ntx;
     const int ty = bid % a.nty;
     const int b = bid / a.nty;
-    const int y0 = ty * T3, x0 = tx * T3;
+    const int y0 = ty * TR3, x0 = tx * T3;
     const int qy = 4 * (tid >> 4), qx = 4 * (tid & 15);   // this thread's 4x4 outputs (tile coords)
     const int M = a.M;
     const int nchunks = a.C[0] + (a.nseg > 1 ? a.C[1] : 0);   // one channel per chunk
     float* wl_all = lds;                                      // [nchunks][4][12]
-    float* pbuf = lds + CMAX3 * 48;                           // [2 buffers][2 halves][PB3]
+    float* pbuf = lds + (nchunks * 48 + 63) / 64 * 64;        // [2 buffers][2 halves][PB3]
 
-    for (int q0 = 0; q0 < nchunks * 48; q0 += 8 * SM_THREADS) {   // 8 loads in flight per thread
+    for (int q0 = 0; q0 < nchunks * 48; q0 += 8 * 2 * HT) {   // 8 loads in flight per thread
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int q = q0 + u * SM_THREADS + threadIdx.x;
+            const int q = q0 + u * 2 * HT + threadIdx.x;
             const int ci = q / 48, m = (q / 12) & 3, t = q % 12;
             const int s = ci < a.C[0] ? 0 : 1;
             const int c = s == 0 ? ci : ci - a.C[0];
@@ -342,13 +359,13 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int q = q0 + u * SM_THREADS + threadIdx.x;
+            const int q = q0 + u * 2 * HT + threadIdx.x;
             if (q < nchunks * 48) wl_all[q] = v[u];
         }
     }
 
     auto inimg = [&](int j) {
-        const int n = j * 256 + tid;
+        const int n = j * HT + tid;
         const int g = n % (S3 / 4), pr = n / (S3 / 4);
         const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
         return n < G3 && (unsigned)iy < (unsigned)a.IH && (unsigned)ix < (unsigned)a.IW;
@@ -359,7 +376,7 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         const float* x = a.x[s] + ((size_t)b * a.C[s] + c) * a.IH * a.IW;
 #pragma unroll
         for (int j = 0; j < GT3; ++j) {
-            const int n = j * 256 + tid;
+            const int n = j * HT + tid;
             const int g = n % (S3 / 4), pr = n / (S3 / 4);
             const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
             r[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -379,7 +396,7 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
                 const float* npl = t.noise ? t.noise + (size_t)b * a.IH * a.IW : nullptr;
 #pragma unroll
                 for (int j = 0; j < GT3; ++j) {
-                    const int n = j * 256 + tid;
+                    const int n = j * HT + tid;
                     const int g = n % (S3 / 4), pr = n / (S3 / 4);
                     const int iy = y0 - 1 + pr, ix = x0 - 4 + 4 * g;
                     nzr[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -414,7 +431,7 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         }
 #pragma unroll
         for (int j = 0; j < GT3; ++j) {
-            const int n = j * 256 + tid;
+            const int n = j * HT + tid;
             if (n < G3) reinterpret_cast<float4*>(dst)[n] = r[j];
         }
     };
@@ -487,14 +504,14 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         __syncthreads();
     }
     // fixed-order combine of the two halves' partial sums (half 1 -> LDS -> half 0 adds)
-    float* part = pbuf;   // 256 threads x MM x 16 floats <= 4 * PB3
+    float* part = pbuf;   // HT threads x MM x 16 floats <= 4 * PB3
     if (half == 1) {
 #pragma unroll
         for (int m = 0; m < MM; ++m)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * 256 + tid] = ACC(m, i, j);
+                for (int j = 0; j < 4; ++j) part[((m * 4 + i) * 4 + j) * HT + tid] = ACC(m, i, j);
     }
     __syncthreads();
     if (half == 1) return;
@@ -504,8 +521,8 @@ __global__ __launch_bounds__(SM_THREADS) void conv3x3_smallm_kernel(SmallMArgs a
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int jp = 0; jp < 2; ++jp)
-                acc2[m][i][jp] += f2{part[((m * 4 + i) * 4 + 2 * jp) * 256 + tid],
-                                     part[((m * 4 + i) * 4 + 2 * jp + 1) * 256 + tid]};
+                acc2[m][i][jp] += f2{part[((m * 4 + i) * 4 + 2 * jp) * HT + tid],
+                                     part[((m * 4 + i) * 4 + 2 * jp + 1) * HT + tid]};
     const int oy0 = y0 + qy, ox0 = x0 + qx;
     const bool xin = ox0 + 3 < a.IW;
     auto store = [&](auto actf) {
@@ -652,7 +669,13 @@ static int conv3x3_smallm_launch(const float* x0, int C0, const float* w0, const
     a.IH = H;
     a.IW = W;
     a.M = M;
-    a.nty = (H + T3 - 1) / T3;
+    // tile rows: 32 (two workgroups per CU; measured: fgan128 B = 512 head 2.25 -> 2.11 ms, B = 64 neutral,
+    // profiles/r02/s15); FFC_HEAD_TR=64 restores the full-height tile for A/B runs
+    static const int tr = [] {
+        const char* e = std::getenv("FFC_HEAD_TR");
+        return e && std::atoi(e) == 64 ? 64 : 32;
+    }();
+    a.nty = (H + tr - 1) / tr;
     a.ntx = (W + T3 - 1) / T3;
     a.act = act;
     a.act_param = act_param;
@@ -668,26 +691,33 @@ static int conv3x3_smallm_launch(const float* x0, int C0, const float* w0, const
                       "ffc_conv3x3_smallm_tf: noise not 16-B aligned");
         a.tf[s] = t ? *t : none;
     }
-    const size_t lds = (CMAX3 * 48 + 4 * (size_t)PB3) * sizeof(float);
+    const int nchunks = C0 + (x1 ? C1 : 0);
+    const size_t lds = head3_lds_bytes(tr, nchunks);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
     typedef void (*C3Kernel)(SmallMArgs);
-    static const C3Kernel kernels[2][4] = {
-        {conv3x3_smallm_kernel<1, false>, conv3x3_smallm_kernel<2, false>, conv3x3_smallm_kernel<3, false>,
-         conv3x3_smallm_kernel<4, false>},
-        {conv3x3_smallm_kernel<1, true>, conv3x3_smallm_kernel<2, true>, conv3x3_smallm_kernel<3, true>,
-         conv3x3_smallm_kernel<4, true>}};
-    auto k = kernels[tf ? 1 : 0][M - 1];
-    static bool raised[2][5] = {};
-    if (!raised[tf][M]) {
+    static const C3Kernel kernels[2][2][4] = {
+        {{conv3x3_smallm_kernel<1, false>, conv3x3_smallm_kernel<2, false>, conv3x3_smallm_kernel<3, false>,
+          conv3x3_smallm_kernel<4, false>},
+         {conv3x3_smallm_kernel<1, true>, conv3x3_smallm_kernel<2, true>, conv3x3_smallm_kernel<3, true>,
+          conv3x3_smallm_kernel<4, true>}},
+        {{conv3x3_smallm_kernel<1, false, 32>, conv3x3_smallm_kernel<2, false, 32>,
+          conv3x3_smallm_kernel<3, false, 32>, conv3x3_smallm_kernel<4, false, 32>},
+         {conv3x3_smallm_kernel<1, true, 32>, conv3x3_smallm_kernel<2, true, 32>, conv3x3_smallm_kernel<3, true, 32>,
+          conv3x3_smallm_kernel<4, true, 32>}}};
+    const int ti = tr == 32 ? 1 : 0;
+    auto k = kernels[ti][tf ? 1 : 0][M - 1];
+    static bool raised[2][2][5] = {};
+    if (!raised[ti][tf][M]) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess) {
             ffc::set_error("ffc_conv3x3_smallm: hipFuncSetAttribute failed");
             return FFC_E_LAUNCH;
         }
-        raised[tf][M] = true;
+        raised[ti][tf][M] = true;
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(SM_THREADS), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(tr == 32 ? 2 * Head3<32>::HT : 2 * Head3<64>::HT), lds,
+                       (hipStream_t)stream, a);
     return ffc::launch_status("ffc_conv3x3_smallm");
 }
 
