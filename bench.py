@@ -46,6 +46,8 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from fastfourierconvolution_amd.graphs import capture_step  # noqa: E402  (no GPU touched at import)
+
 METRIC = "FFC-generator fwd images/sec @ B=256 64×64×3; % HBM roofline; max |Δ| vs ref"
 PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (v_mfma_f32_32x32x2_f32) dense peak
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -242,22 +244,10 @@ def train_main(args):
         # whole-step capture (forward, custom-op backward, Adam): the library launches allocate
         # nothing and never sync, plans / packed-weight buffers exist after the eager warm-up, and
         # the weight re-packs the optimizer's in-place updates trigger are captured with the step
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(max(2, args.warmup)):
-                step()
-        torch.cuda.current_stream().wait_stream(s)
-        try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                step()
+        graph = capture_step(step, warmup=max(2, args.warmup))
+        use_graph = graph is not None
+        if use_graph:
             run = graph.replay
-            run()
-        except Exception as e:  # capture unsupported here: time eagerly, say so
-            print(f"[bench] graph capture failed ({e}); timing eagerly", file=sys.stderr)
-            use_graph = False
-            run = step
     for _ in range(max(1, args.warmup)):
         run()
     torch.cuda.synchronize()
@@ -472,27 +462,12 @@ def main():
     use_graph = not args.no_graph
     run = step
     if use_graph:
-        try:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                step()
-            torch.cuda.current_stream().wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.no_grad(), torch.cuda.graph(graph):
-                step()
+        # thread-local capture after a synchronise, and every rank agrees on graph vs eager BEFORE
+        # the first replay (graphs.py: the RCCL watchdog and the round-2 exit 134)
+        graph = capture_step(step, warmup=1)
+        use_graph = graph is not None
+        if use_graph:
             run = graph.replay
-            run()
-            torch.cuda.synchronize()
-        except Exception as e:  # capture unsupported here: time eagerly, say so
-            print(f"[bench] graph capture failed ({e}); timing eagerly", file=sys.stderr)
-            use_graph = False
-            run = step
-        if world > 1:   # every rank must replay the same collectives: agree on graph vs eager
-            ok = torch.tensor([1 if use_graph else 0], device=dev, dtype=torch.int32)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            if use_graph and ok.item() == 0:
-                use_graph, run = False, step
 
     if world > 1:
         dist.barrier()

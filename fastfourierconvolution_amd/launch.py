@@ -2,8 +2,8 @@
 
 The reference's only multi-GPU path is ``nn.DataParallel`` (train_cond.py:66-68, one thread per
 GPU in one process).  Here every GPU gets its own process, as ``torch.distributed.run`` would
-start them: the parent never touches the GPU (``torch.cuda.device_count()`` does not initialise
-HIP on this image), starts N fresh children with RANK / LOCAL_RANK / WORLD_SIZE /
+start them: the parent never touches the GPU (``visible_gpus`` reads the KFD topology from
+sysfs, no HIP call; tests/test_gpu_launch.py checks /dev/kfd stays closed), starts N fresh children with RANK / LOCAL_RANK / WORLD_SIZE /
 LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, waits for all of them and exits with the first
 failing child's status (the others are terminated by PID).  No exec of the parent, so nothing
 replaces a process that has initialised the GPU.
@@ -16,7 +16,7 @@ import subprocess
 import sys
 import time
 
-__all__ = ["free_port", "rank_env", "spawn_ranks", "visible_gpus"]
+__all__ = ["free_port", "kfd_gpus", "rank_env", "spawn_ranks", "visible_gpus"]
 
 
 def free_port() -> int:
@@ -25,10 +25,64 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def visible_gpus() -> int:
-    """GPUs this process could use, counted without initialising HIP."""
-    import torch
-    return torch.cuda.device_count()
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _visible_filter(n: int, var: str) -> int:
+    """Apply one ``*_VISIBLE_DEVICES`` list to ``n`` enumerated devices: unset keeps all, an
+    empty string hides all, otherwise the entries that name a device (an index < n, or a
+    ``GPU-<uuid>`` ROCr accepts) up to the first invalid one, as the runtimes parse it."""
+    v = os.environ.get(var)
+    if v is None:
+        return n
+    k = 0
+    for tok in (t.strip() for t in v.split(",")):
+        if tok.startswith("GPU-") and var == "ROCR_VISIBLE_DEVICES":
+            k += 1
+        elif tok.isdigit() and int(tok) < n:
+            k += 1
+        else:
+            break
+    return min(k, n)
+
+
+def kfd_gpus(nodes_dir: str = KFD_NODES) -> int:
+    """GPU agents in the KFD topology (nodes with a non-zero ``gpu_id``) whose render node this
+    process may open -- what ROCr will enumerate -- read from sysfs only."""
+    try:
+        names = os.listdir(nodes_dir)
+    except OSError:
+        return 0
+    n = 0
+    for name in names:
+        d = os.path.join(nodes_dir, name)
+        try:
+            with open(os.path.join(d, "gpu_id")) as f:
+                if int(f.read().strip() or "0") == 0:
+                    continue                     # CPU node
+            minor = None
+            with open(os.path.join(d, "properties")) as f:
+                for line in f:
+                    key, _, val = line.partition(" ")
+                    if key == "drm_render_minor":
+                        minor = int(val)
+        except (OSError, ValueError):
+            continue
+        if minor is not None and minor > 0 and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            continue                             # present on the host, not granted to this process
+        n += 1
+    return n
+
+
+def visible_gpus(nodes_dir: str = KFD_NODES) -> int:
+    """GPUs this process could use, counted WITHOUT any HIP / HSA call (so a parent that spawns
+    the ranks never opens /dev/kfd: ``torch.cuda.device_count()`` falls back to hipGetDeviceCount
+    when amdsmi discovery fails).  KFD topology, then ROCR_, HIP_ and CUDA_VISIBLE_DEVICES in the
+    order the ROCm stack applies them."""
+    n = kfd_gpus(nodes_dir)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        n = _visible_filter(n, var)
+    return n
 
 
 def rank_env(rank: int, world: int, port: int, base: dict | None = None) -> dict:

@@ -43,15 +43,15 @@ def test_rccl_moments_all_reduce_in_graph(rccl_world1):
     D.merge_moments(m)
     torch.cuda.synchronize()
     assert torch.equal(m, ref)
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        D.merge_moments(m)
-    torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    from fastfourierconvolution_amd.graphs import capture_step
+
+    def step():
         m.mul_(2.0)
         D.merge_moments(m)
+    # warm-up on a side stream, synchronise, thread-local capture, ranks agree (graphs.py): an
+    # eager all-reduce right before a global-mode capture is what aborted once in round 2
+    g = capture_step(step, warmup=0)
+    assert g is not None
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(m, ref * 2)      # capture records without running: one replayed mul + all-reduce
@@ -86,14 +86,14 @@ def test_syncbn_generator_graph_over_rccl(rccl_world1):
         torch.testing.assert_close(eager, ref, rtol=1e-6, atol=1e-6)
         for k, v in ref_state.items():
             torch.testing.assert_close(G.state_dict()[k], v, rtol=1e-6, atol=1e-7, msg=k)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            G(z)
-        torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            out = G(z)
+        from fastfourierconvolution_amd.graphs import capture_step
+        res = {}
+
+        def step():
+            res["out"] = G(z)
+        graph = capture_step(step, warmup=1)
+        assert graph is not None
+        out = res["out"]
         graph.replay()
         torch.cuda.synchronize()
     torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
