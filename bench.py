@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — FFC-DCGAN generator forward throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gen64|fgan128|fgan128sn|gan64train]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gen64|fgan128|fgan128sn|gan64train|block]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 `--gpus N` without a launcher (WORLD_SIZE unset) starts the N ranks itself
@@ -16,14 +16,15 @@ use batch statistics), synthetic z ~ N(0,1), weights from the reference's weight
 (fgan64_complete.py:22-31: conv N(0, 0.02), BN gamma N(1, 0.02), beta 0).
 One step = one generator forward over one batch; inputs resident in HBM.
 
-Scaling (``--scaling``, default strong): the global batch BASELINE.json names for the workload
-(gen64 256, fgan128 512 = configs[3], fgan128sn 1024 = configs[4]) is split over the N ranks
-(distributed.shard_range; z drawn once from the global seed and sliced), so every N measures the
-same job ("scaling": "strong").  ``--scaling weak`` keeps ``--batch`` samples per GPU instead.
-One process per GPU; train-mode BN statistics are all-reduced over RCCL (SyncBN: the sharded
-result equals the global-batch forward); weights are broadcast once at init.  The step is
-hipGraph-captured (the RCCL all-reduces inside the graph).  At N > 1 the gen64 line also carries
-the gathered global-batch output's parity against the CPU reference.
+Scaling (``--scaling``, default weak): every GPU runs the configuration's batch (gen64 256,
+fgan128 512 = configs[3], fgan128sn 1024 = configs[4]); the job's global batch is N x that, drawn
+once from one seed and sliced per rank, and train-mode BN normalises over ALL of it (SyncBN: the
+BN moments are all-reduced over RCCL, so the sharded result equals the global-batch forward).
+``--scaling strong`` splits the configuration's batch over the ranks instead (the per-rank
+shard steps and the strong-scaling budget are in DESIGN.md §5).  One process per GPU; weights are
+broadcast once at init.  The step is hipGraph-captured (thread-local capture, the RCCL
+all-reduces inside the graph; graphs.py).  At N > 1 the gen64 line also carries the gathered
+global-batch output's parity against the CPU reference.
 
 The JSON line also carries:
   roofline      live per-kernel HIP-event timing of one eager pass (dominant kernel), MFMA f32 peak
@@ -70,13 +71,42 @@ def mfma_roof(dom, achieved):
     return r
 
 
+def time_steps(run, steps, world=1):
+    """Time EXACTLY ``steps`` calls of ``run`` between a barrier + device synchronise on both sides
+    (wall clock, max over ranks), with a HIP event after every step on the launch stream for the
+    per-step median (SURVEY.md §8d asks for the median).  -> (elapsed_s, median_ms_per_step)"""
+    import torch.distributed as dist
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i in range(steps):
+        run()
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    med = per[len(per) // 2] if steps % 2 else 0.5 * (per[steps // 2 - 1] + per[steps // 2])
+    if world > 1:
+        t = torch.tensor([elapsed, med], device=torch.device("cuda", torch.cuda.current_device()),
+                         dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, med = float(t[0]), float(t[1])
+    return elapsed, med
+
+
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn", "gan64train"], default="gen64",
+    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn", "gan64train", "block"], default="gen64",
                    help="gen64: FFCGenerator 64x64 (BASELINE metric, configs[1]/[2]); "
                         "fgan128: fgan128 FGenerator 128x128x3 (configs[3], 64 per GPU = B 512 / 8); "
                         "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4], 128 per GPU); "
-                        "gan64train: generator + discriminator 64x64x3 fwd+bwd + Adam (configs[2], B=256)")
+                        "gan64train: generator + discriminator 64x64x3 fwd+bwd + Adam (configs[2], B=256); "
+                        "block: one FFC_BN_ACT 32->32 at 32x32, B=16 (configs[0])")
     p.add_argument("--mix", choices=["fp32", "fp16"], default=None,
                    help="spectral mix arithmetic (default: fp16 for fgan128sn, fp32 otherwise)")
     p.add_argument("--gpus", type=int, default=None,
@@ -84,12 +114,14 @@ def parse():
                         "WORLD_SIZE is unset")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
-                   help="strong: the workload's global batch split over the ranks; weak: --batch per GPU")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="weak",
+                   help="weak (default): every GPU runs the configuration's batch (gen64 256, fgan128 512, "
+                        "fgan128sn 1024), global batch = N x that, SyncBN over all of it; strong: the "
+                        "configuration's batch split over the ranks")
     p.add_argument("--global-batch", type=int, default=None,
                    help="strong scaling global batch (gen64: 256, fgan128: 512, fgan128sn: 1024)")
     p.add_argument("--batch", type=int, default=None, help="weak scaling samples per GPU (gen64: 256, "
-                                                           "fgan128: 64, fgan128sn: 128)")
+                                                           "fgan128: 512, fgan128sn: 1024)")
     p.add_argument("--dry-run", action="store_true",
                    help="launch + shard plan only, over gloo on the CPU (no GPU touched): rank 0 prints the plan")
     p.add_argument("--nz", type=int, default=100)
@@ -176,10 +208,11 @@ def fgan_cpu_baseline(args, G, z_cpu, sn):
 
 
 def sharded_parity(args, step, cpu_state, z_glob, global_batch, rank):
-    """N > 1 (gen64, strong scaling): one more sharded forward on every rank, outputs gathered to
-    the global batch (all_gather over RCCL), compared on rank 0 with the fp32 CPU reference path
-    run on the global z.  In train mode this checks the SyncBN all-reduces end to end: a naive
-    shard differs from the global-batch forward by ~3e-1 normwise."""
+    """N > 1 (gen64, train-mode BN; every rank calls it): one more sharded forward on every rank,
+    outputs gathered to the global batch (all_gather over RCCL), compared on rank 0 with the fp32
+    CPU reference path run on the global z.  This checks the SyncBN all-reduces end to end: a naive
+    shard differs from the global-batch forward by ~3e-1 normwise.  (Eval mode
+    needs the GPU's running stats and no collective: the caller skips it on every rank.)"""
     from fastfourierconvolution_amd.distributed import gather_batch
     out = gather_batch(step().contiguous(), global_batch)
     if rank != 0:
@@ -189,8 +222,6 @@ def sharded_parity(args, step, cpu_state, z_glob, global_batch, rank):
     with torch.no_grad():
         ref = ffc_generator(z_glob, {k: v.clone() for k, v in cpu_state.items()}, args.nz, args.nc, args.ngf,
                             args.bn_mode == "train", fft="torch")
-    if args.bn_mode != "train":
-        return None    # eval parity needs the GPU's running stats; the train-mode check is the SyncBN one
     return {"normwise_err_vs_cpu_ref": normwise_err(out.cpu(), ref), "mode": f"train, global B={global_batch}, "
             "sharded + SyncBN, outputs gathered", "tolerance": 1e-4}
 
@@ -250,12 +281,7 @@ def train_main(args):
             run = graph.replay
     for _ in range(max(1, args.warmup)):
         run()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed, med = time_steps(run, args.steps)
     value = args.batch * args.steps / elapsed
     obs = rt.LaunchObserver()
     rt.set_observer(obs)
@@ -315,7 +341,8 @@ def train_main(args):
     line = {
         "metric": "FFC-DCGAN G+D fwd+bwd train step images/sec @ B=256 64x64x3 (BASELINE configs[2])",
         "value": round(value, 1), "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "ms_per_step_median": round(med, 4),
+        "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
         "config": {"workload": f"FFCGenerator(nz={args.nz},nc={args.nc},ngf={args.ngf}) + FFCDiscriminator("
@@ -327,8 +354,104 @@ def train_main(args):
     print(json.dumps(line))
 
 
-GLOBAL_BATCH = {"gen64": 256, "fgan128": 512, "fgan128sn": 1024}   # BASELINE.json configs[1..4]
-WEAK_BATCH = {"gen64": 256, "fgan128": 64, "fgan128sn": 128}
+BLOCK_CFG = dict(in_channels=32, out_channels=32, kernel_size=3, ratio_gin=0.5, ratio_gout=0.5, stride=1, padding=1,
+                 norm_layer="BatchNorm2d", activation_layer="ReLU")
+
+
+def block_main(args):
+    """BASELINE configs[0]: one FFC_BN_ACT(32, 32, 3, 0.5, 0.5, stride 1, padding 1, BatchNorm2d, ReLU)
+    block (layers/ffc/ffc_bn_act.py:25-83), x = (x_l, x_g) ~ N(0,1)^(16,16,32,32) each (SURVEY.md
+    §8d cfg1: seed 0), train-mode BN.  One step = one block forward over the batch of 16 samples.
+    The reference quotes this configuration on its CPU path; the same CPU restatement is timed
+    beside the GPU (cpu_baseline), and the GPU output is checked against it (parity)."""
+    import torch.nn as nn
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import _runtime as rt
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("block is the single-device configs[0] workload")
+    B = args.batch or 16
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    with contextlib.redirect_stdout(io.StringIO()):
+        blk = F.FFC_BN_ACT(32, 32, 3, 0.5, 0.5, stride=1, padding=1, norm_layer=nn.BatchNorm2d,
+                           activation_layer=nn.ReLU)
+    blk.apply(weights_init)
+    cpu_state = {k: v.clone() for k, v in blk.state_dict().items()}
+    blk = blk.to(dev).train(args.bn_mode == "train")
+    g = torch.Generator().manual_seed(0)
+    x_cpu = (torch.randn((B, 16, 32, 32), generator=g), torch.randn((B, 16, 32, 32), generator=g))
+    x = tuple(t.to(dev) for t in x_cpu)
+
+    def step():
+        with torch.no_grad():
+            return blk(x)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    use_graph, run = not args.no_graph, step
+    if use_graph:
+        graph = capture_step(step, warmup=1)
+        use_graph = graph is not None
+        if use_graph:
+            run = graph.replay
+    for _ in range(max(1, args.warmup)):
+        run()
+    elapsed, med = time_steps(run, args.steps)
+    value = B * args.steps / elapsed
+    obs = rt.LaunchObserver()
+    rt.set_observer(obs)
+    for _ in range(max(1, args.profile_steps)):
+        step()
+    rt.set_observer(None)
+    summ = obs.summary()
+    nprof = max(1, args.profile_steps)
+    kernels = {k: {"launches_per_step": v["launches"] / nprof, "ms_per_step": v["ms"] / nprof,
+                   "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
+    mm = {k: v for k, v in summ.items() if v["flops"] > 0}
+    dom = max(mm, key=lambda k: mm[k]["ms"])
+    roof = mfma_roof(dom, mm[dom]["flops"] / (mm[dom]["ms"] * 1e-3) / 1e12)
+    roof["traffic"] = None
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        from oracle.ffc_oracle import ffc_bn_act, normwise_err
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        training = args.bn_mode == "train"
+        sd = {k: v.clone() for k, v in cpu_state.items()}
+        if not training:
+            sd = {k: v.detach().cpu().clone() for k, v in blk.state_dict().items()}
+        with torch.no_grad():
+            ref = ffc_bn_act(x_cpu, sd, "", BLOCK_CFG, training, fft="torch")
+            iters, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < args.cpu_seconds or iters == 0:
+                ffc_bn_act(x_cpu, sd, "", BLOCK_CFG, training, fft="torch")
+                iters += 1
+            el = time.perf_counter() - t0
+            got = step()
+        ref_cat, got_cat = torch.cat(ref, 1), torch.cat([t.cpu() for t in got], 1)
+        sd64 = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+        ref64 = torch.cat(ffc_bn_act(tuple(t.double() for t in x_cpu), sd64, "", BLOCK_CFG, training), 1)
+        parity = {"normwise_err_vs_cpu_ref": normwise_err(got_cat, ref_cat),
+                  "normwise_err_vs_fp64_oracle": normwise_err(got_cat, ref64), "tolerance": 1e-4}
+        cpu = {"value": round(B * iters / el, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+               "sample": f"oracle fp32 torch-CPU FFC_BN_ACT fwd (op-for-op reference path), B={B}, {iters} "
+                         f"iterations in {el:.1f}s, {args.bn_mode}-mode BN"}
+    print(json.dumps({
+        "metric": "FFC_BN_ACT(32->32, k3, 0.5/0.5, BN, ReLU) fwd samples/sec @ B=16 32x32 (BASELINE configs[0])",
+        "value": round(value, 1), "unit": "samples/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "ms_per_step_median": round(med, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: x ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",
+        "config": {"workload": "FFC_BN_ACT(32,32,3,0.5,0.5,stride=1,padding=1,BatchNorm2d,ReLU) forward 32x32",
+                   "global_batch": B, "per_gpu_batch": B, "bn_mode": args.bn_mode, "hipgraph": use_graph,
+                   "parallelism": "dp1"},
+        "roofline": roof, "cpu_baseline": cpu, "parity": parity, "kernels": kernels}))
+
+
+GLOBAL_BATCH = {"gen64": 256, "fgan128": 512, "fgan128sn": 1024,   # BASELINE.json configs[1..4]
+                "gan64train": 256, "block": 16}                     # configs[2], configs[0] (one device)
+WEAK_BATCH = dict(GLOBAL_BATCH)   # weak scaling: each GPU runs the configuration's whole batch
 
 
 def ranks_or_launch(args):
@@ -404,6 +527,10 @@ def main():
     world, rank, local = ranks_or_launch(args)
     if args.dry_run:
         return dry_run(args, world, rank)
+    if args.workload == "block":
+        if world > 1:
+            raise SystemExit("block is the single-device configs[0] workload")
+        return block_main(args)
     if args.workload == "gan64train":
         if world > 1:
             raise SystemExit("gan64train is the single-GPU configs[2] workload")
@@ -441,14 +568,11 @@ def main():
         D.broadcast_module(G)           # weights + BN buffers from rank 0, once
         if args.bn_mode == "train":
             D.enable_sync_bn()          # the only data-path exchange: BN moments all-reduce
-    if args.scaling == "strong":      # one global z (same seed for every N), this rank's slice
-        gen = torch.Generator(device="cpu").manual_seed(100)
-        z_glob = torch.randn((global_batch, 128) if fgan else (global_batch, args.nz, 1, 1), generator=gen)
-        z_cpu = z_glob[b0:b1].clone()
-    else:
-        gen = torch.Generator(device="cpu").manual_seed(100 + rank)
-        z_glob = None
-        z_cpu = torch.randn((args.batch, 128) if fgan else (args.batch, args.nz, 1, 1), generator=gen)
+    # one global z from one seed (weak or strong), this rank's slice: at N = 1 both modes time the
+    # same batch, and at N > 1 the gathered output can be checked against the global-batch forward
+    gen = torch.Generator(device="cpu").manual_seed(100)
+    z_glob = torch.randn((global_batch, 128) if fgan else (global_batch, args.nz, 1, 1), generator=gen)
+    z_cpu = z_glob[b0:b1].clone()
     z = z_cpu.to(dev)
 
     def step():
@@ -469,20 +593,9 @@ def main():
         if use_graph:
             run = graph.replay
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(max(1, args.warmup)):
         run()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed, med = time_steps(run, args.steps, world)
     value = global_batch * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
@@ -514,14 +627,23 @@ def main():
     if fu:
         b = sum(v["bytes"] for v in fu.values())
         ms = sum(v["ms"] for v in fu.values())
+        mv = sum(v["moved"] for v in fu.values())
         fft_roof = {"kernel": "+".join(fu), "bound": "hbm", "achieved": round(b / (ms * 1e-3) / 1e9, 1),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                    "algorithmic_bytes_per_step": b / max(1, args.profile_steps)}
+                    "basis": "SURVEY.md §8d algorithmic bytes: fused train FU 12*N_r, R2C 4*N_r + 8*N_c, "
+                             "C2R 8*N_c + 4*N_r (no spill counted)",
+                    "algorithmic_bytes_per_step": b / max(1, args.profile_steps),
+                    "moved_bytes_per_step": mv / max(1, args.profile_steps),
+                    "moved_frac": round(mv / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "ms_per_step": round(ms / max(1, args.profile_steps), 4),
+                    "per_stage": {k: {"us_per_launch": round(1e3 * v["ms"] / v["launches"], 2),
+                                      "frac": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+                                  for k, v in fu.items()}}
 
     # ---- CPU baseline + parity (rank 0, N=1 only); N > 1: the gathered sharded output (SyncBN)
     cpu = None
     parity = None
-    if world > 1 and not fgan and args.scaling == "strong" and not args.no_cpu_baseline:
+    if world > 1 and not fgan and args.bn_mode == "train" and not args.no_cpu_baseline:
         parity = sharded_parity(args, step, cpu_state, z_glob, global_batch, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and fgan:
         cpu, parity = fgan_cpu_baseline(args, G, z_cpu, sn)
@@ -552,7 +674,8 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step_median": round(med, 4), "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None,
             "dtype": "f32" if args.mix == "fp32" else "f32 (fp16 spectral mix)",
             "data": "synthetic: z ~ N(0,1); weights per fgan64_complete.py:22-31 weights_init",

@@ -50,11 +50,12 @@ class LaunchObserver:
         torch.cuda.synchronize()
         agg = {}
         for label, e0, e1, work in self.records:
-            a = agg.setdefault(label, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            a = agg.setdefault(label, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "moved": 0.0})
             a["launches"] += 1
             a["ms"] += e0.elapsed_time(e1)
             a["flops"] += work.get("flops", 0.0)
             a["bytes"] += work.get("bytes", 0.0)
+            a["moved"] += work.get("moved", work.get("bytes", 0.0))
         return agg
 
 

@@ -266,14 +266,23 @@ class _FFCExec:
         # ones (untuned shapes), rebuild them on the costliest job's (cached: happens once)
         qi = [i for i, jb in enumerate(jobs) if jb[0].launch_key[0] == "q"]
         if len({jobs[i][0].launch_key for i in qi}) > 1:
-            cfg = max((jobs[i][0].plan for i in qi), key=_plan.convq_cost).cfg
+            # the decision is cached per layer shape, including "this job cannot take that cfg" (it
+            # stays on its own kernel): nothing is re-planned or re-packed on later forwards
             cache = self._ffc_cache()
-            for i in qi:
-                ckey, cB, cM, csegs, cw = built[i]
-                ex2 = rt.ConvExec(cB, cM, csegs, cw, dev, convq_cfg=cfg)
-                if ex2.launch_key[0] == "q":
-                    cache[ckey] = ex2
-                    jobs[i] = (ex2,) + jobs[i][1:]
+            rkey = ("rebuild",) + tuple(built[i][0] for i in qi)
+            dec = cache.get(rkey)
+            if dec is None:
+                cfg = max((jobs[i][0].plan for i in qi), key=_plan.convq_cost).cfg
+                dec = {}
+                for i in qi:
+                    ckey, cB, cM, csegs, cw = built[i]
+                    ex2 = rt.ConvExec(cB, cM, csegs, cw, dev, convq_cfg=cfg)
+                    if ex2.launch_key[0] == "q":
+                        cache[ckey] = dec[i] = ex2
+                cache[rkey] = dec
+            for i, ex2 in dec.items():
+                ex2.ensure_packed(built[i][4])
+                jobs[i] = (ex2,) + jobs[i][1:]
         groups = {}
         for jb in jobs:
             groups.setdefault(jb[0].launch_key, []).append(jb)

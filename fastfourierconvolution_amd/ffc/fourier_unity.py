@@ -89,7 +89,11 @@ class FourierUnitSN(nn.Module):
             slab = torch.empty((B, 2 * C, 4), device=dev, dtype=torch.float32)
             # pass 0 keeps its mix output Y for pass 1 (no second row R2C + column FFT + mix)
             yspill = torch.empty(int(n_y), device=dev, dtype=torch.float32) if rt.FU_SPILL else None
-            with rt.observe("fu_pass0", bytes=4.0 * n_r + (4.0 * n_y if rt.FU_SPILL else 0.0)):
+            # bytes: SURVEY.md §8d's algorithmic basis (fused train FU = 12*N_r: x read in each pass,
+            # out written once); moved: what this kernel pair actually streams (t at the pre-upsample
+            # size, the Y spill written and read back)
+            with rt.observe("fu_pass0", bytes=4.0 * n_r,
+                            moved=4.0 * t.numel() + (4.0 * n_y if rt.FU_SPILL else 0.0)):
                 check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
                                           None if in_fold else ptr(in_shift), int(in_relu), ptr(mixT), 0, ptr(slab),
                                           None, None, 0, None, ctypes.byref(in_fold.struct) if in_fold else None,
@@ -104,7 +108,9 @@ class FourierUnitSN(nn.Module):
                 in_scale, in_shift = in_fold.materialize(stream)
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
-        with rt.observe("fu_pass1", bytes=(4.0 * n_y + 4.0 * n_r if yspill is not None else 4.0 * n_r) + 4.0 * n_r):
+        with rt.observe("fu_pass1", bytes=8.0 * n_r,
+                        moved=(4.0 * n_y if yspill is not None else 4.0 * t.numel()) + 4.0 * t.numel() * bool(residual)
+                        + 4.0 * n_r):
             check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT), 1,
                                       None, ptr(sc), ptr(sh), int(residual), ptr(out), None,
                                       ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), stream),
@@ -136,11 +142,13 @@ class FourierUnitSN(nn.Module):
         nY = B * C * H * (W // 2 + 1)           # complex bins of Y
         mix_flops = 2.0 * (2 * C) ** 2 * (B * H * (W // 2 + 1))   # (2C x 2C) GEMM over every bin
         T = torch.empty((B, C, h, w // 2 + 1, 2), device=dev, dtype=torch.float32)
-        with rt.observe("fu2d_r2c", bytes=4.0 * t.numel() + 8.0 * nT):
+        n_r, n_c = float(B * C * H * W), float(B * C * H * (W // 2 + 1))   # SURVEY.md §8d, full resolution
+        with rt.observe("fu2d_r2c", bytes=4.0 * n_r + 8.0 * n_c, moved=4.0 * t.numel() + 8.0 * nT):
             check(L.ffc_fu2d_r2c(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(T), stream),
                   "ffc_fu2d_r2c")
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
-        c2r_bytes = 8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)
+        c2r_bytes = 8.0 * n_c + 4.0 * n_r                                   # SURVEY.md §8d C2R pass
+        c2r_moved = 8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)
         if use_batch:
             rows = L.ffc_fu2d_slab_rows(B, C, H, W)
             slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
@@ -152,7 +160,7 @@ class FourierUnitSN(nn.Module):
                       "ffc_fu2d_mix(pass 0)")
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
             if Y is not None:
-                with rt.observe("fu2d_c2r", bytes=c2r_bytes):
+                with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):
                     check(L.ffc_fu2d_c2r_bn(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
                                             int(in_relu), int(residual), ptr(sc), ptr(sh), ptr(out), stream),
                           "ffc_fu2d_c2r_bn")
@@ -165,7 +173,7 @@ class FourierUnitSN(nn.Module):
             with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
                 check(L.ffc_fu2d_mix_cols(ptr(T), B, C, H, W, up, ptr(mixT), int(f16), ptr(sc), ptr(sh), ptr(Yc),
                                           stream), "ffc_fu2d_mix_cols")
-            with rt.observe("fu2d_c2r", bytes=c2r_bytes):
+            with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):
                 check(L.ffc_fu2d_c2r_rows(ptr(Yc), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
                                           int(in_relu), int(residual), ptr(out), stream), "ffc_fu2d_c2r_rows")
             return out
@@ -173,7 +181,7 @@ class FourierUnitSN(nn.Module):
         with rt.observe("fu2d_mix1", flops=mix_flops, bytes=8.0 * nT + 8.0 * nY):
             check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 1, None, ptr(sc), ptr(sh), ptr(Y), stream),
                   "ffc_fu2d_mix(pass 1)")
-        with rt.observe("fu2d_c2r", bytes=c2r_bytes):
+        with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):
             check(L.ffc_fu2d_c2r(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift), int(in_relu),
                                  int(residual), ptr(out), stream), "ffc_fu2d_c2r")
         return out

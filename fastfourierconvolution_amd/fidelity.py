@@ -8,9 +8,11 @@ scope (tier framing: no network, not on the hot path).
 
   * ``random_normal``      torch_fidelity/noise.py:8-9      (numpy RandomState.randn -> float32)
   * ``GenerativeModelModuleWrapper``  torch_fidelity/generative_model_modulewrapper.py:10-68
-                           (argument checks, eval mode, optional .cuda()); ``FFCGenerator`` takes
-                           4-D noise (B, nz, 1, 1) (models/ffc_generator.py:30) while the caller
-                           draws 2-D (B, z_size): the wrapper reshapes for 4-D generators
+                           (argument checks, eval mode, optional .cuda()).  torch_fidelity itself
+                           passes the 2-D noise (B, z_size) through unchanged; ``FFCGenerator``
+                           takes 4-D noise (B, nz, 1, 1) (models/ffc_generator.py:30), so this
+                           wrapper has an explicit ``noise_4d`` argument (default: True exactly
+                           for ``FFCGenerator`` instances) -- an extension, not reference behaviour
   * ``generate_batches``   torch_fidelity/utils.py:160-208 without the feature extractor: batches
                            of ``batch_size`` (default 64, defaults.py:5), RandomState(rng_seed)
                            (default 2020, defaults.py:56), ``torch.no_grad()``, the last batch ragged
@@ -40,7 +42,7 @@ class GenerativeModelModuleWrapper(nn.Module):
     ValueError where torch_fidelity's ``vassert`` raises.  Only the "normal" noise source is on the
     reference's path (fgan_complete.py passes ``args.z_type`` = "normal")."""
 
-    def __init__(self, module, z_size, z_type="normal", num_classes=0, make_eval=True, cuda=None):
+    def __init__(self, module, z_size, z_type="normal", num_classes=0, make_eval=True, cuda=None, noise_4d=None):
         super().__init__()
         if not isinstance(module, nn.Module):
             raise ValueError("Not an instance of torch.nn.Module")
@@ -56,8 +58,12 @@ class GenerativeModelModuleWrapper(nn.Module):
         if cuda is not None:
             self.module = self.module.cuda() if cuda else self.module.cpu()
         self.z_size, self.z_type, self.num_classes = z_size, z_type, num_classes
-        # FFCGenerator's first layer is a ConvTranspose2d on a 1x1 input: it takes (B, nz, 1, 1)
-        self._noise_4d = hasattr(module, "ffc0") and not hasattr(module, "noise_to_feature")
+        # FFCGenerator's first layer is a ConvTranspose2d on a 1x1 input: it takes (B, nz, 1, 1);
+        # torch_fidelity proper would hand it the 2-D noise unchanged (noise_4d=False)
+        if noise_4d is None:
+            from .models import FFCGenerator
+            noise_4d = isinstance(module, FFCGenerator)
+        self._noise_4d = bool(noise_4d)
 
     def forward(self, z):
         if self._noise_4d and z.dim() == 2:

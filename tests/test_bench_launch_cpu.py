@@ -3,8 +3,8 @@
 `python bench.py --gpus N` starts N ranks itself (fastfourierconvolution_amd/launch.py) when no
 launcher set WORLD_SIZE; `--dry-run` runs the launch and the batch plan without a GPU.  These
 tests check that N ranks really start, that strong scaling splits the BASELINE global batches
-(256 / 512 / 1024) and weak scaling keeps the per-GPU batch, and that a GPU count that cannot be
-honoured is an error rather than a silent one-GPU line.
+(256 / 512 / 1024) and weak scaling (the default) keeps the configuration's batch per GPU, and that
+a GPU count that cannot be honoured is an error rather than a silent one-GPU line.
 """
 from __future__ import annotations
 
@@ -38,7 +38,7 @@ def _line(res):
 @pytest.mark.parametrize("workload,n,per", [("gen64", 2, [128, 128]), ("fgan128", 2, [256, 256]),
                                             ("fgan128sn", 4, [256] * 4), ("gen64", 3, [86, 85, 85])])
 def test_strong_scaling_plan(workload, n, per):
-    line = _line(_bench("--gpus", str(n), "--dry-run", "--workload", workload))
+    line = _line(_bench("--gpus", str(n), "--dry-run", "--workload", workload, "--scaling", "strong"))
     assert line["n_gpus"] == n and line["scaling"] == "strong"
     assert line["global_batch"] == {"gen64": 256, "fgan128": 512, "fgan128sn": 1024}[workload]
     assert line["per_gpu_batch"] == per and line["tiles_global_batch"]
@@ -46,8 +46,16 @@ def test_strong_scaling_plan(workload, n, per):
 
 
 def test_weak_scaling_plan():
-    line = _line(_bench("--gpus", "2", "--dry-run", "--scaling", "weak", "--workload", "fgan128"))
+    line = _line(_bench("--gpus", "2", "--dry-run", "--scaling", "weak", "--workload", "fgan128", "--batch", "64"))
     assert line["global_batch"] == 128 and line["per_gpu_batch"] == [64, 64]
+
+
+@pytest.mark.parametrize("workload,per", [("gen64", 256), ("fgan128", 512), ("fgan128sn", 1024)])
+def test_weak_scaling_is_default(workload, per):
+    """the default N-GPU line runs the configuration's batch on every GPU (weak scaling)"""
+    line = _line(_bench("--gpus", "2", "--dry-run", "--workload", workload))
+    assert line["scaling"] == "weak" and line["per_gpu_batch"] == [per, per] and line["global_batch"] == 2 * per
+    assert line["tiles_global_batch"]
 
 
 def test_single_rank_plan():

@@ -109,6 +109,9 @@ def test_eval_caller_reshapes_for_ffc_generator():
     with contextlib.redirect_stdout(io.StringIO()):
         fg = F.FGenerator(128)
     assert not GenerativeModelModuleWrapper(fg, 128, "normal", 0)._noise_4d
+    # explicit override either way (torch_fidelity proper passes 2-D noise unchanged)
+    assert not GenerativeModelModuleWrapper(g, 16, "normal", 0, noise_4d=False)._noise_4d
+    assert GenerativeModelModuleWrapper(nn.Identity(), 16, "normal", 0, noise_4d=True)._noise_4d
 
 
 # --------------------------------------------------------------------------- GPU

@@ -217,3 +217,41 @@ def test_gan64train_full_batch_layerwise():
     print(f"gan64train B=256: {len(res)} gradients, worst normwise error {max(e for _, e, _ in res):.2e}")
     bad = sorted(((e, k) for k, e, _ in res if not e < TOL), reverse=True)
     assert not bad, bad[:12]
+
+
+# --------------------------------------------------------------------------- configs[0] (bench --workload block)
+BLOCK_CFG = dict(in_channels=32, out_channels=32, kernel_size=3, ratio_gin=0.5, ratio_gout=0.5, stride=1, padding=1,
+                 norm_layer="BatchNorm2d", activation_layer="ReLU")
+
+
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_block_config0_b16(mode):
+    """BASELINE configs[0] at exactly its batch: FFC_BN_ACT(32, 32, 3, 0.5, 0.5, 1, 1, BN, ReLU),
+    x = (x_l, x_g) ~ N(0,1)^(16,16,32,32), bench.py's weights; the output pair and (train) the
+    updated running statistics against the fp64 oracle (layers/ffc/ffc_bn_act.py:70-83)"""
+    import fastfourierconvolution_amd as F
+    torch.manual_seed(1234)
+    with contextlib.redirect_stdout(io.StringIO()):
+        blk = F.FFC_BN_ACT(32, 32, 3, 0.5, 0.5, stride=1, padding=1, norm_layer=nn.BatchNorm2d,
+                           activation_layer=nn.ReLU)
+    blk.apply(_weights_init)
+    if mode == "eval":     # randomised running statistics (SURVEY.md §8c: untrained eval outputs are tiny)
+        g = torch.Generator().manual_seed(3)
+        for m in blk.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.running_mean.copy_(0.1 * torch.randn(m.num_features, generator=g))
+                m.running_var.copy_(0.5 + torch.rand(m.num_features, generator=g))
+    sd = _sd64(blk)
+    g = torch.Generator().manual_seed(0)
+    x = (torch.randn((16, 16, 32, 32), generator=g), torch.randn((16, 16, 32, 32), generator=g))
+    blk = blk.cuda().train(mode == "train")
+    with torch.no_grad():
+        out = blk(tuple(t.cuda() for t in x))
+    torch.cuda.synchronize()
+    ref = ffc_bn_act(tuple(t.double() for t in x), sd, "", BLOCK_CFG, mode == "train")
+    for o, r in zip(out, ref):
+        assert normwise_err(o.cpu(), r) <= TOL
+    if mode == "train":    # the oracle's batch_norm updated sd's running stats in place
+        for k, v in blk.state_dict().items():
+            if k.endswith(("running_mean", "running_var")):
+                assert normwise_err(v.cpu(), sd[k]) <= TOL, k
