@@ -36,6 +36,11 @@
 namespace {
 
 constexpr int QTHREADS = 512;   // 4 compute waves + 4 staging waves
+#ifndef FFC_CONVQ_SLOTS
+#define FFC_CONVQ_SLOTS 2
+#endif
+constexpr int QSLOTS = FFC_CONVQ_SLOTS;   // staging register slots (chunks in flight + the one being stored)
+static_assert(QSLOTS >= 2 && QSLOTS <= 6, "convq staging slots");
 
 struct ConvQArgs {
     ffc_convp_job jobs[2];
@@ -321,7 +326,11 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const bool ok = inb && cb + j < st.C;
+#ifdef FFC_QPROBE_COALB   // timing probe only: the same number of loads, lane-contiguous addresses
+            const floatx4 v = *reinterpret_cast<const floatx4*>(st.x + ((long long)(stid * 4 + j * 1024 + cb * 8192) % (st.C * st.IHW)));
+#else
             const floatx4 v = *reinterpret_cast<const floatx4*>(src + (ok ? (long long)(cb + j) * st.IHW : 0));
+#endif
             const floatx4 z = {0.0f, 0.0f, 0.0f, 0.0f};
             sv[j] = ok ? v : z;
         }
@@ -397,8 +406,8 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
             unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0;
             QSTAMP(q0);
 #endif
-            floatx4 sv0[8], sv1[8];
-            int wb0 = -1, wb1 = -1;
+            floatx4 sv[QSLOTS][8];
+            int wbs[QSLOTS];
             stage_setup(ss);
             auto issue = [&](floatx4 (&dst)[8], int& wb) {   // the chunk at the load cursor (ss, sch)
                 if (ss < nseg) {
@@ -436,22 +445,27 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
                 qw += qb - qa;
 #endif
             };
-            issue(sv0, wb0);                 // chunk 0
-            issue(sv1, wb1);                 // chunk 1 (if any)
-            store_timed(sv0, wb0, lds);
+            // QSLOTS register slots: chunks c + 1 .. c + QSLOTS - 1 are in flight while chunk c is split
+            // and stored (slot of chunk c = c % QSLOTS; the loop is unrolled by QSLOTS so every slot
+            // index is a compile-time constant)
+#pragma unroll
+            for (int u = 0; u < QSLOTS; ++u) {
+                wbs[u] = -1;
+                if (u < nst) issue(sv[u], wbs[u]);
+            }
+            store_timed(sv[0], wbs[0], lds);
             bar();
-            for (int ci = 0; ci < nst; ci += 2) {
+            for (int c0 = 1; c0 <= nst; c0 += QSLOTS) {
+#pragma unroll
+                for (int u = 0; u < QSLOTS; ++u) {
+                    const int c = c0 + u;    // the chunk stored in this period (c % QSLOTS == (u + 1) % QSLOTS)
+                    if (c > nst) break;
 #ifndef FFC_QPROBE_NOSTAGE
-                if (ci + 2 < nst) issue(sv0, wb0);
-                if (ci + 1 < nst) store_timed(sv1, wb1, lds + ebuf);
+                    if (c + QSLOTS - 1 < nst) issue(sv[u], wbs[u]);   // slot u held chunk c - 1
+                    if (c < nst) store_timed(sv[(u + 1) % QSLOTS], wbs[(u + 1) % QSLOTS], lds + (c & 1) * ebuf);
 #endif
-                bar();
-                if (ci + 1 >= nst) break;
-#ifndef FFC_QPROBE_NOSTAGE
-                if (ci + 3 < nst) issue(sv1, wb1);
-                if (ci + 2 < nst) store_timed(sv0, wb0, lds);
-#endif
-                bar();
+                    bar();
+                }
             }
 #ifdef FFC_TRACE_Q
             QSTAMP(qa);
@@ -526,7 +540,9 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = mfma_split3(a[t][mt], b, acc[mt][nt]);
                 }
+#ifndef FFC_QPROBE_NOA   // timing probe only: A of the first chunk reused
                 load_A(kn + 16 * t, a[t]);   // refill: the next chunk's tap t
+#endif
                 // keep the next tap's reads ahead of this tap's MFMAs (the scheduler otherwise sinks
                 // each read to just before its first use and waits on it), the refill after them
                 if (t + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTW, 0);   // DS_READ

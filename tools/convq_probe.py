@@ -14,7 +14,8 @@ model = sys.argv[2] if len(sys.argv) > 2 else "gen64"
 dev = torch.device("cuda", 0)
 # (C_l = C_g in, IH, M_l = M_g out, c of the ST = conv2 input channels)
 LAYERS_ALL = {"gen64": [(256, 4, 128, 64), (128, 8, 64, 32), (64, 16, 32, 16)],
-              "fgan128": [(128, 8, 64, 32), (64, 16, 32, 16), (32, 32, 64, 32), (32, 64, 64, 32)]}
+              # fgan128 (ngf 128) conv3..conv6: in_cl = in_cg = C, out_l = out_g = M, ST c = M / 2
+              "fgan128": [(256, 8, 128, 64), (128, 16, 64, 32), (64, 32, 64, 32), (64, 64, 64, 32)]}
 LAYERS = LAYERS_ALL.get(model, LAYERS_ALL["gen64"])
 
 
