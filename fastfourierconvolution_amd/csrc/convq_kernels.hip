@@ -31,7 +31,11 @@
 // slab rows [block*4 + wave], activation) as in convp.
 #include "ffc_internal.h"
 
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 
 namespace {
 
@@ -48,6 +52,7 @@ struct ConvQArgs {
     int ebuf;                  // bytes per LDS buffer (multiple of 256)
     int ksplit;                // K splits per output tile (1: no split)
     float* part;               // ksplit > 1: per (slot, split, wave) fragment partial sums
+    int ntiles;                // rows of the tile table (the grid may be smaller: persistent workgroups)
 };
 
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -204,21 +209,18 @@ __device__ __forceinline__ void convq_epilogue(const ffc_convp_job& J, int wave,
     if constexpr (MT > 1) epilogue(acc[1], m0 + 32 + 4 * h);
 }
 
+// One output tile (one row of the tile table) of one workgroup; returns when the tile is done (the
+// staging waves after their last barrier of the tile, the compute waves after the epilogue).  Every
+// wave of the workgroup runs the same tiles, so the barrier counts match tile by tile.
 template <int MT, int NTW>
-__global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-#else
-    const ConvQArgs& args = args_byval;
-#endif
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix, char* lds) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave_id = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stager = wave_id >= 4;
     const int wave = wave_id & 3;            // compute waves: the phase
     const int stid = tid - 256;              // staging waves: unit slot 0..255
     const int h = lane >> 5, cl = lane & 31;
-    const int4 tile = args.tiles[blockIdx.x];
+    const int4 tile = args.tiles[tix];
     const int ji = __builtin_amdgcn_readfirstlane(tile.x);
     const int m0 = __builtin_amdgcn_readfirstlane(tile.y);
     const int pb = __builtin_amdgcn_readfirstlane(tile.z);
@@ -470,7 +472,7 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
 #ifdef FFC_TRACE_Q
             QSTAMP(qa);
             if (tid == 256) {
-                unsigned long long* tr = g_ffc_trace_q + 16 * blockIdx.x;
+                unsigned long long* tr = g_ffc_trace_q + 16 * tix;
                 tr[9] = ql;
                 tr[10] = qs;
                 tr[11] = qw;
@@ -633,7 +635,7 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
         unsigned long long tq_e;
         QSTAMP(tq_e);
         if (tid == 0) {
-            unsigned long long* tr = g_ffc_trace_q + 16 * blockIdx.x;
+            unsigned long long* tr = g_ffc_trace_q + 16 * tix;
             tr[0] = tq_rt0;
             tr[1] = __builtin_amdgcn_s_memrealtime();
             tr[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
@@ -647,6 +649,21 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
         }
     }
 #endif
+}
+
+// Persistent over the tile table: workgroup b runs tiles b, b + G, b + 2G, ... (G = gridDim.x, a
+// multiple of 8, so every tile of a workgroup comes from its XCD's range of the XCD-remapped table).
+// A tile's epilogue stores drain while the staging waves already load and split the next tile's
+// first chunk, and the next tile's MFMAs start without a fresh workgroup launch.
+template <int MT, int NTW>
+__global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+#else
+    const ConvQArgs& args = args_byval;
+#endif
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW>(args, tix, lds);
 }
 
 // K split, second pass: workgroup = one output tile (slot), wave w = phase w; adds the ksplit
@@ -692,6 +709,44 @@ __global__ __launch_bounds__(256) void convq_reduce_kernel(ConvQArgs args_byval,
     convq_epilogue<MT, NTW>(args.jobs[ji], wave, lane, pb, m0, acc);
 }
 
+// Workgroups of the persistent grid: every CU's resident workgroups (occupancy of this kernel at this
+// LDS size, queried once per (kernel, LDS bytes, device)), rounded down to a multiple of 8 (the XCD
+// count: workgroup b then stays on XCD b % 8 for all its tiles), never more than the tiles.
+// FFC_CONVQ_PERSIST=0 launches one workgroup per tile (the previous grid; A/B measurements).
+int persistent_grid(const void* k, size_t lds, int ntiles) {
+    static const bool off = [] {
+        const char* e = getenv("FFC_CONVQ_PERSIST");
+        return e && e[0] == '0';
+    }();
+    if (off) return ntiles;
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, size_t, int>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        ffc::set_error("ffc_convq_forward: hipGetDevice failed");
+        return -1;
+    }
+    int slots = 0;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find({k, lds, dev});
+        if (it != cache.end()) {
+            slots = it->second;
+        } else {
+            int cus = 0, per = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, QTHREADS, lds) != hipSuccess || cus <= 0) {
+                ffc::set_error("ffc_convq_forward: occupancy query failed");
+                return -1;
+            }
+            slots = cus * (per > 0 ? per : 1);
+            slots = slots >= 8 ? slots / 8 * 8 : slots;
+            cache[{k, lds, dev}] = slots;
+        }
+    }
+    return ntiles < slots ? ntiles : slots;
+}
+
 template <int MT, int NTW>
 int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const int4* slots, int nslots) {
     auto k = convq_kernel<MT, NTW>;
@@ -707,7 +762,9 @@ int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const in
             raised = true;
         }
     }
-    hipLaunchKernelGGL(k, dim3(ntiles), dim3(QTHREADS), lds, s, a);
+    const int grid = persistent_grid(reinterpret_cast<const void*>(k), lds, ntiles);
+    if (grid <= 0) return FFC_E_LAUNCH;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(QTHREADS), lds, s, a);
     if (a.ksplit > 1) {
         const int rc = ffc::launch_status("ffc_convq_forward_split");
         if (rc != FFC_OK) return rc;
@@ -849,6 +906,7 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
     a.tiles = reinterpret_cast<const int4*>(tiles);
     a.ksplit = ksplit;
     a.part = part;
+    a.ntiles = ntiles;
     const int4* sl = reinterpret_cast<const int4*>(slot_tiles);
     hipStream_t s = (hipStream_t)stream;
     switch (cfg) {
