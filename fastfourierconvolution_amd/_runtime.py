@@ -429,14 +429,12 @@ def pick_pw_cfg(B, M, Q):
 # operand, six piece products), "f32" = v_mfma_f32_32x32x2_f32 (A/B measurements, tests)
 CONV_ARITH = __import__("os").environ.get("FFC_CONV_ARITH", "split")
 PRESPLIT_A = __import__("os").environ.get("FFC_CONVP_PRESPLIT", "0") == "1"   # A/B knob: A3 planes (off: measured neutral / -1 %)
-# stride-2 transposed-conv jobs on ffc_convq_forward (operands split once while staged, warp-specialised)
-# under the split-bf16 products.  It wins where the grid is small (<= CONVQ_MAX_CONVP_TILES convp
-# workgroups per job: the strong-scaling shards, fgan128's low-resolution layers) and loses to
-# ffc_convp_forward on large grids (measured, tools/convq_probe.py): "auto" picks per job, "1" /
-# "force" always convq where it applies, "0" never
+# stride-2 transposed-conv jobs on ffc_convq_forward (operands split once while staged, warp-specialised,
+# persistent workgroups) under the split-bf16 products: taken wherever it plans ("auto" / "1" / "force");
+# "0" never (convp for everything, A/B measurements).  Until r02 it lost to convp on large grids; the
+# persistent grid (r03) reversed that (tools/convq_probe.py)
 USE_CONVQ = __import__("os").environ.get("FFC_CONVQ", "auto") != "0"
 CONVQ_FORCE = __import__("os").environ.get("FFC_CONVQ", "auto") in ("1", "force")
-CONVQ_MAX_CONVP_TILES = 256
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
@@ -482,9 +480,9 @@ class ConvExec:
               if USE_PATCH and not (pw_only and PW_KERNEL == "gemm") else None)
         if USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and convq_cfg is not None:
             pp = _plan.plan_convq_job(B, M, segs, convq_cfg) or pp   # the launch group's common cfg
-        elif USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only and (
-                CONVQ_FORCE or pp is None or pp.npb * (-(-M // 32)) <= CONVQ_MAX_CONVP_TILES or
-                _plan.job_signature(B, M, segs) in _plan.convq_tuned()[0]):   # measured faster there
+        elif USE_PATCH and USE_CONVQ and CONV_ARITH == "split" and not pw_only:
+            # persistent convq (r03) measured faster than convp on every timed stride-2 shape, large
+            # grids included (profiles/r03/r03g_probe_fgan128_*.log); convp stays for what it cannot plan
             pp = _plan.pick_convq_cfg(B, M, segs) or pp
         if pw_ok and pw_only and PW_KERNEL == "pw":
             self.kind, self.plan = "pw", _plan.plan_job(B, M, segs)

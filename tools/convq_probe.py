@@ -14,8 +14,10 @@ model = sys.argv[2] if len(sys.argv) > 2 else "gen64"
 dev = torch.device("cuda", 0)
 # (C_l = C_g in, IH, M_l = M_g out, c of the ST = conv2 input channels)
 LAYERS_ALL = {"gen64": [(256, 4, 128, 64), (128, 8, 64, 32), (64, 16, 32, 16)],
-              # fgan128 (ngf 128) conv3..conv6: in_cl = in_cg = C, out_l = out_g = M, ST c = M / 2
-              "fgan128": [(256, 8, 128, 64), (128, 16, 64, 32), (64, 32, 64, 32), (64, 64, 64, 32)]}
+              # fgan128 (ngf 128) conv2 (local input only: c = 0) and conv3..conv6: in_cl = in_cg = C,
+              # out_l = out_g = M, ST c = M / 2
+              "fgan128": [(1024, 4, 256, 0), (256, 8, 128, 64), (128, 16, 64, 32), (64, 32, 64, 32),
+                          (64, 64, 64, 32)]}
 LAYERS = LAYERS_ALL.get(model, LAYERS_ALL["gen64"])
 
 
@@ -23,12 +25,14 @@ def job_pair(C, IH, M, c):
     g = torch.Generator().manual_seed(C + IH)
     xl = torch.randn(B, C, IH, IH, generator=g).to(dev)
     xg = torch.randn(B, C, IH, IH, generator=g).to(dev)
-    v = torch.randn(B, c, 2 * IH, 2 * IH, generator=g).to(dev)
+    v = torch.randn(B, max(c, 1), 2 * IH, 2 * IH, generator=g).to(dev)
     wl = torch.randn(C, M, 4, 4, generator=g).to(dev) * 0.02
     wg = torch.randn(C, M, 4, 4, generator=g).to(dev) * 0.02
     wlg = torch.randn(C, M, 4, 4, generator=g).to(dev) * 0.02
-    w2 = torch.randn(M, c, 1, 1, generator=g).to(dev) * 0.02
+    w2 = torch.randn(M, max(c, 1), 1, 1, generator=g).to(dev) * 0.02
     segT = _plan.Seg("convT", C, IH, IH, 4, 2, 1)
+    if c == 0:   # FFCTranspose with ratio_gin 0: out_l = l2l(x_l), out_g = l2g(x_l)
+        return [([segT], [(wl, 1, 4, 4, None)], [xl]), ([segT], [(wlg, 1, 4, 4, None)], [xl])]
     jobs = [([segT, segT], [(wl, 1, 4, 4, None), (wg, 1, 4, 4, None)], [xl, xg]),
             ([segT, _plan.Seg("pw", c, 2 * IH, 2 * IH)], [(wlg, 1, 4, 4, None), (w2, 0, 1, 1, None)], [xl, v])]
     return jobs
@@ -91,10 +95,10 @@ def main():
     row = [f"C{C}@{IH}x{IH}->M{M}"]
     for var in ["convp", 0, 1, 2, 3]:
         if var == "convp":
-            rt.USE_CONVQ = False
+            rt.USE_CONVQ = rt.CONVQ_FORCE = False
             os.environ.pop("FFC_CONVQ_CFG", None)
         else:
-            rt.USE_CONVQ = True
+            rt.USE_CONVQ = rt.CONVQ_FORCE = True
             os.environ["FFC_CONVQ_CFG"] = str(var)
         try:
             us, tf, keys = time_layer(jobs)
