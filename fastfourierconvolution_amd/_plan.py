@@ -325,6 +325,11 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         for si, sg in enumerate(segs):
             ty = _taps(sg, base.Sy, ph.py, sg.IH, ph.PH)
             tx = _taps(sg, base.Sx, ph.px, sg.IW, ph.PW)
+            if NP == 1 and len(ty) == len(tx) == 3 and sg.kind == "conv":
+                # 3x3 (FFC k3, BASELINE configs[0] / fgan128's head): run as 4x4 taps in 4-channel
+                # chunks with a zero-weight 4th row / column (k index -1), one pixel past the 3rd
+                ty = ty + [(-1, ty[-1][1] + 1)]
+                tx = tx + [(-1, tx[-1][1] + 1)]
             T = len(ty) * len(tx)
             if T == 16 and NP == 1 and len(ty) == len(tx) == 4:
                 cc[si] = 4
@@ -381,7 +386,8 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
             for ch in range(cpad[si]):
                 for (ky, oy) in ty:
                     for (kx, ox) in tx:
-                        ktab.append((si | (ch << 4), oy, ox, ky | (kx << 16)) if ch < sg.C else PAD_ENTRY)
+                        ktab.append((si | (ch << 4), oy, ox, ky | (kx << 16))
+                                    if ch < sg.C and ky >= 0 and kx >= 0 else PAD_ENTRY)
             k += cpad[si] * T
         if k == 0:
             return None

@@ -405,7 +405,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             // two register slots: the loads of chunk c + 2 are in flight while chunk c + 1 is split and
             // stored, so a chunk's load latency overlaps a whole chunk period of MFMAs
 #ifdef FFC_TRACE_Q
-            unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0;
+            unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0, qi = 0;
             QSTAMP(q0);
 #endif
             floatx4 sv[QSLOTS][8];
@@ -463,7 +463,14 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
                     const int c = c0 + u;    // the chunk stored in this period (c % QSLOTS == (u + 1) % QSLOTS)
                     if (c > nst) break;
 #ifndef FFC_QPROBE_NOSTAGE
+#ifdef FFC_TRACE_Q
+                    QSTAMP(qa);
+#endif
                     if (c + QSLOTS - 1 < nst) issue(sv[u], wbs[u]);   // slot u held chunk c - 1
+#ifdef FFC_TRACE_Q
+                    QSTAMP(qb);
+                    qi += qb - qa;
+#endif
                     if (c < nst) store_timed(sv[(u + 1) % QSLOTS], wbs[(u + 1) % QSLOTS], lds + (c & 1) * ebuf);
 #endif
                     bar();
@@ -478,6 +485,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
                 tr[11] = qw;
                 tr[12] = qa - q0;
                 tr[13] = nst;
+                tr[14] = qi;
             }
 #endif
             return;   // no barrier follows

@@ -38,9 +38,9 @@ print(f"layer {li} B={B} cfg {cfg}: {us:.1f} us/launch (events), {ntiles} workgr
 names = ["barrier", "A issue", "MFMA taps", "direct", "epilogue", "total"]
 cw = buf[:, 3:9].astype(np.float64)
 print("compute wave 0 (kcycles mean): " + ", ".join(f"{n} {v / 1e3:.2f}" for n, v in zip(names, cw.mean(0))))
-sw = buf[:, 9:13].astype(np.float64)
+sw = buf[:, [9, 10, 11, 14, 12]].astype(np.float64)
 print("staging wave 4 (kcycles mean): " + ", ".join(f"{n} {v / 1e3:.2f}" for n, v in
-                                                 zip(["loads", "split+store", "barrier", "total"], sw.mean(0))) +
+                                                 zip(["loads", "split+store", "barrier", "issue", "total"], sw.mean(0))) +
       f", chunks {buf[:, 13].mean():.1f}")
 cu = (buf[:, 2] & 0xF00) >> 8
 print(f"workgroups per (XCC, CU): max {np.bincount(((buf[:, 2] >> 32) & 7) * 16 + cu).max()}")
