@@ -57,6 +57,7 @@ struct ConvQArgs {
 
 typedef __attribute__((address_space(3))) void* lptr_t;
 
+
 #ifdef FFC_TRACE_Q
 // Diagnostic build only (tools/trace_convq.py): per workgroup 16 u64:
 // [0] realtime start [1] realtime end (compute wave 0) [2] HW_ID | XCC_ID << 32
@@ -320,28 +321,32 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
         st.hu = hu;
         st.wb = n < st.nunits ? ((hu * NS + ns) * QS + pr * QR + 4 * g) * 48 : -1;
     };
-    // every lane loads (a clamped, valid address) and selects afterwards: no branch around a load
-    auto stage_load = [&](floatx4 (&sv)[8], int ch0) {
+    // Every lane loads from a valid address (out-of-range units read the segment base) and the zero
+    // select happens at store time, on the returned lane mask: a select right behind the loads made
+    // the compiler wait for them at issue (s_waitcnt vmcnt), and conditional addresses compiled to
+    // divergent branches that reused the load registers (more waits) -- together they serialised the
+    // staging pipeline (r03 trace: "issue" 4.6k cycles per chunk on gen64 layer 0).
+    auto stage_load = [&](floatx4 (&sv)[8], int ch0) -> int {
         const int cb = ch0 + 8 * st.hu;
         const bool inb = st.sb >= 0;
-        const float* src = st.x + (inb ? (long long)st.sb * st.sstride + st.off : 0);
+        const long long base = (long long)(inb ? st.sb : 0) * st.sstride + (inb ? st.off : 0);
+        int mask = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const bool ok = inb && cb + j < st.C;
-#ifdef FFC_QPROBE_COALB   // timing probe only: the same number of loads, lane-contiguous addresses
-            const floatx4 v = *reinterpret_cast<const floatx4*>(st.x + ((long long)(stid * 4 + j * 1024 + cb * 8192) % (st.C * st.IHW)));
-#else
-            const floatx4 v = *reinterpret_cast<const floatx4*>(src + (ok ? (long long)(cb + j) * st.IHW : 0));
-#endif
-            const floatx4 z = {0.0f, 0.0f, 0.0f, 0.0f};
-            sv[j] = ok ? v : z;
+            mask |= ok ? (1 << j) : 0;
+            const long long o = base + (long long)(ok ? cb + j : 0) * st.IHW;
+            sv[j] = *reinterpret_cast<const floatx4*>(st.x + o);
         }
+        return mask;
     };
-    auto stage_store = [&](const floatx4 (&sv)[8], int wb, char* buf) {
+    auto stage_store = [&](const floatx4 (&sv)[8], int wb, int mask, char* buf) {
         if (wb >= 0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float v8[8] = {sv[0][e], sv[1][e], sv[2][e], sv[3][e], sv[4][e], sv[5][e], sv[6][e], sv[7][e]};
+                float v8[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v8[j] = (mask >> j) & 1 ? sv[j][e] : 0.0f;
                 const Split3 sp = split3(v8);
                 u32x4* d = reinterpret_cast<u32x4*>(buf + wb + 48 * e);
                 d[0] = __builtin_bit_cast(u32x4, sp.hi);
@@ -383,6 +388,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
     const int slo = min(lo, nstaged), nst = min(hi, nstaged) - slo;
     const int dlo = max(lo, nstaged) - nstaged, dhi = max(hi, nstaged) - nstaged;
 
+    const int npad = (nst + QSLOTS - 1) / QSLOTS * QSLOTS;   // barrier periods after the first (>= nst)
     if (nst > 0) {
         int ss = 0;
         while (J.seg[ss].direct) ++ss;
@@ -409,30 +415,36 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             QSTAMP(q0);
 #endif
             floatx4 sv[QSLOTS][8];
-            int wbs[QSLOTS];
+            int wbs[QSLOTS], msk[QSLOTS];
             stage_setup(ss);
-            auto issue = [&](floatx4 (&dst)[8], int& wb) {   // the chunk at the load cursor (ss, sch)
-                if (ss < nseg) {
-                    stage_load(dst, sch);
-                    wb = st.wb;
+            // the chunk at the load cursor (ss, sch); past the last chunk the loads still issue (the
+            // previous addresses, mask 0, no store): every period then has the same load / wait
+            // pattern, so the compiler's wait counts stay exact (a conditional issue made it wait for
+            // every outstanding load at the loop head, serialising the pipeline)
+            int ic = 0;   // chunks issued (this workgroup's K range is chunks 0 .. nst - 1)
+            auto issue = [&](floatx4 (&dst)[8], int& wb, int& mask) {
+                const bool live = ss < nseg && ic < nst;
+                ++ic;
+                mask = stage_load(dst, live ? sch : 0);
+                mask = live ? mask : 0;
+                wb = live ? st.wb : -1;
+                if (live) {
                     sch += 16;
                     advance_stager();
-                } else {
-                    wb = -1;
                 }
             };
-            auto store_timed = [&](const floatx4 (&src)[8], int wb, char* buf) {
+            auto store_timed = [&](const floatx4 (&src)[8], int wb, int mask, char* buf) {
 #ifdef FFC_TRACE_Q
                 QSTAMP(qa);
                 float chk = src[0][0] + src[7][3];
                 asm volatile("" ::"v"(chk));   // data arrived
                 QSTAMP(qb);
                 ql += qb - qa;
-                stage_store(src, wb, buf);
+                stage_store(src, wb, mask, buf);
                 QSTAMP(qa);
                 qs += qa - qb;
 #else
-                stage_store(src, wb, buf);
+                stage_store(src, wb, mask, buf);
 #endif
             };
             auto bar = [&]() {
@@ -451,27 +463,27 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             // and stored (slot of chunk c = c % QSLOTS; the loop is unrolled by QSLOTS so every slot
             // index is a compile-time constant)
 #pragma unroll
-            for (int u = 0; u < QSLOTS; ++u) {
-                wbs[u] = -1;
-                if (u < nst) issue(sv[u], wbs[u]);
-            }
-            store_timed(sv[0], wbs[0], lds);
+            for (int u = 0; u < QSLOTS; ++u) issue(sv[u], wbs[u], msk[u]);
+            store_timed(sv[0], wbs[0], msk[0], lds);
             bar();
-            for (int c0 = 1; c0 <= nst; c0 += QSLOTS) {
+            // periods 1 .. npad (nst rounded up to whole QSLOTS-period rounds: no exit in the middle of the
+            // unrolled body, so every path into the loop head has the same loads in flight); periods past
+            // nst issue nothing live, store nothing and only meet the compute waves' padding barriers
+            for (int c0 = 1; c0 <= npad; c0 += QSLOTS) {
 #pragma unroll
                 for (int u = 0; u < QSLOTS; ++u) {
                     const int c = c0 + u;    // the chunk stored in this period (c % QSLOTS == (u + 1) % QSLOTS)
-                    if (c > nst) break;
 #ifndef FFC_QPROBE_NOSTAGE
 #ifdef FFC_TRACE_Q
                     QSTAMP(qa);
 #endif
-                    if (c + QSLOTS - 1 < nst) issue(sv[u], wbs[u]);   // slot u held chunk c - 1
+                    issue(sv[u], wbs[u], msk[u]);   // chunk c + QSLOTS - 1 into slot u (it held chunk c - 1)
 #ifdef FFC_TRACE_Q
                     QSTAMP(qb);
                     qi += qb - qa;
 #endif
-                    if (c < nst) store_timed(sv[(u + 1) % QSLOTS], wbs[(u + 1) % QSLOTS], lds + (c & 1) * ebuf);
+                    store_timed(sv[(u + 1) % QSLOTS], wbs[(u + 1) % QSLOTS], msk[(u + 1) % QSLOTS],
+                                lds + (c & 1) * ebuf);   // chunk c (past the last chunk: wb = -1, no store)
 #endif
                     bar();
                 }
@@ -582,6 +594,9 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             tq_bar += tq_b - tq_a;
 #endif
         }
+#ifndef FFC_QPROBE_NOBAR
+        for (int ci = nst; ci < npad; ++ci) __syncthreads();   // the staging waves' padding periods
+#endif
     }
 #ifdef FFC_TRACE_Q
     QSTAMP(tq_c);
