@@ -50,20 +50,38 @@ __device__ __forceinline__ void twiddle(int e, float& c, float& s) {
     s = INV ? c_tws[e * (128 / N)] : -c_tws[e * (128 / N)];
 }
 
+// This lane's stage-A twiddles W_N^{jj*k2} (k2 = 1..N2-1; jj*k2 < N): loaded once per kernel, before
+// its line loops -- inside them every line FFT paid a dependent table load (per-lane index, so a
+// vector-memory load) before its twiddle multiplies.
+template <int N>
+struct LaneTw {
+    float c[Split<N>::N2], s[Split<N>::N2];
+    __device__ __forceinline__ explicit LaneTw(int jj) {
+#pragma unroll
+        for (int k2 = 1; k2 < Split<N>::N2; ++k2) {
+            c[k2] = c_twc[jj * k2 * (128 / N)];
+            s[k2] = c_tws[jj * k2 * (128 / N)];
+        }
+    }
+};
+
 // Stage A on this lane's samples x[jj + N1*m] (m = 0..N2-1, in re/im): N2-point FFT in registers,
 // then the twiddles W_N^{jj*k2}.  Result index k2 holds Y[jj][k2].
 template <int N, bool INV>
-__device__ __forceinline__ void stage_a(float (&re)[Split<N>::N2], float (&im)[Split<N>::N2], int jj) {
+__device__ __forceinline__ void stage_a(float (&re)[Split<N>::N2], float (&im)[Split<N>::N2], const LaneTw<N>& tw) {
     constexpr int N2 = Split<N>::N2;
     fft_reg<N2, INV>(re, im);
 #pragma unroll
     for (int k2 = 1; k2 < N2; ++k2) {
-        float c, s;
-        twiddle<N, INV>(jj * k2, c, s);
+        const float c = tw.c[k2], s = INV ? tw.s[k2] : -tw.s[k2];
         const float xr = re[k2] * c - im[k2] * s;
         im[k2] = re[k2] * s + im[k2] * c;
         re[k2] = xr;
     }
+}
+template <int N, bool INV>
+__device__ __forceinline__ void stage_a(float (&re)[Split<N>::N2], float (&im)[Split<N>::N2], int jj) {
+    stage_a<N, INV>(re, im, LaneTw<N>(jj));
 }
 
 // Stage B through an LDS line of N float2 (element n at line[n*stride]): writes stage-A results,
@@ -93,7 +111,7 @@ __device__ __forceinline__ void stage_b(float2* line, int stride, const float (&
 
 // In-place length-N complex FFT of line[n*stride] by the N1 lanes jj of one wave.
 template <int N, bool INV>
-__device__ __forceinline__ void line_fft(float2* line, int stride, int jj) {
+__device__ __forceinline__ void line_fft(float2* line, int stride, int jj, const LaneTw<N>& tw) {
     constexpr int N1 = Split<N>::N1, N2 = Split<N>::N2, Q = Split<N>::Q;
     float re[N2], im[N2];
 #pragma unroll
@@ -102,7 +120,7 @@ __device__ __forceinline__ void line_fft(float2* line, int stride, int jj) {
         re[m] = v.x;
         im[m] = v.y;
     }
-    stage_a<N, INV>(re, im, jj);
+    stage_a<N, INV>(re, im, tw);
     float ore[Q][N1], oim[Q][N1];
     stage_b<N, INV>(line, stride, re, im, jj, ore, oim);
 #pragma unroll
@@ -118,9 +136,10 @@ __device__ __forceinline__ void column_pass(float2* Z, int ZS, int ncols, int ti
     constexpr int N1 = Split<ROWS>::N1;
     constexpr int LPR = NT / N1;   // lines per round
     const int jj = tid % N1;
+    const LaneTw<ROWS> tw(jj);
     for (int c0 = 0; c0 < ncols; c0 += LPR) {
         const int col = c0 + tid / N1;
-        if (col < ncols) line_fft<ROWS, INV>(Z + col, ZS, jj);
+        if (col < ncols) line_fft<ROWS, INV>(Z + col, ZS, jj, tw);
     }
 }
 
@@ -192,6 +211,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     {
         constexpr int LPR = FU2_THREADS / N1;
         const int jj = tid % N1;
+        const LaneTw<w> twr(jj);
         for (int g0 = 0; g0 < h / 2; g0 += LPR) {
             const int g = g0 + tid / N1;
             if (g < h / 2) {
@@ -201,7 +221,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
                     re[m] = R[(2 * g) * RS + jj + N1 * m];
                     im[m] = R[(2 * g + 1) * RS + jj + N1 * m];
                 }
-                stage_a<w, false>(re, im, jj);
+                stage_a<w, false>(re, im, twr);
                 float2* line = Z + 2 * g * ZS;    // rows 2g, 2g+1 of Z: 2*ZS >= w slots
                 float ore[Q][N1], oim[Q][N1];
                 stage_b<w, false>(line, 1, re, im, jj, ore, oim);
@@ -284,37 +304,89 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     const int plane = blockIdx.x;
     const int ch = plane % a.C;
     const int tid = threadIdx.x;
+    const LaneTw<H> twc(tid % Split<H>::N1);   // column IFFTs (step 2)
+    const LaneTw<W> twr(tid % N1);             // row C2R (step 3)
 
-    // 1. Y plane -> LDS rows of stride ZS (16 float2 loads in flight per thread per batch); a raw
-    //    (spilled) Y gets the FU's BN + ReLU here, the same expression as mix pass 1
+    // 1. Y plane -> LDS rows of stride ZS; a raw (spilled) Y gets the FU's BN + ReLU here, the same
+    //    expression as mix pass 1.  Non-planar: the whole plane as 16-byte loads (two complex bins,
+    //    possibly across a row end), all issued before the first wait, and (UP = 2) the residual
+    //    t values this thread adds in step 3 issued with them -- one memory latency per plane
+    //    instead of three (two Y batches, then the residual under the row pass).
+    const float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
+    const float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
+    constexpr int tW = W / UP;
+    const float* tpl = a.t + (size_t)plane * (H / UP) * tW;
+    float* opl = a.out + (size_t)plane * H * W;
+    constexpr int RLPR = FU2_THREADS / N1;                      // row pairs per round of step 3
+    constexpr int RROUNDS = (H / 2 + RLPR - 1) / RLPR;
+    constexpr int RITER = (2 * W / 4 + N1 - 1) / N1;            // float4 outputs per thread per row pair
+    constexpr bool RPRE = !PLANAR && UP == 2;
+    float2 res[RPRE ? RROUNDS : 1][RPRE ? RITER : 1];
     {
-        const float2* src = reinterpret_cast<const float2*>(a.Y) + (size_t)plane * H * WP;
-        const float* pre = a.Y + (size_t)plane * 2 * H * WP;   // PLANAR: Re plane, Im plane behind it
         const bool bn = a.bn_scale != nullptr;
         const float bsr = bn ? a.bn_scale[2 * ch] : 1.0f, bhr = bn ? a.bn_shift[2 * ch] : 0.0f;
         const float bsi = bn ? a.bn_scale[2 * ch + 1] : 1.0f, bhi = bn ? a.bn_shift[2 * ch + 1] : 0.0f;
-        for (int i0 = 0; i0 < H * WP; i0 += 16 * FU2_THREADS) {
-            float2 v[16];
+        if constexpr (!PLANAR) {
+            constexpr int N4 = H * WP / 2;                         // H even: whole float4 pairs
+            constexpr int NL = (N4 + FU2_THREADS - 1) / FU2_THREADS;
+            const float4* src4 = reinterpret_cast<const float4*>(a.Y) + (size_t)plane * N4;
+            float4 v[NL];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int i = i0 + u * FU2_THREADS + tid;
-                if (i < H * WP) {
-                    if constexpr (PLANAR) {
-                        const int k = i % WP;
-                        const float sc = (k == 0 || 2 * k == W) ? 1.0f : a.iscale;
-                        v[u] = make_float2(pre[i] * sc, pre[H * WP + i] * sc);
-                    } else {
-                        v[u] = src[i];
+            for (int u = 0; u < NL; ++u) {
+                const int i = u * FU2_THREADS + tid;
+                v[u] = src4[i < N4 ? i : 0];
+            }
+            if constexpr (RPRE) {
+                if (a.residual) {
+                    const int jj = tid % N1;
+#pragma unroll
+                    for (int rd = 0; rd < RROUNDS; ++rd) {
+                        const int g = rd * RLPR + tid / N1;
+#pragma unroll
+                        for (int i = 0; i < RITER; ++i) {
+                            const int q4 = jj + N1 * i;
+                            const int rr = q4 / (W / 4), x = 4 * (q4 % (W / 4));
+                            const int y = 2 * g + rr;
+                            const bool ok = g < H / 2 && q4 < 2 * W / 4;
+                            res[rd][i] = *reinterpret_cast<const float2*>(tpl + (ok ? (y / 2) * tW + x / 2 : 0));
+                        }
                     }
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int i = i0 + u * FU2_THREADS + tid;
-                if (i < H * WP) {
-                    const int r = i / WP, k = i - r * WP;
-                    if (bn) v[u] = make_float2(fmaxf(fmaf(v[u].x, bsr, bhr), 0.0f), fmaxf(fmaf(v[u].y, bsi, bhi), 0.0f));
-                    Z[r * ZS + k] = v[u];
+            for (int u = 0; u < NL; ++u) {
+                const int i = u * FU2_THREADS + tid;
+                if (i < N4) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        float2 z = e ? make_float2(v[u].z, v[u].w) : make_float2(v[u].x, v[u].y);
+                        const int f = 2 * i + e, r = f / WP, k = f - r * WP;
+                        if (bn) z = make_float2(fmaxf(fmaf(z.x, bsr, bhr), 0.0f), fmaxf(fmaf(z.y, bsi, bhi), 0.0f));
+                        Z[r * ZS + k] = z;
+                    }
+                }
+            }
+        } else {
+            const float* pre = a.Y + (size_t)plane * 2 * H * WP;   // PLANAR: Re plane, Im plane behind it
+            for (int i0 = 0; i0 < H * WP; i0 += 16 * FU2_THREADS) {
+                float2 v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int i = i0 + u * FU2_THREADS + tid;
+                    if (i < H * WP) {
+                        const int k = i % WP;
+                        const float isc = (k == 0 || 2 * k == W) ? 1.0f : a.iscale;
+                        v[u] = make_float2(pre[i] * isc, pre[H * WP + i] * isc);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int i = i0 + u * FU2_THREADS + tid;
+                    if (i < H * WP) {
+                        const int r = i / WP, k = i - r * WP;
+                        if (bn) v[u] = make_float2(fmaxf(fmaf(v[u].x, bsr, bhr), 0.0f), fmaxf(fmaf(v[u].y, bsi, bhi), 0.0f));
+                        Z[r * ZS + k] = v[u];
+                    }
                 }
             }
         }
@@ -340,7 +412,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
         const int jj = tid % N1c;
         for (int l0 = 0; l0 < W / 2; l0 += LPR) {
             const int l = l0 + tid / N1c;
-            if (l < W / 2) line_fft<H, true>(Z + (l == 0 ? WP : l), ZS, jj);
+            if (l < W / 2) line_fft<H, true>(Z + (l == 0 ? WP : l), ZS, jj, twc);
         }
     }
 #endif
@@ -348,16 +420,12 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
 
     // 3. rows two at a time: z[k] = A_ext[k] + i B_ext[k] (Hermitian extension of each half
     //    spectrum, Im of bins 0 and W/2 dropped) -> inverse FFT -> Re = row 2g, Im = row 2g+1
-    const float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
-    const float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
-    constexpr int tW = W / UP;
-    const float* tpl = a.t + (size_t)plane * (H / UP) * tW;
-    float* opl = a.out + (size_t)plane * H * W;
     {
-        constexpr int LPR = FU2_THREADS / N1;
+        constexpr int LPR = RLPR;
         const int jj = tid % N1;
-        for (int g0 = 0; g0 < H / 2; g0 += LPR) {
-            const int g = g0 + tid / N1;
+#pragma unroll
+        for (int rd = 0; rd < RROUNDS; ++rd) {
+            const int g = rd * LPR + tid / N1;
             if (g < H / 2) {
                 float2* ra = Z + 2 * g * ZS;
                 float2* rb = ra + ZS;
@@ -383,7 +451,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                     im[m] = A.y + B.x;
                 }
 #ifndef FFC_C2R_SKIP_ROW
-                stage_a<W, true>(re, im, jj);
+                stage_a<W, true>(re, im, twr);
                 float ore[Q][N1], oim[Q][N1];
                 stage_b<W, true>(ra, 1, re, im, jj, ore, oim);
 #else
@@ -424,7 +492,12 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                                 v.z += in_tf(s.z, sc, sh, a.in_relu);
                                 v.w += in_tf(s.w, sc, sh, a.in_relu);
                             } else {
-                                const float2 s = *reinterpret_cast<const float2*>(trow + x / 2);
+                                float2 s;
+                                if constexpr (RPRE) {
+                                    s = res[rd][i];
+                                } else {
+                                    s = *reinterpret_cast<const float2*>(trow + x / 2);
+                                }
                                 const float s0 = in_tf(s.x, sc, sh, a.in_relu), s1 = in_tf(s.y, sc, sh, a.in_relu);
                                 v.x += s0;
                                 v.y += s0;
@@ -818,9 +891,10 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_cols_kernel(MixArgs a) {
                 }
             }
         __syncthreads();
+        const LaneTw<HC> tw(jj);
         for (int l0 = 0; l0 < C * CPW; l0 += FU2_THREADS / N1) {   // inverse column FFTs (length HC)
             const int line = l0 + tid / N1;
-            if (line < C * CPW) line_fft<HC, true>(Ycol + line * LS, 1, jj);
+            if (line < C * CPW) line_fft<HC, true>(Ycol + line * LS, 1, jj, tw);
         }
         __syncthreads();
         for (int i = tid; i < C * CPW * (HC / 2); i += FU2_THREADS) {
