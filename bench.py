@@ -112,7 +112,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=None,
                    help="number of GPUs / ranks (default: WORLD_SIZE, or 1); starts the ranks itself when "
                         "WORLD_SIZE is unset")
-    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--scaling", choices=["strong", "weak"], default="weak",
                    help="weak (default): every GPU runs the configuration's batch (gen64 256, fgan128 512, "
@@ -630,8 +630,9 @@ def main():
         mv = sum(v["moved"] for v in fu.values())
         fft_roof = {"kernel": "+".join(fu), "bound": "hbm", "achieved": round(b / (ms * 1e-3) / 1e9, 1),
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                    "basis": "SURVEY.md §8d algorithmic bytes: fused train FU 12*N_r, R2C 4*N_r + 8*N_c, "
-                             "C2R 8*N_c + 4*N_r (no spill counted)",
+                    "basis": "SURVEY.md §8d algorithmic bytes per launch (fused train FU 12*N_r, R2C 4*N_r + "
+                             "8*N_c, C2R 8*N_c + 4*N_r; no spill counted), each capped at the bytes the launch "
+                             "moves (the upsample-folded R2C reads t and writes T, 1/4 of the formula)",
                     "algorithmic_bytes_per_step": b / max(1, args.profile_steps),
                     "moved_bytes_per_step": mv / max(1, args.profile_steps),
                     "moved_frac": round(mv / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
@@ -672,8 +673,11 @@ def main():
                          f"{iters - 1} timed iterations in {cpu_el:.1f}s, {args.bn_mode}-mode BN"}
 
     if rank == 0:
+        metric = METRIC if not fgan else (
+            f"fgan128 FGenerator{' + spectral norm, fp16 mix' if sn else ''} fwd images/sec @ B={global_batch // world}"
+            f" per GPU 128x128x3 (BASELINE configs[{4 if sn else 3}])")
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric, "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "ms_per_step_median": round(med, 4), "higher_is_better": True,
             "scaling": args.scaling, "vs_baseline": None,

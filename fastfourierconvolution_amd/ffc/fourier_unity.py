@@ -90,10 +90,10 @@ class FourierUnitSN(nn.Module):
             # pass 0 keeps its mix output Y for pass 1 (no second row R2C + column FFT + mix)
             yspill = torch.empty(int(n_y), device=dev, dtype=torch.float32) if rt.FU_SPILL else None
             # bytes: SURVEY.md §8d's algorithmic basis (fused train FU = 12*N_r: x read in each pass,
-            # out written once); moved: what this kernel pair actually streams (t at the pre-upsample
-            # size, the Y spill written and read back)
-            with rt.observe("fu_pass0", bytes=4.0 * n_r,
-                            moved=4.0 * t.numel() + (4.0 * n_y if rt.FU_SPILL else 0.0)):
+            # out written once), never more than the kernel moves (t is read at the pre-upsample size);
+            # moved: what this kernel pair actually streams (including the Y spill written and read back)
+            mv0 = 4.0 * t.numel() + (4.0 * n_y if rt.FU_SPILL else 0.0)
+            with rt.observe("fu_pass0", bytes=min(4.0 * n_r, mv0), moved=mv0):
                 check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
                                           None if in_fold else ptr(in_shift), int(in_relu), ptr(mixT), 0, ptr(slab),
                                           None, None, 0, None, ctypes.byref(in_fold.struct) if in_fold else None,
@@ -108,9 +108,8 @@ class FourierUnitSN(nn.Module):
                 in_scale, in_shift = in_fold.materialize(stream)
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
-        with rt.observe("fu_pass1", bytes=8.0 * n_r,
-                        moved=(4.0 * n_y if yspill is not None else 4.0 * t.numel()) + 4.0 * t.numel() * bool(residual)
-                        + 4.0 * n_r):
+        mv1 = (4.0 * n_y if yspill is not None else 4.0 * t.numel()) + 4.0 * t.numel() * bool(residual) + 4.0 * n_r
+        with rt.observe("fu_pass1", bytes=min(8.0 * n_r, mv1), moved=mv1):
             check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT), 1,
                                       None, ptr(sc), ptr(sh), int(residual), ptr(out), None,
                                       ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), stream),
@@ -143,12 +142,16 @@ class FourierUnitSN(nn.Module):
         mix_flops = 2.0 * (2 * C) ** 2 * (B * H * (W // 2 + 1))   # (2C x 2C) GEMM over every bin
         T = torch.empty((B, C, h, w // 2 + 1, 2), device=dev, dtype=torch.float32)
         n_r, n_c = float(B * C * H * W), float(B * C * H * (W // 2 + 1))   # SURVEY.md §8d, full resolution
-        with rt.observe("fu2d_r2c", bytes=4.0 * n_r + 8.0 * n_c, moved=4.0 * t.numel() + 8.0 * nT):
+        # SURVEY.md §8d's R2C bytes, capped at what the kernel moves: with the upsample folded in it
+        # reads t (N_r / 4) and writes T (N_c / 4), and counting the full-resolution bytes would credit
+        # bytes never transferred
+        mvr = 4.0 * t.numel() + 8.0 * nT
+        with rt.observe("fu2d_r2c", bytes=min(4.0 * n_r + 8.0 * n_c, mvr), moved=mvr):
             check(L.ffc_fu2d_r2c(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(T), stream),
                   "ffc_fu2d_r2c")
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
-        c2r_bytes = 8.0 * n_c + 4.0 * n_r                                   # SURVEY.md §8d C2R pass
         c2r_moved = 8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)
+        c2r_bytes = min(8.0 * n_c + 4.0 * n_r, c2r_moved)                   # SURVEY.md §8d C2R pass
         if use_batch:
             rows = L.ffc_fu2d_slab_rows(B, C, H, W)
             slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
