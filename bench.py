@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py — FFC-DCGAN generator forward throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gen64|fgan128|fgan128sn|gan64train|block]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload gen64|fgan128|fgan128sn|gan64train|fgan128train|block]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 `--gpus N` without a launcher (WORLD_SIZE unset) starts the N ranks itself
@@ -101,11 +101,14 @@ def time_steps(run, steps, world=1):
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn", "gan64train", "block"], default="gen64",
+    p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn", "gan64train", "fgan128train", "block"],
+                   default="gen64",
                    help="gen64: FFCGenerator 64x64 (BASELINE metric, configs[1]/[2]); "
                         "fgan128: fgan128 FGenerator 128x128x3 (configs[3], 64 per GPU = B 512 / 8); "
                         "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4], 128 per GPU); "
                         "gan64train: generator + discriminator 64x64x3 fwd+bwd + Adam (configs[2], B=256); "
+                        "fgan128train: fgan128 training iteration, G update + D update (fgan128_complete.py:680-703, "
+                        "B=64); "
                         "block: one FFC_BN_ACT 32->32 at 32x32, B=16 (configs[0])")
     p.add_argument("--mix", choices=["fp32", "fp16"], default=None,
                    help="spectral mix arithmetic (default: fp16 for fgan128sn, fp32 otherwise)")
@@ -354,6 +357,153 @@ def train_main(args):
     print(json.dumps(line))
 
 
+def fgan128train_main(args):
+    """One iteration of the fgan128 training loop (fgan128_complete.py:680-703, num_dis_updates = 1):
+    a generator update (z -> FGenerator -> Discriminator -> hinge_loss_gen -> backward through D into
+    G -> AdamW on G, D frozen) then a discriminator update (z -> FGenerator no-grad -> D(fake), D(real)
+    -> hinge_loss_dis -> backward -> AdamW on D), at the reference's default batch 64 (:759), AdamW
+    lr 2e-4 betas (0.5, 0.999) (:624-625), train-mode BN, spectral-norm D (one power iteration per D
+    call), NoiseInjection noise drawn on the GPU.  Both z are redrawn on the GPU every step; the
+    "real" batch is a fixed synthetic tensor in [-1, 1] (no dataset).  Every G / D layer, forward and
+    backward, is a libffc_amd.so kernel (fastfourierconvolution_amd/training.py); the whole iteration
+    is one hipGraph.  Single GPU (the reference's loop is)."""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import _runtime as rt
+    from fastfourierconvolution_amd.training import discriminator_step, generator_step
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("fgan128train is a single-GPU workload (the reference's training loop)")
+    B = args.batch
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    with contextlib.redirect_stdout(io.StringIO()):
+        G = F.FGenerator(128)
+    D = F.Discriminator()
+    G.apply(weights_init)
+    D.apply(weights_init)
+    cpu_state = ({k: v.clone() for k, v in G.state_dict().items()}, {k: v.clone() for k, v in D.state_dict().items()})
+    G, D = G.to(dev).train(), D.to(dev).train()
+    use_graph = not args.no_graph
+    kw = dict(lr=2e-4, betas=(0.5, 0.999), foreach=True, capturable=use_graph)
+    optim_G = torch.optim.AdamW(G.parameters(), **kw)
+    optim_D = torch.optim.AdamW(D.parameters(), **kw)
+    gen = torch.Generator(device="cpu").manual_seed(100)
+    real = (torch.rand((B, 3, 128, 128), generator=gen) * 2 - 1).to(dev)
+    z_g = torch.empty((B, 128), device=dev)
+    z_d = torch.empty((B, 128), device=dev)
+
+    def step():
+        z_g.normal_()
+        loss_G = generator_step(G, D, optim_G, optim_D, z_g)
+        z_d.normal_()
+        loss_D = discriminator_step(G, D, optim_G, optim_D, z_d, real)
+        return loss_G, loss_D
+
+    run = step
+    if use_graph:
+        graph = capture_step(step, warmup=max(2, args.warmup))
+        use_graph = graph is not None
+        if use_graph:
+            run = graph.replay
+    for _ in range(max(1, args.warmup)):
+        run()
+    elapsed, med = time_steps(run, args.steps)
+    value = B * args.steps / elapsed
+    obs = rt.LaunchObserver()
+    rt.set_observer(obs)
+    for _ in range(max(1, args.profile_steps)):
+        step()
+    rt.set_observer(None)
+    summ = obs.summary()
+    nprof = max(1, args.profile_steps)
+    kernels = {k: {"launches_per_step": v["launches"] / nprof, "ms_per_step": v["ms"] / nprof,
+                   "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
+    mm = {k: v for k, v in summ.items() if v["flops"] > 0}
+    dom = max(mm, key=lambda k: mm[k]["ms"])
+    achieved = summ[dom]["flops"] / (summ[dom]["ms"] * 1e-3) / 1e12
+    roof = mfma_roof(dom, achieved)
+    tr = pmc_traffic(dom, args.workload)
+    roof["traffic"] = tr["bytes_per_launch"] if tr else None
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        cpu, parity = fgan128train_cpu(args, cpu_state, dev)
+    line = {
+        "metric": f"fgan128 G+D training iteration images/sec @ B={B} 128x128x3 (fgan128_complete.py:680-703)",
+        "value": round(value, 1), "unit": "images/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "ms_per_step_median": round(med, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: z ~ N(0,1) redrawn on the GPU each step, real = fixed U(-1, 1) batch; weights per "
+                "fgan128_complete.py:23-32 weights_init",
+        "config": {"workload": "FGenerator(z=128) + spectral-norm Discriminator: generator update + 1 discriminator "
+                               "update, hinge losses, AdamW", "global_batch": B, "per_gpu_batch": B,
+                   "bn_mode": "train", "hipgraph": use_graph, "parallelism": "dp1"},
+        "roofline": roof, "cpu_baseline": cpu, "parity": parity, "kernels": kernels,
+    }
+    print(json.dumps(line))
+
+
+def fgan128train_cpu(args, cpu_state, dev):
+    """cpu_baseline: the oracle's fp32 torch-CPU iteration (G update fwd + bwd through D, D update fwd on
+    fake and real + bwd; no optimizer) on a bounded sample; parity: both hinge losses of one HIP iteration
+    (explicit noise, same z) vs the fp64 oracle from the same initial state (u / v included)."""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd.training import discriminator_step, generator_step
+    from oracle.ffc_oracle import fgan128_discriminator, fgan128_generator, hinge_loss_dis, hinge_loss_gen
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    nb = 2
+    gen = torch.Generator().manual_seed(7)
+    zg, zd = torch.randn((nb, 128), generator=gen), torch.randn((nb, 128), generator=gen)
+    real = torch.rand((nb, 3, 128, 128), generator=gen) * 2 - 1
+
+    def noises(dt):
+        g = torch.Generator().manual_seed(8)
+        return [(torch.randn((nb, 1, 2 ** (n + 1), 2 ** (n + 1)), generator=g).to(dt),
+                 torch.randn((nb, 1, 2 ** (n + 1), 2 ** (n + 1)), generator=g).to(dt)) for n in (2, 3, 4, 5, 6)]
+
+    def oracle_iter(dt, fft):
+        sdg = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in cpu_state[0].items()}
+        sdd = {k: (v.to(dt) if v.is_floating_point() else v.clone()) for k, v in cpu_state[1].items()}
+        for k, v in sdg.items():
+            if v.is_floating_point() and not k.endswith(("running_mean", "running_var")):
+                v.requires_grad_(True)
+        lg = hinge_loss_gen(fgan128_discriminator(fgan128_generator(zg.to(dt), sdg, True, noises(dt), fft=fft),
+                                                  sdd, True))
+        lg.backward()
+        for k, v in sdd.items():
+            if k.endswith(("weight_orig", "bias")):
+                v.requires_grad_(True)
+        with torch.no_grad():
+            fake = fgan128_generator(zd.to(dt), sdg, True, noises(dt), fft=fft)
+        ld = hinge_loss_dis(fgan128_discriminator(fake, sdd, True), fgan128_discriminator(real.to(dt), sdd, True))
+        ld.backward()
+        return lg.item(), ld.item()
+    iters, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds or iters == 0:
+        oracle_iter(torch.float32, "torch")
+        iters += 1
+    el = time.perf_counter() - t0
+    cpu = {"value": round(nb * iters / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
+           "sample": f"oracle fp32 torch-CPU fgan128 G+D iteration (torch autograd through the op-for-op reference "
+                     f"path, no optimizer), B={nb}, {iters} iterations in {el:.1f}s, train-mode BN"}
+    ref = oracle_iter(torch.float64, "numpy")
+    with contextlib.redirect_stdout(io.StringIO()):
+        G2 = F.FGenerator(128)
+    D2 = F.Discriminator()
+    G2.load_state_dict(cpu_state[0])
+    D2.load_state_dict(cpu_state[1])
+    G2, D2 = G2.to(dev).train(), D2.to(dev).train()
+    oG = torch.optim.AdamW(G2.parameters(), lr=0.0, weight_decay=0.0)
+    oD = torch.optim.AdamW(D2.parameters(), lr=0.0, weight_decay=0.0)
+    nz = [(a.to(dev), b.to(dev)) for a, b in noises(torch.float32)]
+    lg = generator_step(G2, D2, oG, oD, zg.to(dev), nz).item()
+    ld = discriminator_step(G2, D2, oG, oD, zd.to(dev), real.to(dev), nz).item()
+    parity = {"loss_G_rel_err_vs_fp64_oracle": abs(lg - ref[0]) / abs(ref[0]),
+              "loss_D_rel_err_vs_fp64_oracle": abs(ld - ref[1]) / abs(ref[1]), "mode": f"train, B={nb}, explicit noise",
+              "gradients": "D layer-wise and G step vs the fp64 oracle in tests/test_gpu_fgan_d.py (<= 1e-4 normwise)",
+              "tolerance": 1e-4}
+    return cpu, parity
+
+
 BLOCK_CFG = dict(in_channels=32, out_channels=32, kernel_size=3, ratio_gin=0.5, ratio_gout=0.5, stride=1, padding=1,
                  norm_layer="BatchNorm2d", activation_layer="ReLU")
 
@@ -450,7 +600,7 @@ def block_main(args):
 
 
 GLOBAL_BATCH = {"gen64": 256, "fgan128": 512, "fgan128sn": 1024,   # BASELINE.json configs[1..4]
-                "gan64train": 256, "block": 16}                     # configs[2], configs[0] (one device)
+                "gan64train": 256, "fgan128train": 64, "block": 16}                     # configs[2], configs[0] (one device)
 WEAK_BATCH = dict(GLOBAL_BATCH)   # weak scaling: each GPU runs the configuration's whole batch
 
 
@@ -531,6 +681,10 @@ def main():
         if world > 1:
             raise SystemExit("block is the single-device configs[0] workload")
         return block_main(args)
+    if args.workload == "fgan128train":
+        if args.batch is None:
+            args.batch = 64
+        return fgan128train_main(args)
     if args.workload == "gan64train":
         if world > 1:
             raise SystemExit("gan64train is the single-GPU configs[2] workload")

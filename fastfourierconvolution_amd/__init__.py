@@ -5,16 +5,16 @@
 exports FourierUnitSN, SELayer, SpectralTransform, FFC, FFCTranspose, FFC_BN_ACT, SNFFC, SNFFCTranspose
 (layers/snffc), Resizer,
 Print, debug_print, NoiseInjection (the names layers/__init__.py:2-18 exports for this path)
-plus the restated callers FFCModel / FFCGenerator / FFCDiscriminator / FGenerator (fgan128).  All compute runs in
+plus the restated callers FFCModel / FFCGenerator / FFCDiscriminator / FGenerator and Discriminator (fgan128).  All compute runs in
 the gfx950 HIP library libffc_amd.so (include/ffc_amd.h); there is no CPU fallback.
 """
 from .config import Config
 from .ffc import (FFC, FFC_BN_ACT, SNFFC, FFCTranspose, FourierUnitSN, SELayer, SNFFCTranspose, SpectralTransform,
                   set_mix_precision, spectral_norm_ffc)
 from .layers_misc import NoiseInjection, Print, Resizer, debug_print
-from .models import FFCDiscriminator, FFCGenerator, FFCModel, FGenerator
+from .models import Discriminator, FFCDiscriminator, FFCGenerator, FFCModel, FGanDiscriminator, FGenerator
 
 __all__ = ["FourierUnitSN", "SELayer", "SpectralTransform", "FFC", "FFCTranspose", "FFC_BN_ACT", "SNFFC",
            "SNFFCTranspose", "spectral_norm_ffc", "set_mix_precision", "Resizer",
            "Print", "debug_print", "NoiseInjection", "FFCModel", "FFCGenerator", "FFCDiscriminator", "FGenerator",
-           "Config"]
+           "Discriminator", "FGanDiscriminator", "Config"]

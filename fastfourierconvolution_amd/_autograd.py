@@ -237,6 +237,8 @@ class _ConvLayerFn(torch.autograd.Function):
                 saved_t.append(pre)
             else:
                 saved_t.append(y)
+            if RECORD is not None and act in (1, 2):   # ReLU / LeakyReLU kinks (fgan128 Discriminator)
+                RECORD.append(y.detach())
             outs.append(y)
         ctx.spec = spec
         ctx.save_for_backward(*[x if x is not None else torch.empty(0) for x in xs], *ws, *saved_t)
@@ -563,8 +565,10 @@ class _LinearAs1x1:
 
 
 def linear(owner_cache, lin: nn.Linear, z):
-    """nn.Linear forward + backward (fgan128_complete.py:453-455 noise_to_feature) -> (B, N)"""
+    """nn.Linear forward + backward (fgan128_complete.py:453-455 noise_to_feature, and the spectral-norm
+    fc of the fgan128 Discriminator, :540) -> (B, N)"""
     B, K = z.shape
+    rt.sn_refresh_train(lin)   # the 1x1 view below must see this call's W / sigma
     (y,) = conv_layer(owner_cache, B, [(lin.out_features, 0, 0.0)], [(0, 0, _plan.Seg("pw", K, 1, 1), _LinearAs1x1(lin))],
                       [z.reshape(B, K, 1, 1)])
     return y.reshape(B, lin.out_features)

@@ -1,8 +1,9 @@
 """The reference's callers of the FFC block, restated over the drop-in layers.
 
 FFCModel (models/ffcmodel.py:12-110), FFCGenerator (models/ffc_generator.py:14-44),
-FFCDiscriminator (models/ffc_discriminator.py:11-58) and the fgan128 FGenerator
-(fgan128_complete.py:442-522, BASELINE config 4).  The layer stacks are identical; the
+FFCDiscriminator (models/ffc_discriminator.py:11-58), the fgan128 FGenerator
+(fgan128_complete.py:442-522, BASELINE config 4) and the fgan128 spectral-norm Discriminator it is
+trained against (fgan128_complete.py:525-562).  The layer stacks are identical; the
 only change is that the ``inplanes=`` keyword the reference callers pass (and its base class
 rejects, models/ffcmodel.py:17) is accepted and ignored.
 """
@@ -14,6 +15,7 @@ import torch.nn as nn
 from . import _autograd as ag
 from . import _runtime as rt
 from ._lib import check, ptr
+from . import _plan
 from .config import Config
 from .ffc import FFC_BN_ACT
 from .layers_misc import NoiseInjection, Print, Resizer, debug_print
@@ -209,3 +211,48 @@ class FGenerator(FFCModel):
         out = torch.empty(fake.shape, device=fake.device, dtype=torch.uint8)   # :516-521
         check(rt.lib().ffc_quantize_u8(ptr(fake), ptr(out), fake.numel(), rt.stream_of(fake)), "ffc_quantize_u8")
         return out
+
+
+class Discriminator(FFCModel):
+    """fgan128_complete.py:525-562: the plain-CNN critic FGenerator is trained against (:616, :680-703).
+    conv1..conv9 (3x3 s1 / 4x4 s2 Conv2d with bias, spectral norm when ``sn``), LeakyReLU(0.1) after
+    each, fc = Linear(mg*mg*512, 1) on the flattened 4x4x512 map, no output activation (the reference
+    builds ``last_act`` = Sigmoid and leaves it unused, :545-546, :558).  Module names and the
+    state_dict are the reference's.
+
+    Every conv is one implicit-GEMM launch of libffc_amd.so with bias + LeakyReLU in its epilogue
+    (_autograd.conv_layer: data / weight / bias gradients on the HIP kernels too); the spectral-norm
+    pre-hook runs before each launch as the reference's module call runs it (one power iteration per
+    forward in train mode).  Input: (B, 3, 32*mg, 32*mg) fp32 on the GPU."""
+
+    CONVS = ((3, 64, 3, 1), (64, 64, 4, 2), (64, 128, 3, 1), (128, 128, 4, 2), (128, 256, 3, 1),
+             (256, 256, 4, 2), (256, 512, 3, 1), (512, 512, 4, 2), (512, 512, 4, 2))
+
+    def __init__(self, sn: bool = True, mg: int = 4):
+        super().__init__()
+        self.mg = mg
+        sn_fn = torch.nn.utils.spectral_norm if sn else (lambda m: m)
+        for i, (cin, cout, k, s) in enumerate(self.CONVS, 1):
+            setattr(self, f"conv{i}", sn_fn(nn.Conv2d(cin, cout, k, stride=s, padding=(1, 1))))
+        self.fc = sn_fn(nn.Linear(self.mg * self.mg * 512, 1))
+        self.act = nn.LeakyReLU(0.1)
+        self.last_act = nn.Sigmoid()
+        self._caches = {}
+
+    def forward(self, x):
+        x = rt.require(x, "x")
+        side = 32 * self.mg
+        if x.dim() != 4 or tuple(x.shape[1:]) != (3, side, side):
+            raise RuntimeError(f"Discriminator: x must be (B, 3, {side}, {side}), got {tuple(x.shape)}")
+        act, param = rt.act_code(self.act)
+        m = x
+        for i in range(1, len(self.CONVS) + 1):
+            conv = getattr(self, f"conv{i}")
+            B, C, H, W = m.shape
+            sg = _plan.Seg("conv", C, H, W, conv.kernel_size[0], conv.stride[0], conv.padding[0])
+            (m,) = ag.conv_layer(self._caches.setdefault(i, {}), B, [(conv.out_channels, act, param)],
+                                 [(0, 0, sg, conv)], [m])
+        return ag.linear(self._caches.setdefault("fc", {}), self.fc, m.reshape(m.shape[0], -1))   # :556
+
+
+FGanDiscriminator = Discriminator

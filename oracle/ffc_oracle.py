@@ -19,6 +19,8 @@ BASELINE.json:north_star (file:line citations into /root/reference):
 * NoiseInjection    layers/noise_injection.py:20-32
 * fgan128 FGenerator fgan128_complete.py:442-522 (reconstructed: the script runs main() at import)
 * SNFFC             layers/snffc/snffc.py:12-33 (torch.nn.utils.spectral_norm restated: sn_materialize)
+* fgan128 Discriminator fgan128_complete.py:525-572 (a plain spectral-norm CNN: pinned against torch.nn
+  modules built per those lines, tests/test_oracle_fgan_d.py)
 
 The arithmetic itself lives in the un-vendored third-party dependency PyTorch
 (pinned torch==1.10.2 at requirements.txt:5).  Its published semantics are
@@ -299,13 +301,42 @@ def sn_materialize(sd, dims, training, n_power_iterations=1, eps=1e-12):
             W.reshape(W.shape[0], -1)
         u, v = sd[m + ".weight_u"], sd[m + ".weight_v"]
         if training:
-            for _ in range(n_power_iterations):
-                v = F.normalize(torch.mv(Wm.t(), u), dim=0, eps=eps)
-                u = F.normalize(torch.mv(Wm, v), dim=0, eps=eps)
+            with torch.no_grad():   # u, v are constants of the weight's gradient, as in torch
+                for _ in range(n_power_iterations):
+                    v = F.normalize(torch.mv(Wm.t(), u), dim=0, eps=eps)
+                    u = F.normalize(torch.mv(Wm, v), dim=0, eps=eps)
             sd[m + ".weight_u"], sd[m + ".weight_v"] = u, v
         sigma = torch.dot(u, torch.mv(Wm, v))
         sd[m + ".weight"] = W / sigma
     return sd
+
+
+FGAN_D_CONVS = ((3, 64, 3, 1), (64, 64, 4, 2), (64, 128, 3, 1), (128, 128, 4, 2), (128, 256, 3, 1),
+                (256, 256, 4, 2), (256, 512, 3, 1), (512, 512, 4, 2), (512, 512, 4, 2))
+
+
+def fgan128_discriminator(x, sd, training, sn=True, mg=4):
+    """Discriminator.forward (fgan128_complete.py:525-562): conv1..conv9 (padding 1, bias) each followed
+    by LeakyReLU(0.1), fc on the flattened (512, mg, mg) map, no output activation.  With ``sn`` the
+    spectral-norm weights are materialized first (sn_materialize: one power iteration in training
+    mode, which updates sd's u / v as the reference's module call does)."""
+    if sn:
+        sn_materialize(sd, {}, training)
+    for i, (_, _, k, s) in enumerate(FGAN_D_CONVS, 1):
+        x = F.leaky_relu(F.conv2d(x, _w(sd, f"conv{i}.weight", x.dtype), _w(sd, f"conv{i}.bias", x.dtype),
+                                  stride=s, padding=1), 0.1)
+    x = x.reshape(-1, mg * mg * 512)                                               # :556
+    return F.linear(x, _w(sd, "fc.weight", x.dtype), _w(sd, "fc.bias", x.dtype))
+
+
+def hinge_loss_gen(fake):
+    """fgan128_complete.py:581-585"""
+    return -fake.mean()
+
+
+def hinge_loss_dis(fake, real):
+    """fgan128_complete.py:566-572"""
+    return F.relu(1.0 - real).mean() + F.relu(1.0 + fake).mean()
 
 
 # ----------------------------------------------------------------------------- fixture driver
