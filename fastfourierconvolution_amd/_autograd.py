@@ -170,14 +170,19 @@ def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0
 
 
 def wgrad_splits(B, Mu, NT, P, bt=64):
-    """split-K count for ffc_conv_wgrad: ~512 workgroups (2 per CU), >= 256 k per split (>= 64 when
-    K < 4096), partial sums capped at 32 M floats.  Measured on MI355X over every config-3 weight
-    gradient (tools/wgrad_probe.py, profiles/r01g/wgrad_probe*.log): the workgroup count decides;
-    the former >= 1024-k floor left 1x1 and 8x8-plane gradients on 8-128 workgroups at 2-8x the time"""
+    """split-K count for ffc_conv_wgrad (split-once kernel).  128x128 tiles: >= 512 workgroups and
+    <= 1024 k per split; 64x64 tiles: >= 1024 workgroups and <= 4096 k per split; at most 1024 splits,
+    >= 64 k each, partial sums capped at 32 M floats.  Fitted on MI355X to every weight gradient of
+    the gan64train (B = 256) and fgan128train (B = 64) steps over 4-8 split counts each
+    (tools/wgrad_probe.py, profiles/r03/wgrad/): the large tiles lose to the partial-sum traffic
+    beyond ~1 k-deep splits, the small ones want the deeper grid"""
     tiles = -(-Mu // bt) * -(-NT // bt)
     K = B * P
-    S = -(-512 // max(1, tiles))
-    S = min(S, max(1, K // (256 if K >= 4096 else 64)), max(1, (32 << 20) // max(1, Mu * NT)))
+    if bt >= 128:
+        S = max(-(-512 // max(1, tiles)), K // 1024)
+    else:
+        S = max(-(-1024 // max(1, tiles)), K // 4096)
+    S = min(S, 1024, max(1, K // 64), max(1, (32 << 20) // max(1, Mu * NT)))
     return max(1, S)
 
 
@@ -449,9 +454,10 @@ class _SEFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         vec = (lambda n: torch.empty((B, n, 1, 1), device=dev, dtype=torch.float32)) if hid else (lambda n: None)
         dpre2, hact, dpre1, mean = vec(C), vec(hid), vec(hid), vec(C)
-        with rt.observe("se_bwd", bytes=12.0 * x.numel()):
+        ws = torch.empty(4 * B * C, device=dev, dtype=torch.float32)
+        with rt.observe("se_bwd", bytes=(16.0 if hid else 8.0) * x.numel()):
             check(rt.lib().ffc_se_bwd(ptr(x), ptr(dy), B, C, H, W, ptr(w1) if hid else None, ptr(w2) if hid else None,
-                                      hid, ptr(dx), ptr(dpre2), ptr(hact), ptr(dpre1), ptr(mean), _stream(x)),
+                                      hid, ptr(dx), ptr(dpre2), ptr(hact), ptr(dpre1), ptr(mean), ptr(ws), _stream(x)),
                   "ffc_se_bwd")
         dw1 = dw2 = None
         if not hid:   # Linear(C, 0) / Linear(0, C): empty weights get empty gradients

@@ -191,7 +191,7 @@ SIGNATURES = [
     ("ffc_rfft2_planes", c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
     ("ffc_irfft2_planes", c_int, [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p]),
     ("ffc_se_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("ffc_conv_full_smallm", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int,
                                      c_void_p, c_int, c_float, c_void_p]),
     ("ffc_pool2", c_int, [c_void_p, c_longlong, c_int, c_int, c_float, c_void_p, c_void_p]),

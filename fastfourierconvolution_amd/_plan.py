@@ -325,9 +325,14 @@ def plan_patch_job(B: int, M: int, segs, cfg: int | None = None):
         for si, sg in enumerate(segs):
             ty = _taps(sg, base.Sy, ph.py, sg.IH, ph.PH)
             tx = _taps(sg, base.Sx, ph.px, sg.IW, ph.PW)
-            if NP == 1 and len(ty) == len(tx) == 3 and sg.kind == "conv":
-                # 3x3 (FFC k3, BASELINE configs[0] / fgan128's head): run as 4x4 taps in 4-channel
-                # chunks with a zero-weight 4th row / column (k index -1), one pixel past the 3rd
+            if NP == 1 and len(ty) == len(tx) == 3 and (sg.kind == "conv" or (sg.kind == "convT" and sg.s == 1)):
+                # 3x3 (FFC k3, BASELINE configs[0] / fgan128's head; the stride-1 ConvTranspose2d k3 is
+                # the data gradient of a 3x3 conv, e.g. the fgan128 Discriminator's): run as 4x4 taps in
+                # 4-channel chunks with a zero-weight 4th row / column (k index -1), one pixel past the
+                # 3rd, taps in ascending offset order (a ConvTranspose2d's offsets fall with k)
+                ty, tx = sorted(ty, key=lambda t: t[1]), sorted(tx, key=lambda t: t[1])
+                if any(b[1] - a[1] != 1 for a, b in zip(ty, ty[1:])) or any(b[1] - a[1] != 1 for a, b in zip(tx, tx[1:])):
+                    return None
                 ty = ty + [(-1, ty[-1][1] + 1)]
                 tx = tx + [(-1, tx[-1][1] + 1)]
             T = len(ty) * len(tx)

@@ -332,6 +332,181 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     }
 }
 
+// Split-once variant (default): each staged element is split into its three exact bf16 pieces
+// once, when the workgroup writes the chunk to LDS (three bf16 planes per operand), instead of per
+// use by every wave that reads it; the MFMA loop then reads each operand fragment as three
+// ds_read_b128 (8 consecutive k per lane: the lane-half h of a 32x32x16 bf16 fragment holds
+// k = 8h .. 8h + 7, the same mapping for both operands).  Staging: a thread owns 8 consecutive k of
+// one row per group; when P % 8 == 0 the group lies in one sample, so U comes in as two float4 and
+// the V gather walks its 8 pixels incrementally; the K split is then cut on 8-k boundaries.
+// Row stride 40 bf16 (80 B = 20 dwords): the 16 rows of a ds_read_b128 group hit distinct banks.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgradq_kernel(WgradArgs a) {
+    constexpr int BK = 32, LDR = 40;
+    constexpr int GA = BM * BK / 8 / 256, GB = BN * BK / 8 / 256;   // 8-k groups per thread
+    constexpr int TM = BM / 64, TN = BN / 64;                       // 32x32 tiles per wave per dimension
+    static_assert(GA >= 1 && GB >= 1, "tile too small for 256 staging threads");
+    __shared__ __attribute__((aligned(16))) unsigned short As[3][BM * LDR];
+    __shared__ __attribute__((aligned(16))) unsigned short Bs[3][BN * LDR];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int T = a.k * a.k, NT = a.Nv * T, P = a.PH * a.PW;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN, z = blockIdx.z;
+    const bool vec = (P & 7) == 0;
+    const long long Ktot = (long long)a.B * P;
+    long long K0, K1;
+    if (vec) {
+        const long long K8 = Ktot >> 3;
+        K0 = (K8 * z / a.S) << 3;
+        K1 = (K8 * (z + 1) / a.S) << 3;
+    } else {
+        K0 = Ktot * z / a.S;
+        K1 = Ktot * (z + 1) / a.S;
+    }
+    const size_t VP = (size_t)a.VH * a.VW;
+    const int kq = tid & 3;          // this thread's 8-k group within a chunk: k = 8 kq .. 8 kq + 7
+    const int rb = tid >> 2;         // row of its first group; further groups 64 rows apart
+    bool aok[GA], vok[GB];
+    int vn[GB], vky[GB], vkx[GB];
+#pragma unroll
+    for (int g = 0; g < GA; ++g) aok[g] = m0 + rb + 64 * g < a.Mu;
+#pragma unroll
+    for (int g = 0; g < GB; ++g) {
+        const int col = n0 + rb + 64 * g;
+        vok[g] = col < NT;
+        const int n = vok[g] ? col / T : 0, t = vok[g] ? col - n * T : 0;
+        vn[g] = n;
+        vky[g] = (t / a.k) * a.d - a.p;
+        vkx[g] = (t % a.k) * a.d - a.p;
+    }
+    float av[GA][8], bv[GB][8];
+    auto load_chunk = [&](long long kk0) {
+        const long long kb = kk0 + 8 * kq;
+        if (vec) {
+            if (kb < K1) {
+                const int b = (int)(kb / P), q0 = (int)(kb - (long long)b * P);
+#pragma unroll
+                for (int g = 0; g < GA; ++g) {
+                    if (aok[g]) {
+                        const float4* u = reinterpret_cast<const float4*>(
+                            a.U + ((size_t)b * a.Mu + m0 + rb + 64 * g) * P + q0);
+                        const float4 u0 = u[0], u1 = u[1];
+                        av[g][0] = u0.x; av[g][1] = u0.y; av[g][2] = u0.z; av[g][3] = u0.w;
+                        av[g][4] = u1.x; av[g][5] = u1.y; av[g][6] = u1.z; av[g][7] = u1.w;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) av[g][e] = 0.0f;
+                    }
+                }
+                const int qy0 = q0 / a.PW, qx0 = q0 - qy0 * a.PW;
+                const float* Vb = a.V + (size_t)b * a.Nv * VP;
+#pragma unroll
+                for (int g = 0; g < GB; ++g) {
+                    int qy = qy0, qx = qx0;
+                    const float* Vn = Vb + (size_t)vn[g] * VP;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int iy = qy * a.s + vky[g], ix = qx * a.s + vkx[g];
+                        bv[g][e] = (vok[g] && iy >= 0 && iy < a.VH && ix >= 0 && ix < a.VW)
+                                       ? Vn[(size_t)iy * a.VW + ix] : 0.0f;
+                        if (++qx == a.PW) { qx = 0; ++qy; }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+#pragma unroll
+                    for (int g = 0; g < GA; ++g) av[g][e] = 0.0f;
+#pragma unroll
+                    for (int g = 0; g < GB; ++g) bv[g][e] = 0.0f;
+                }
+            }
+            return;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const long long kk = kb + e;
+            const bool ok = kk < K1;
+            const int b = ok ? (int)(kk / P) : 0, q = ok ? (int)(kk - (long long)b * P) : 0;
+            const int qy = q / a.PW, qx = q - qy * a.PW;
+#pragma unroll
+            for (int g = 0; g < GA; ++g)
+                av[g][e] = (ok && aok[g]) ? a.U[((size_t)b * a.Mu + m0 + rb + 64 * g) * P + q] : 0.0f;
+            const float* Vb = a.V + (size_t)b * a.Nv * VP;
+#pragma unroll
+            for (int g = 0; g < GB; ++g) {
+                const int iy = qy * a.s + vky[g], ix = qx * a.s + vkx[g];
+                bv[g][e] = (ok && vok[g] && iy >= 0 && iy < a.VH && ix >= 0 && ix < a.VW)
+                               ? Vb[(size_t)vn[g] * VP + (size_t)iy * a.VW + ix] : 0.0f;
+            }
+        }
+    };
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+    const int h = lane >> 5, cl = lane & 31;
+    if (K0 < K1) load_chunk(K0);
+    for (long long kk0 = K0; kk0 < K1; kk0 += BK) {
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < GA; ++g) {
+            const Split3 sp = split3(av[g]);
+            const int o = (rb + 64 * g) * LDR + 8 * kq;
+            *reinterpret_cast<bf16x8*>(&As[0][o]) = sp.hi;
+            *reinterpret_cast<bf16x8*>(&As[1][o]) = sp.mid;
+            *reinterpret_cast<bf16x8*>(&As[2][o]) = sp.lo;
+        }
+#pragma unroll
+        for (int g = 0; g < GB; ++g) {
+            const Split3 sp = split3(bv[g]);
+            const int o = (rb + 64 * g) * LDR + 8 * kq;
+            *reinterpret_cast<bf16x8*>(&Bs[0][o]) = sp.hi;
+            *reinterpret_cast<bf16x8*>(&Bs[1][o]) = sp.mid;
+            *reinterpret_cast<bf16x8*>(&Bs[2][o]) = sp.lo;
+        }
+        __syncthreads();
+        if (kk0 + BK < K1) load_chunk(kk0 + BK);   // next chunk's loads overlap this chunk's MFMAs
+#pragma unroll
+        for (int q = 0; q < BK / 16; ++q) {
+            Split3 ys[TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int o = (wn + 32 * j + cl) * LDR + 16 * q + 8 * h;
+                ys[j].hi = *reinterpret_cast<const bf16x8*>(&Bs[0][o]);
+                ys[j].mid = *reinterpret_cast<const bf16x8*>(&Bs[1][o]);
+                ys[j].lo = *reinterpret_cast<const bf16x8*>(&Bs[2][o]);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int o = (wm + 32 * i + cl) * LDR + 16 * q + 8 * h;
+                Split3 xs;
+                xs.hi = *reinterpret_cast<const bf16x8*>(&As[0][o]);
+                xs.mid = *reinterpret_cast<const bf16x8*>(&As[1][o]);
+                xs.lo = *reinterpret_cast<const bf16x8*>(&As[2][o]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_split3(xs, ys[j], acc[i][j]);
+            }
+        }
+    }
+    float* out = a.out + (size_t)z * a.Mu * NT;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn + 32 * j + cl;
+        if (col >= NT) continue;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m < a.Mu) out[(size_t)m * NT + col] = acc[i][j][r];
+            }
+    }
+}
+
 int wgrad_tile(int Mu, int NT) { return (Mu >= 128 && NT >= 128) ? 128 : 64; }
 
 // few weights, many splits: 16 weights x 16 split groups per workgroup, fixed-order LDS combine
@@ -490,82 +665,122 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float* __restrict__ Z
 }
 
 // ------------------------------------------------------------------ SELayer backward
-// One workgroup per sample.  Forward (spectral_transform.py:23-28): m = mean_HW x, h = relu(W1 m),
-// g = sigmoid(W2 h), out = x * g.  Writes dx, and the per-sample vectors the weight gradients
-// need: dpre2 (B, C) = d(W2 h), hact (B, hid), dpre1 (B, hid) = d(W1 m), mean (B, C).
-__global__ __launch_bounds__(256) void se_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dout,
-                                                     int C, int HW, const float* __restrict__ w1,
-                                                     const float* __restrict__ w2, int hid, float* __restrict__ dx,
-                                                     float* __restrict__ dpre2, float* __restrict__ hact_o,
-                                                     float* __restrict__ dpre1, float* __restrict__ mean_o) {
+// Forward (spectral_transform.py:23-28): m = mean_HW x, h = relu(W1 m), g = sigmoid(W2 h), out = x * g.
+// Three launches, so the two plane-wide passes spread over the whole chip (one workgroup per sample
+// ran B workgroups: 1 ms per 128x128 fgan128 layer at B = 64):
+//   sums  one wave per (b, c) plane: ws.mean = mean_HW x, ws.dot = sum_HW dy * x
+//   gate  one workgroup per sample: g, dpre2 = d(W2 h), hact, dpre1 = d(W1 m), dmean = W1^T dpre1 / HW
+//   apply dx = dy * g + dmean (per plane), float4 where HW % 4 == 0
+// ws: 4 * B * C floats (mean, dot, gate, dmean).
+__global__ __launch_bounds__(256) void se_bwd_sums_kernel(const float* __restrict__ x, const float* __restrict__ dout,
+                                                          int P, int HW, float* __restrict__ ws_mean,
+                                                          float* __restrict__ ws_dot) {
+    const int lane = threadIdx.x & 63;
+    const int pl = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pl >= P) return;
+    const float* xp = x + (size_t)pl * HW;
+    const float* dp = dout + (size_t)pl * HW;
+    float s = 0.0f, q = 0.0f;
+    if ((HW & 3) == 0) {
+        const float4* x4 = reinterpret_cast<const float4*>(xp);
+        const float4* d4 = reinterpret_cast<const float4*>(dp);
+        for (int i = lane; i < HW / 4; i += 64) {
+            const float4 a = x4[i], d = d4[i];
+            s += (a.x + a.y) + (a.z + a.w);
+            q = fmaf(d.x, a.x, fmaf(d.y, a.y, fmaf(d.z, a.z, fmaf(d.w, a.w, q))));
+        }
+    } else {
+        for (int i = lane; i < HW; i += 64) {
+            s += xp[i];
+            q = fmaf(dp[i], xp[i], q);
+        }
+    }
+    s = ffc::wave_sum(s);
+    q = ffc::wave_sum(q);
+    if (lane == 0) {
+        ws_mean[pl] = s / (float)HW;
+        ws_dot[pl] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void se_bwd_gate_kernel(int C, int HW, const float* __restrict__ w1,
+                                                          const float* __restrict__ w2, int hid,
+                                                          const float* __restrict__ ws_mean,
+                                                          const float* __restrict__ ws_dot, float* __restrict__ ws_gate,
+                                                          float* __restrict__ ws_dmean, float* __restrict__ dpre2,
+                                                          float* __restrict__ hact_o, float* __restrict__ dpre1,
+                                                          float* __restrict__ mean_o) {
     extern __shared__ float sm[];
     float* mean = sm;            // C
     float* dot = mean + C;       // C
-    float* gate = dot + C;       // C
-    float* dmean = gate + C;     // C
-    float* hpre = dmean + C;     // hid
+    float* hpre = dot + C;       // hid (<= 32)
     float* dp1 = hpre + 32;      // hid
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const float* xb = x + (size_t)b * C * HW;
-    const float* db = dout + (size_t)b * C * HW;
-    for (int c = wave; c < C; c += 4) {
-        float s = 0.0f, q = 0.0f;
-        for (int i = lane; i < HW; i += 64) {
-            const float xv = xb[(size_t)c * HW + i];
-            s += xv;
-            q = fmaf(db[(size_t)c * HW + i], xv, q);
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const size_t o = (size_t)b * C;
+    if (hid == 0) {
+        for (int c = tid; c < C; c += 256) {
+            ws_gate[o + c] = 0.5f;   // Linear(C, 0) -> zeros -> sigmoid(0)
+            ws_dmean[o + c] = 0.0f;
         }
-        s = ffc::wave_sum(s);
-        q = ffc::wave_sum(q);
-        if (lane == 0) {
-            mean[c] = s / (float)HW;
-            dot[c] = q;
-        }
+        return;
+    }
+    for (int c = tid; c < C; c += 256) {
+        mean[c] = ws_mean[o + c];
+        dot[c] = ws_dot[o + c];
     }
     __syncthreads();
-    if (hid > 0) {
-        if (tid < hid) {
-            float s = 0.0f;
-            for (int c = 0; c < C; ++c) s = fmaf(w1[(size_t)tid * C + c], mean[c], s);
-            hpre[tid] = s;
-        }
-        __syncthreads();
-        for (int c = tid; c < C; c += 256) {
-            float s = 0.0f;
-            for (int j = 0; j < hid; ++j) s = fmaf(w2[(size_t)c * hid + j], fmaxf(hpre[j], 0.0f), s);
-            const float g = 1.0f / (1.0f + expf(-s));
-            gate[c] = g;
-            const float d2 = dot[c] * g * (1.0f - g);
-            dot[c] = d2;
-            dpre2[(size_t)b * C + c] = d2;
-            mean_o[(size_t)b * C + c] = mean[c];
-        }
-        __syncthreads();
-        if (tid < hid) {
-            float s = 0.0f;
-            for (int c = 0; c < C; ++c) s = fmaf(w2[(size_t)c * hid + tid], dot[c], s);
-            const float d1 = hpre[tid] > 0.0f ? s : 0.0f;
-            dp1[tid] = d1;
-            dpre1[(size_t)b * hid + tid] = d1;
-            hact_o[(size_t)b * hid + tid] = fmaxf(hpre[tid], 0.0f);
-        }
-        __syncthreads();
-        for (int c = tid; c < C; c += 256) {
-            float s = 0.0f;
-            for (int j = 0; j < hid; ++j) s = fmaf(w1[(size_t)j * C + c], dp1[j], s);
-            dmean[c] = s / (float)HW;
+    if (tid < hid) {
+        float s = 0.0f;
+        for (int c = 0; c < C; ++c) s = fmaf(w1[(size_t)tid * C + c], mean[c], s);
+        hpre[tid] = s;
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        float s = 0.0f;
+        for (int j = 0; j < hid; ++j) s = fmaf(w2[(size_t)c * hid + j], fmaxf(hpre[j], 0.0f), s);
+        const float g = 1.0f / (1.0f + expf(-s));
+        ws_gate[o + c] = g;
+        const float d2 = dot[c] * g * (1.0f - g);
+        dot[c] = d2;
+        dpre2[o + c] = d2;
+        mean_o[o + c] = mean[c];
+    }
+    __syncthreads();
+    if (tid < hid) {
+        float s = 0.0f;
+        for (int c = 0; c < C; ++c) s = fmaf(w2[(size_t)c * hid + tid], dot[c], s);
+        const float d1 = hpre[tid] > 0.0f ? s : 0.0f;
+        dp1[tid] = d1;
+        dpre1[(size_t)b * hid + tid] = d1;
+        hact_o[(size_t)b * hid + tid] = fmaxf(hpre[tid], 0.0f);
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        float s = 0.0f;
+        for (int j = 0; j < hid; ++j) s = fmaf(w1[(size_t)j * C + c], dp1[j], s);
+        ws_dmean[o + c] = s / (float)HW;
+    }
+}
+
+__global__ __launch_bounds__(256) void se_bwd_apply_kernel(const float* __restrict__ dout, long long n, int HW,
+                                                           const float* __restrict__ gate,
+                                                           const float* __restrict__ dmean, float* __restrict__ dx) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    if ((HW & 3) == 0) {
+        const int hw4 = HW / 4;
+        const float4* d4 = reinterpret_cast<const float4*>(dout);
+        float4* o4 = reinterpret_cast<float4*>(dx);
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += stride) {
+            const long long pl = i / hw4;
+            const float g = gate[pl], m = dmean[pl];
+            const float4 d = d4[i];
+            o4[i] = make_float4(fmaf(d.x, g, m), fmaf(d.y, g, m), fmaf(d.z, g, m), fmaf(d.w, g, m));
         }
     } else {
-        for (int c = tid; c < C; c += 256) {
-            gate[c] = 0.5f;   // Linear(C, 0) -> zeros -> sigmoid(0)
-            dmean[c] = 0.0f;
+        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+            const long long pl = i / HW;
+            dx[i] = fmaf(dout[i], gate[pl], dmean[pl]);
         }
-    }
-    __syncthreads();
-    float* dxb = dx + (size_t)b * C * HW;
-    for (size_t i = tid; i < (size_t)C * HW; i += 256) {
-        const int c = (int)(i / HW);
-        dxb[i] = fmaf(db[i], gate[c], dmean[c]);
     }
 }
 
@@ -771,7 +986,10 @@ extern "C" int ffc_conv_wgrad(const float* U, int Mu, int PH, int PW, const floa
         return e && std::string(e) == "f32";
     }();
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, (hipStream_t)stream, a); };
-    if (bt == 128) {   // 32-deep chunks: 64 MFMAs per wave between barriers (measured 18 % faster than 16)
+    const char* kv = getenv("FFC_WGRAD_KERNEL");   // A/B knob: "old" = the split-per-use kernel below
+    if (!exact && !bk_knob && !(kv && std::string(kv) == "old")) {
+        bt == 128 ? go(wgradq_kernel<128, 128>) : go(wgradq_kernel<64, 64>);
+    } else if (bt == 128) {   // 32-deep chunks: 64 MFMAs per wave between barriers (measured 18 % faster than 16)
         if (bk_knob == 16)
             exact ? go(wgrad_kernel<128, 16, false>) : go(wgrad_kernel<128, 16, true>);
         else
@@ -826,14 +1044,26 @@ extern "C" int ffc_irfft2_planes(const float* Z, int P, int H, int W, float inte
 
 extern "C" int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H, int W, const float* w1,
                           const float* w2, int hidden, float* dx, float* dpre2, float* hact, float* dpre1, float* mean,
-                          void* stream) {
-    FFC_CHECK_ARG(x && dout && dx && B > 0 && C > 0 && H > 0 && W > 0 && hidden >= 0 && hidden <= 32,
+                          float* ws, void* stream) {
+    FFC_CHECK_ARG(x && dout && dx && ws && B > 0 && C > 0 && H > 0 && W > 0 && hidden >= 0 && hidden <= 32,
                   "ffc_se_bwd: bad args");
     FFC_CHECK_ARG(hidden == 0 || (w1 && w2 && dpre2 && hact && dpre1 && mean), "ffc_se_bwd: missing buffers");
-    const size_t lds = (4 * (size_t)C + 64) * sizeof(float);
+    const size_t lds = (2 * (size_t)C + 64) * sizeof(float);
     FFC_CHECK_ARG(lds <= 64 * 1024, "ffc_se_bwd: too many channels");
-    hipLaunchKernelGGL(se_bwd_kernel, dim3(B), dim3(256), lds, (hipStream_t)stream, x, dout, C, H * W, w1, w2, hidden,
-                       dx, dpre2, hact, dpre1, mean);
+    const int P = B * C, HW = H * W;
+    float* ws_mean = ws;
+    float* ws_dot = ws + P;
+    float* ws_gate = ws + 2 * (size_t)P;
+    float* ws_dmean = ws + 3 * (size_t)P;
+    hipStream_t s = (hipStream_t)stream;
+    if (hidden > 0)
+        hipLaunchKernelGGL(se_bwd_sums_kernel, dim3((P + 3) / 4), dim3(256), 0, s, x, dout, P, HW, ws_mean, ws_dot);
+    hipLaunchKernelGGL(se_bwd_gate_kernel, dim3(B), dim3(256), lds, s, C, HW, w1, w2, hidden, ws_mean, ws_dot,
+                       ws_gate, ws_dmean, dpre2, hact, dpre1, mean);
+    const long long n = (long long)P * HW;
+    const long long units = (HW & 3) == 0 ? n / 4 : n;
+    const int grid = (int)std::min<long long>((units + 255) / 256, 8192);
+    hipLaunchKernelGGL(se_bwd_apply_kernel, dim3(grid), dim3(256), 0, s, dout, n, HW, ws_gate, ws_dmean, dx);
     return ffc::launch_status("ffc_se_bwd");
 }
 

@@ -521,11 +521,12 @@ int ffc_rfft2_planes(const float* x, int P, int H, int W, float interior_scale, 
  * power-of-two planes 16..128 on line FFTs, other planes (H, W <= 64) on direct DFTs. */
 int ffc_irfft2_planes(const float* Z, int P, int H, int W, float interior_scale, const float* addend, float* y,
                       void* stream);
-/* SELayer backward (spectral_transform.py:23-28), one workgroup per sample: dx, plus the
- * per-sample vectors of the two Linear weight gradients: dpre2 (B, C), hact (B, hidden),
- * dpre1 (B, hidden), mean (B, C).  hidden = C // 16 may be 0 (gate 0.5). */
+/* SELayer backward (spectral_transform.py:23-28): dx, plus the per-sample vectors of the two
+ * Linear weight gradients: dpre2 (B, C), hact (B, hidden), dpre1 (B, hidden), mean (B, C).
+ * hidden = C // 16 may be 0 (gate 0.5).  ws: 4 * B * C floats of scratch (per-plane sums, gate,
+ * mean gradient); three launches (plane sums over the whole chip, per-sample gate, dx). */
 int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H, int W, const float* w1, const float* w2,
-               int hidden, float* dx, float* dpre2, float* hact, float* dpre1, float* mean, void* stream);
+               int hidden, float* dx, float* dpre2, float* hact, float* dpre1, float* mean, float* ws, void* stream);
 /* Conv2d whose kernel covers the whole input plane (k == H == W, padding 0 -> 1x1 output) with
  * M <= 4 outputs, up to two summed segments (FFCDiscriminator's last FFC_BN_ACT, 4x4 -> 1x1 + Sigmoid,
  * models/ffc_discriminator.py:31; ffc.py:89-97): out[b][m] = act(sum x_s[b][k] w_s[m][k] + bias[m]),

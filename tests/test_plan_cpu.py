@@ -174,6 +174,9 @@ def emulate_patch(plan, xs, ws, layouts):
                 if ch >= sg.C:
                     assert sx == 15
                     continue
+                if sx == 15:   # a 3x3 job's zero-weight 4th tap row / column (4x4 taps)
+                    assert T == 16 and sg.k == 3
+                    continue
                 assert sx == (s | (ch << 4))
                 tt = plan.taptab[ph["tap_base"][s] + t]
                 dy, dx = int(tt) >> 16, int(tt) & 0xFFFF
@@ -211,6 +214,10 @@ PATCH_CASES = {
     "conv_k4s2p1": [_plan.Seg("conv", 5, 8, 8, 4, 2, 1), _plan.Seg("conv", 3, 8, 8, 4, 2, 1)],
     "conv_k4s2p1_pw": [_plan.Seg("conv", 6, 16, 16, 4, 2, 1), _plan.Seg("pw", 5, 8, 8)],
     "conv_k4s2p1_odd": [_plan.Seg("conv", 3, 9, 7, 4, 2, 1)],
+    "conv_k3s1p1": [_plan.Seg("conv", 5, 8, 12, 3, 1, 1)],
+    # the data gradient of a 3x3 conv (fgan128 Discriminator conv3 / conv5 / conv7): ConvTranspose2d k3 s1 p1
+    "convT_k3s1p1": [_plan.Seg("convT", 6, 8, 8, 3, 1, 1)],
+    "convT_k3s1p1_odd": [_plan.Seg("convT", 3, 5, 7, 3, 1, 1)],
 }
 
 

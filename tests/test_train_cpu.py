@@ -45,7 +45,7 @@ def test_wgrad_splits_bounded():
         for Mu, NT, P in ((128, 1024, 16), (3, 512, 1024), (512, 512, 12), (16, 256, 1)):
             S = wgrad_splits(B, Mu, NT, P)
             K = B * P
-            assert 1 <= S <= max(1, K // (256 if K >= 4096 else 64)) and S * Mu * NT <= max(Mu * NT, 32 << 20)
+            assert 1 <= S <= min(1024, max(1, K // 64)) and S * Mu * NT <= max(Mu * NT, 32 << 20)
 
 
 def _tw(N):
