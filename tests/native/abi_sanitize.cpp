@@ -185,7 +185,7 @@ static void validation_paths() {
     EXPECT_INVALID(ffc_conv_wgrad(cp, 4, 4, 4, cp, 4, 4, 4, 1, 3, 1, 1, 1, 2, nullptr, p, 0, nullptr), "workspace");
     EXPECT_INVALID(ffc_rfft2_planes(cp, 1, 128, 96, 1.f, p, nullptr), "ffc_rfft2_planes");
     EXPECT_INVALID(ffc_irfft2_planes(cp, 1, 8, 1, 1.f, nullptr, p, nullptr), "ffc_irfft2_planes");
-    EXPECT_INVALID(ffc_se_bwd(cp, cp, 1, 4, 4, 4, nullptr, nullptr, 40, p, p, p, p, p, nullptr), "ffc_se_bwd");
+    EXPECT_INVALID(ffc_se_bwd(cp, cp, 1, 4, 4, 4, nullptr, nullptr, 40, p, p, p, p, p, p, nullptr), "ffc_se_bwd");
     EXPECT_INVALID(ffc_conv_full_smallm(cp, 16, cp, nullptr, 0, nullptr, nullptr, 1, 9, p, 0, 0.f, nullptr),
                    "ffc_conv_full_smallm");
     EXPECT_INVALID(ffc_pool2(cp, 1, 3, 4, 0.25f, p, nullptr), "ffc_pool2");
