@@ -243,6 +243,33 @@ def test_smallm_convt_vs_oracle(M, H, W, bias):
     assert normwise_err(ol.cpu(), rl) <= TOL
 
 
+@pytest.mark.parametrize("cin,M,H,W,bias", [(64, 3, 32, 32, False), (64, 1, 32, 32, True), (32, 4, 12, 20, True),
+                                              (16, 3, 8, 36, False), (128, 2, 16, 48, False)])
+def test_smallm_convt_mfma_vs_oracle(cin, M, H, W, bias):
+    """ConvT k4 s2 p1 with M <= 4 at shapes the MFMA small-M kernel takes (both segments a multiple of 8
+    channels, W even; smallm_mfma.hip, used under FFC_SMALLM_MFMA=1, see the subprocess test below) --
+    the FFC-DCGAN generator's last layer (models/ffc_generator.py:28) and ragged 8 x 32 tiles"""
+    import fastfourierconvolution_amd as F
+    from oracle.ffc_oracle import ffc_bn_act
+    cfg = dict(in_channels=cin, out_channels=M, kernel_size=4, ratio_gin=0.5, ratio_gout=0.0, stride=2, padding=1,
+               bias=bias, activation_layer="Tanh", upsampling=True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = F.FFC_BN_ACT(cin, M, 4, 0.5, 0.0, 2, 1, bias=bias, activation_layer=torch.nn.Tanh, upsampling=True)
+    gen = torch.Generator().manual_seed(cin + M + H)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn(p.shape, generator=gen) * (2.0 / cin) ** 0.5)
+    sd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in m.state_dict().items()}
+    xl = torch.randn(3, cin // 2, H, W, generator=gen)
+    xg = torch.randn(3, cin // 2, H, W, generator=gen)
+    m = m.cuda()
+    with torch.no_grad():
+        ol, og = m((xl.cuda(), xg.cuda()))
+        rl, rg = ffc_bn_act((xl.double(), xg.double()), sd, "", cfg, True)
+    assert og == 0 and rg == 0
+    assert normwise_err(ol.cpu(), rl) <= 1e-5
+
+
 def _w_sharded_gpu(rank, port, out_dir):
     """one rank of a 2-way sample shard on cuda:0 (gloo carries the BN moments; RCCL needs one
     GPU per rank, which the 1-GPU test box does not have)"""
@@ -343,3 +370,19 @@ def test_pointwise_conv_kernels(B, C, M, H, patch):
     finally:
         rt.USE_PATCH = old
     assert normwise_err(out.cpu(), ref.cpu()) <= TOL
+
+
+def test_smallm_mfma_kernels_in_subprocess():
+    """the MFMA small-M kernels (smallm_mfma.hip, off by default: measured slower than the VALU
+    kernels) still match the oracle: the ConvT and deferred-head parity tests rerun in a child
+    process with FFC_SMALLM_MFMA=1"""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, FFC_SMALLM_MFMA="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(here, "test_gpu_parity.py") + "::test_smallm_convt_mfma_vs_oracle",
+                        os.path.join(here, "test_gpu_defer.py") + "::test_conv3x3_smallm_tf_ragged"],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
