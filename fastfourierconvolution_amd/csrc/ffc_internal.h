@@ -32,8 +32,31 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 static __device__ __forceinline__ Split3 split3(const float (&v)[8]) {
     u32x4 hv, mv, lv;
+#ifndef FFC_SPLIT_PACKED
+    // scalar v_sub_f32: packed f32 VALU (v_pk_add_f32) costs extra issue cycles beside MFMAs
+    // (MI355X_MICROARCH.md issue-cost rows), and the staging / split code runs beside the MFMA
+    // waves on the same SIMD.  Scalar split + no SLP packing (build.py -fno-slp-vectorize), measured
+    // against the packed split (profiles/r03/s2d): gen64 0.4915 -> 0.4810 ms, fgan128 16.03 -> 15.51 ms,
+    // gan64train 10.43 -> 9.85 ms.  Same operations, bit-identical pieces.  FFC_SPLIT_PACKED: the old form.
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {   // element pairs: the subtractions as v_pk_add_f32
+    for (int q = 0; q < 4; ++q) {
+        unsigned u[2], u1[2], u2[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float a = v[2 * q + e];
+            u[e] = __builtin_bit_cast(unsigned, a);
+            const float r1 = a - __builtin_bit_cast(float, u[e] & 0xFFFF0000u);
+            u1[e] = __builtin_bit_cast(unsigned, r1);
+            const float r2 = r1 - __builtin_bit_cast(float, u1[e] & 0xFFFF0000u);
+            u2[e] = __builtin_bit_cast(unsigned, r2);
+        }
+        hv[q] = pack_hi16(u[0], u[1]);
+        mv[q] = pack_hi16(u1[0], u1[1]);
+        lv[q] = pack_hi16(u2[0], u2[1]);
+    }
+#else
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // element pairs: the subtractions as v_pk_add_f32 (FFC_SPLIT_PACKED)
         const f32x2 a = {v[2 * q], v[2 * q + 1]};
         const u32x2 ua = __builtin_bit_cast(u32x2, a);
         const f32x2 r1 = a - __builtin_bit_cast(f32x2, ua & 0xFFFF0000u);
@@ -44,6 +67,7 @@ static __device__ __forceinline__ Split3 split3(const float (&v)[8]) {
         mv[q] = pack_hi16(u1[0], u1[1]);
         lv[q] = pack_hi16(u2[0], u2[1]);
     }
+#endif
     Split3 s;
     s.hi = __builtin_bit_cast(bf16x8, hv);
     s.mid = __builtin_bit_cast(bf16x8, mv);
