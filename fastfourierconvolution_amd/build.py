@@ -18,9 +18,7 @@ LIB = os.path.join(PKG, "libffc_amd.so")
 BUILD = os.path.join(PKG, "build_obj")
 ARCH = os.environ.get("FFC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
-# -fno-slp-vectorize: no SLP packing of adjacent scalar f32 ops into v_pk_*_f32, which cost extra issue
-# cycles beside MFMAs on gfx950 (ffc_internal.h split3; measured in profiles/r03/s2d)
-FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-fno-slp-vectorize"]
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 
 
 def sources():

@@ -40,6 +40,10 @@
 namespace {
 
 constexpr int QTHREADS = 512;   // 4 compute waves + 4 staging waves
+#ifndef FFC_CONVQ_PRIO
+#define FFC_CONVQ_PRIO 0   // static wave priority (A/B): 1 staging waves, 2 compute waves; both within
+                           // +-0.5 % of none on gen64 / fgan128 (profiles/r03/s2e)
+#endif
 #ifndef FFC_CONVQ_SLOTS
 #define FFC_CONVQ_SLOTS 2
 #endif
@@ -730,6 +734,11 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
     const ConvQArgs& args = args_byval;
 #endif
     extern __shared__ __attribute__((aligned(16))) char lds[];
+#if FFC_CONVQ_PRIO == 1
+    if ((threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);   // staging waves win VALU arbitration
+#elif FFC_CONVQ_PRIO == 2
+    if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(1);    // compute waves win it
+#endif
     int pend = -1;   // staging waves: the tile whose epilogue is still in the hand-off area
     for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW>(args, tix, lds, pend);
     if (args.epi_off >= 0) {

@@ -35,9 +35,11 @@ static __device__ __forceinline__ Split3 split3(const float (&v)[8]) {
 #ifndef FFC_SPLIT_PACKED
     // scalar v_sub_f32: packed f32 VALU (v_pk_add_f32) costs extra issue cycles beside MFMAs
     // (MI355X_MICROARCH.md issue-cost rows), and the staging / split code runs beside the MFMA
-    // waves on the same SIMD.  Scalar split + no SLP packing (build.py -fno-slp-vectorize), measured
-    // against the packed split (profiles/r03/s2d): gen64 0.4915 -> 0.4810 ms, fgan128 16.03 -> 15.51 ms,
-    // gan64train 10.43 -> 9.85 ms.  Same operations, bit-identical pieces.  FFC_SPLIT_PACKED: the old form.
+    // waves on the same SIMD.  Same operations, bit-identical pieces; FFC_SPLIT_PACKED: the old form.
+    // Same-box A/B (profiles/r03/s2e): gen64 0.4775 -> 0.4678 ms, fgan128 15.88 -> 15.50 ms, gan64train
+    // 10.22 -> 9.97 ms.
+    // (A whole-library -fno-slp-vectorize build was faster still but broke the B = 8 generator smoke
+    // test -- profiles/r03/s2f -- so the library keeps the default vectorizer.)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         unsigned u[2], u1[2], u2[2];

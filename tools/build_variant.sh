@@ -15,7 +15,7 @@ objs=()
 for src in "$tmp"/fastfourierconvolution_amd/csrc/*.hip "$tmp"/fastfourierconvolution_amd/csrc/*.cpp; do
   o="$tmp/$(basename "$src").o"
   if [[ $src == *.cpp ]]; then x="-x hip"; else x=""; fi
-  hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -fno-slp-vectorize ${VARIANT_FLAGS:-} $x -c "$src" -o "$o" &
+  hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 ${VARIANT_FLAGS:-} $x -c "$src" -o "$o" &
   objs+=("$o")
 done
 wait
