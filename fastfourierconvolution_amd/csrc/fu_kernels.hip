@@ -18,6 +18,7 @@
 #include "bn_common.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 #include <set>
 
@@ -363,6 +364,80 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     }
 }
 
+// Pass 1 from the spilled Y, split over channel groups: one wave per (sample, 64 / H channels).
+// fu_kernel's pass 1 runs a whole sample per 8-wave workgroup, one workgroup per CU at B = 256, so
+// its load / column-IFFT / row-C2R phases cannot overlap; pass 1 needs no cross-channel data (the
+// mix ran in pass 0), so here every wave takes 64 / H channels (64 rows, (64 / H) (W/2 + 1) column
+// lines) and many waves share a CU.  Same arithmetic per line as fu_kernel (bit-identical).
+template <int H, int W, int UP>
+__global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
+    constexpr int WP = W / 2 + 1;
+    constexpr int NB = H * WP;
+    constexpr int CPG = 64 / H;   // channels per wave
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int C = a.C, C2 = 2 * C;
+    const int ngroups = C / CPG;
+    const int b = blockIdx.x / ngroups, c0 = (blockIdx.x - b * ngroups) * CPG;
+    const int tid = threadIdx.x;
+    float* Yre = smem;
+    float* Yim = Yre + CPG * NB;
+    // Y rows 2 c0 .. 2 (c0 + CPG) of this sample -> BN + ReLU -> the Y planes
+    const float4* ys = reinterpret_cast<const float4*>(a.yspill + ((size_t)b * C2 + 2 * c0) * NB);
+    for (int i = tid; i < 2 * CPG * NB / 4; i += 64) {
+        const int ol = (4 * i) / NB, n = 4 * i - ol * NB, o = 2 * c0 + ol;
+        const float4 v = ys[i];
+        const float sc = a.bn_scale[o], sh = a.bn_shift[o];
+        float* dst = ((ol & 1) ? Yim : Yre) + (ol >> 1) * NB + n;
+        *reinterpret_cast<float4*>(dst) = make_float4(fmaxf(fmaf(v.x, sc, sh), 0.0f), fmaxf(fmaf(v.y, sc, sh), 0.0f),
+                                                      fmaxf(fmaf(v.z, sc, sh), 0.0f), fmaxf(fmaf(v.w, sc, sh), 0.0f));
+    }
+    __syncthreads();
+    for (int q = tid; q < CPG * WP; q += 64) {   // inverse column C2C over H, ortho scale
+        const int ch = q / WP, k = q - ch * WP;
+        float* yr = Yre + ch * NB + k;
+        float* yi = Yim + ch * NB + k;
+        float re[H], im[H];
+#pragma unroll
+        for (int y = 0; y < H; ++y) {
+            re[y] = yr[y * WP];
+            im[y] = yi[y * WP];
+        }
+        fft_reg<H, true>(re, im);
+#pragma unroll
+        for (int y = 0; y < H; ++y) {
+            yr[y * WP] = re[y] * a.norm;
+            yi[y * WP] = im[y] * a.norm;
+        }
+    }
+    __syncthreads();
+    {   // per-row C2R over W + residual: one row per lane (CPG * H = 64)
+        const int ch = tid / H, y = tid - ch * H;
+        const float* yr = Yre + (ch * H + y) * WP;
+        const float* yi = Yim + (ch * H + y) * WP;
+        float re[W], im[W];
+        re[0] = yr[0];
+        im[0] = 0.0f;
+#pragma unroll
+        for (int k = 1; k < W / 2; ++k) {
+            const float vr = yr[k], vi = yi[k];
+            re[k] = vr;
+            im[k] = vi;
+            re[W - k] = vr;
+            im[W - k] = -vi;
+        }
+        re[W / 2] = yr[W / 2];
+        im[W / 2] = 0.0f;
+        fft_reg<W, true>(re, im);
+        if (a.residual) {
+            float sres[W];
+            load_s_row<W, UP>(a, nullptr, b, c0 + ch, y, H, sres);
+#pragma unroll
+            for (int x = 0; x < W; ++x) re[x] += sres[x];
+        }
+        store_row<W>(a.out + ((size_t)(b * C + c0 + ch) * H + y) * W, re);
+    }
+}
+
 // out[k][o] = w[o][k] for o < R (zero for R <= o < Rpad); w is (R, K) row-major
 __global__ void pack_transpose_kernel(const float* __restrict__ w, int R, int K, int Rpad, float* __restrict__ wt) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -401,6 +476,24 @@ FuKernel pick_kernel(int H, int W, int up, int pass) {
 }
 
 bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
+
+FuKernel pick_split(int H, int W, int up) {
+    if (H != W) return nullptr;
+    switch (H) {
+        case 8: return up == 1 ? fu_pass1_split_kernel<8, 8, 1> : fu_pass1_split_kernel<8, 8, 2>;
+        case 16: return up == 1 ? fu_pass1_split_kernel<16, 16, 1> : fu_pass1_split_kernel<16, 16, 2>;
+        case 32: return up == 1 ? fu_pass1_split_kernel<32, 32, 1> : fu_pass1_split_kernel<32, 32, 2>;
+    }
+    return nullptr;
+}
+// FFC_FU_SPLIT=0: pass 1 as one workgroup per sample (fu_kernel) for A/B runs
+bool fu_split_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("FFC_FU_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 // LDS plan: Z/Y planes, then the mix weight when it fits, then the stats scratch unless it fits in
 // the Y-imaginary plane.  bytes = 0: unsupported.
@@ -514,6 +607,15 @@ extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int
                 return FFC_E_LAUNCH;
             }
             raised.insert(reinterpret_cast<const void*>(k));
+        }
+    }
+    // pass 1 from the spill with the BN scale / shift given: one wave per (sample, 64 / H channels)
+    if (pass == 1 && yspill && !mix_fold && fu_split_on() && H * W <= 64 * 64 && H <= 64 && C % (64 / H) == 0) {
+        FuKernel ks = pick_split(H, W, up);
+        if (ks) {
+            const size_t slds = (size_t)2 * (64 / H) * H * (W / 2 + 1) * sizeof(float);
+            hipLaunchKernelGGL(ks, dim3((unsigned)B * (C / (64 / H))), dim3(64), slds, (hipStream_t)stream, a);
+            return ffc::launch_status("ffc_fu_forward");
         }
     }
     hipLaunchKernelGGL(k, dim3(B), dim3(FU_THREADS), lds, (hipStream_t)stream, a);
