@@ -32,6 +32,9 @@ __device__ __forceinline__ void fft_reg(float (&re)[N], float (&im)[N]) {
         const int step = 128 / (2 * half);
 #pragma unroll
         for (int j = 0; j < half; ++j) {
+            // twiddle W_{2 half}^j: 1 at j = 0, -i (forward) / +i (inverse) at the quarter turn -- both
+            // multiply-free (the table's cos(pi/2) is 6e-17, not 0); the rest from the table
+            const bool quarter = j * step == 32;
             float wr = 1.0f, wi = 0.0f;
             if (j != 0) {
                 wr = c_twc[j * step];
@@ -39,8 +42,17 @@ __device__ __forceinline__ void fft_reg(float (&re)[N], float (&im)[N]) {
             }
 #pragma unroll
             for (int i = j; i < N; i += 2 * half) {
-                const float xr = re[i + half] * wr - im[i + half] * wi;
-                const float xi = re[i + half] * wi + im[i + half] * wr;
+                float xr, xi;
+                if (j == 0) {
+                    xr = re[i + half];
+                    xi = im[i + half];
+                } else if (quarter) {
+                    xr = INV ? -im[i + half] : im[i + half];
+                    xi = INV ? re[i + half] : -re[i + half];
+                } else {
+                    xr = re[i + half] * wr - im[i + half] * wi;
+                    xi = re[i + half] * wi + im[i + half] * wr;
+                }
                 re[i + half] = re[i] - xr;
                 im[i + half] = im[i] - xi;
                 re[i] += xr;
