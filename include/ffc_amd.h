@@ -349,7 +349,8 @@ typedef struct ffc_in_tf {
 
 /* ffc_conv3x3_smallm over deferred inputs: segment s is read through tf_s (NULL: as stored).
  * Replaces the producer's ffc_bn_act_noise_apply pass + ffc_conv3x3_smallm (the fgan128 conv6 ->
- * conv7 hand-off); results are bit-identical to that pair. */
+ * conv7 hand-off); results match that pair to within 2e-6 normwise (this kernel's GELU uses the
+ * A&S 7.1.26 erf, |error| <= 1.5e-7; the apply pass uses erff). */
 int ffc_conv3x3_smallm_tf(const float* x0, int C0, const float* w0, const float* x1, int C1,
                           const float* w1, const float* bias, int B, int H, int W, int M, float* out,
                           int act, float act_param, const ffc_in_tf* tf0, const ffc_in_tf* tf1,
