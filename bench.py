@@ -71,6 +71,23 @@ def mfma_roof(dom, achieved):
     return r
 
 
+def profile_pass(step, n):
+    """One instrumented eager pass (rt.LaunchObserver: HIP events around every library launch on its
+    stream) of ``n`` steps.  The GPU is held busy (torch.cuda._sleep) while the host enqueues each
+    step, so the stream never runs dry inside an event pair: the events then time the kernels alone,
+    not the host's op-dispatch gaps between them.  -> (observer summary, last step's output)"""
+    from fastfourierconvolution_amd import _runtime as rt
+    obs = rt.LaunchObserver()
+    out = None
+    for _ in range(max(1, n)):
+        torch.cuda.synchronize()
+        torch.cuda._sleep(100_000_000)    # >= 40 ms of GPU time: the whole step is enqueued behind it
+        rt.set_observer(obs)
+        out = step()
+        rt.set_observer(None)
+    return obs.summary(), out
+
+
 def time_steps(run, steps, world=1):
     """Time EXACTLY ``steps`` calls of ``run`` between a barrier + device synchronise on both sides
     (wall clock, max over ranks), with a HIP event after every step on the launch stream for the
@@ -286,12 +303,7 @@ def train_main(args):
         run()
     elapsed, med = time_steps(run, args.steps)
     value = args.batch * args.steps / elapsed
-    obs = rt.LaunchObserver()
-    rt.set_observer(obs)
-    for _ in range(max(1, args.profile_steps)):
-        step()
-    rt.set_observer(None)
-    summ = obs.summary()
+    summ, _ = profile_pass(step, args.profile_steps)
     nprof = max(1, args.profile_steps)
     kernels = {k: {"launches_per_step": v["launches"] / nprof, "ms_per_step": v["ms"] / nprof,
                    "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
@@ -408,12 +420,7 @@ def fgan128train_main(args):
         run()
     elapsed, med = time_steps(run, args.steps)
     value = B * args.steps / elapsed
-    obs = rt.LaunchObserver()
-    rt.set_observer(obs)
-    for _ in range(max(1, args.profile_steps)):
-        step()
-    rt.set_observer(None)
-    summ = obs.summary()
+    summ, _ = profile_pass(step, args.profile_steps)
     nprof = max(1, args.profile_steps)
     kernels = {k: {"launches_per_step": v["launches"] / nprof, "ms_per_step": v["ms"] / nprof,
                    "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
@@ -549,12 +556,7 @@ def block_main(args):
         run()
     elapsed, med = time_steps(run, args.steps)
     value = B * args.steps / elapsed
-    obs = rt.LaunchObserver()
-    rt.set_observer(obs)
-    for _ in range(max(1, args.profile_steps)):
-        step()
-    rt.set_observer(None)
-    summ = obs.summary()
+    summ, _ = profile_pass(step, args.profile_steps)
     nprof = max(1, args.profile_steps)
     kernels = {k: {"launches_per_step": v["launches"] / nprof, "ms_per_step": v["ms"] / nprof,
                    "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}
@@ -754,12 +756,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
 
     # ---- live per-kernel roofline: one instrumented eager pass (HIP events on the launch stream)
-    obs = rt.LaunchObserver()
-    rt.set_observer(obs)
-    for _ in range(max(1, args.profile_steps)):
-        out = step()
-    rt.set_observer(None)
-    summ = obs.summary()
+    summ, out = profile_pass(step, args.profile_steps)
     kernels = {k: {"launches_per_step": v["launches"] / max(1, args.profile_steps),
                    "ms_per_step": v["ms"] / max(1, args.profile_steps),
                    "avg_us": 1e3 * v["ms"] / v["launches"]} for k, v in summ.items()}

@@ -8,6 +8,7 @@ Print, debug_print, NoiseInjection (the names layers/__init__.py:2-18 exports fo
 plus the restated callers FFCModel / FFCGenerator / FFCDiscriminator / FGenerator and Discriminator (fgan128).  All compute runs in
 the gfx950 HIP library libffc_amd.so (include/ffc_amd.h); there is no CPU fallback.
 """
+from . import ops  # noqa: F401  (registers the torch.ops.ffc.* custom ops)
 from .config import Config
 from .ffc import (FFC, FFC_BN_ACT, SNFFC, FFCTranspose, FourierUnitSN, SELayer, SNFFCTranspose, SpectralTransform,
                   set_mix_precision, spectral_norm_ffc)

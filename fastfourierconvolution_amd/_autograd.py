@@ -1,21 +1,24 @@
-"""Training path: custom-op autograd for the FFC operator surface (BASELINE config 3,
-FFC-DCGAN generator + discriminator forward + backward).
+"""Training path: the implementations behind the autograd-registered custom ops of ops.py for the
+FFC operator surface (BASELINE config 3, FFC-DCGAN generator + discriminator forward + backward),
+and the module-facing helpers that compose those ops.
 
 The reference differentiates through ATen.  Here every op the reference's forward is made of
-is one ``torch.autograd.Function`` whose forward AND backward launch the HIP kernels of
-``libffc_amd.so`` (no torch compute on the path, no CPU fallback):
+is one ``torch.ops.ffc.*`` custom op whose forward AND backward (another ffc op, wired by
+``register_autograd``) launch the HIP kernels of ``libffc_amd.so`` (no torch compute on the path,
+no CPU fallback):
 
-  reference op (file:line)                                  Function        backward kernels
-  FFC / FFCTranspose local convs + ST conv2, summed per     _ConvLayerFn    act_bwd; adjoint conv/convT
-    output branch (ffc.py:89-97, ffc_transpose.py:96-106,                   on ffc_conv_forward /
-    spectral_transform.py:108), FU conv_layer (fourier_unity               ffc_convp_forward (same weight,
-    .py:45), ST conv1 (:89)                                                other layout); ffc_conv_wgrad
-  BatchNorm2d (+ activation): bn_l/bn_g (ffc_bn_act.py:       _BNActFn        ffc_bn_bwd
+  reference op (file:line)                                  custom op          backward op / kernels
+  FFC / FFCTranspose local convs + ST conv2, summed per     ffc::conv_layer    ffc::conv_layer_backward:
+    output branch (ffc.py:89-97, ffc_transpose.py:96-106,                      act_bwd; adjoint conv/convT on
+    spectral_transform.py:108), FU conv_layer (fourier_unity                  ffc_conv_forward / convp (same
+    .py:45), ST conv1 (:89), nn.Linear                                        weight, other layout); wgrad
+  BatchNorm2d (+ activation): bn_l/bn_g (ffc_bn_act.py:       ffc::bn_act        ffc::bn_act_backward (ffc_bn_bwd)
     73-81), ST bn1+act1 (:89), FU bn+relu (:46-49)
-  SELayer (spectral_transform.py:23-28, :87)                 _SEFn           ffc_se_bwd + ffc_conv_wgrad
-  AvgPool2d(2) / Upsample(x2) downsample (:44-47, :77)       _Pool2Fn/_Up2Fn ffc_up2 / ffc_pool2
-  rfftn + Re/Im interleave (fourier_unity.py:38-42)          _RFFT2Fn        ffc_irfft2_planes (x 0.5)
-  de-interleave + irfftn (+ x residual) (:51-56, ST :108)     _IRFFT2Fn       ffc_rfft2_planes (x 2)
+  SELayer (spectral_transform.py:23-28, :87)                 ffc::se_scale      ffc::se_scale_backward
+  AvgPool2d(2) / Upsample(x2) downsample (:44-47, :77)       ffc::pool2/up2     each other (adjoints)
+  rfftn + Re/Im interleave (fourier_unity.py:38-42)          ffc::rfft2         ffc::irfft2 (mirrored x 0.5)
+  de-interleave + irfftn (+ x residual) (:51-56, ST :108)     ffc::irfft2        ffc::rfft2 (mirrored x 2)
+  NoiseInjection (noise_injection.py:25-32)                  ffc::noise_inject  ffc::noise_wgrad
 
 FFT adjoints (verified in fp64): d/dX of irfftn(ortho) is rfftn(ortho) with the
 mirrored bins doubled; d/dx of rfftn(ortho) is irfftn(ortho) with the mirrored bins halved.
@@ -23,6 +26,9 @@ The modules switch to this path when autograd is recording and an input or param
 gradient; under ``torch.no_grad()`` the fused inference kernels run.
 """
 from __future__ import annotations
+
+import functools
+import json
 
 import torch
 import torch.nn as nn
@@ -153,8 +159,7 @@ def conv_forward(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0
                                          ptr(out), act[0], float(act[1]), stream), "ffc_conv_full_smallm")
         return out
     C0, C1 = segs[0].C, (segs[1].C if x1 is not None else 0)
-    pkey = ("ctpack", key, weights[0][0].data_ptr(), weights[0][0]._version,
-            None if w1 is None else (w1.data_ptr(), w1._version))
+    pkey = ("ctpack", key, rt.weight_key(weights[0][0]), rt.weight_key(w1))
     wp = cache.get(pkey)
     if wp is None:
         for old in [k for k in cache if k[:2] == ("ctpack", key)]:
@@ -214,350 +219,354 @@ def channel_sum(g):
     return mom[:, 1].float()
 
 
-class ConvLayerSpec:
-    """outputs j = act_j(sum of the edges (j, i, seg, layout) applied to inputs i)"""
+# --------------------------------------------------------------------------- conv layer (ffc::conv_layer)
+# spec (JSON): {"outs": [[M, act, param], ...], "edges": [[j, i, kind, k, s, p, d, op, layout, bias], ...]}:
+# output j = act_j(sum over its edges of conv(kind, k, s, p, d, op)(xs[i]) with ws[e] (+ bs[bias])).
+# Shapes come from the tensors, so one spec serves every batch size.
+_CL_CACHE = {}   # plans / packed weights of every conv_layer op, keyed by (spec, shapes)
 
-    def __init__(self, cache, B, outs, edges, n_in):
-        self.cache, self.B, self.outs, self.edges, self.n_in = cache, B, outs, edges, n_in
+
+@functools.lru_cache(maxsize=4096)
+def parse_conv_spec(spec: str):
+    d = json.loads(spec)
+    return [tuple(o) for o in d["outs"]], [tuple(e) for e in d["edges"]]
 
 
-class _ConvLayerFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, spec: ConvLayerSpec, *args):
-        n_in, ne = spec.n_in, len(spec.edges)
-        xs = [a.contiguous() if a is not None else None for a in args[:n_in]]
-        ws = [w.detach().contiguous() for w in args[n_in:n_in + ne]]
-        bs = [b.detach().contiguous() if b is not None else None for b in args[n_in + ne:n_in + 2 * ne]]
-        outs, saved_t = [], []
-        for j, (M, act, param) in enumerate(spec.outs):
-            es = [(e, spec.edges[e]) for e in range(ne) if spec.edges[e][0] == j]
-            segs = tuple(ed[2] for _, ed in es)
-            wts = [(ws[e], ed[3], ed[2].k, ed[2].k, bs[e]) for e, ed in es]
-            fused = act if act != 5 else 0
-            y = conv_forward(spec.cache, ("fwd", j, spec.B, segs, tuple(ed[3] for _, ed in es)), spec.B, M, segs, wts,
-                             [xs[ed[1]] for _, ed in es], act=(fused, param))
-            if act == 5:
-                pre = y
-                y = _act_out(pre, act, param, _stream(pre))
-                saved_t.append(pre)
-            else:
-                saved_t.append(y)
-            if RECORD is not None and act in (1, 2):   # ReLU / LeakyReLU kinks (fgan128 Discriminator)
-                RECORD.append(y.detach())
-            outs.append(y)
-        ctx.spec = spec
-        ctx.save_for_backward(*[x if x is not None else torch.empty(0) for x in xs], *ws, *saved_t)
-        ctx.has_bias = [b is not None for b in bs]
-        return tuple(outs)
+def conv_spec(outs, edges) -> str:
+    """outs: [(M, act, param)]; edges: [(j, i, Seg, layout, bias index or -1)] -> spec string"""
+    return json.dumps({"outs": [[int(M), int(a), float(p)] for M, a, p in outs],
+                       "edges": [[j, i, sg.kind, sg.k, sg.s, sg.p, sg.d, sg.op, lay, b] for j, i, sg, lay, b in edges]},
+                      separators=(",", ":"))
 
-    @staticmethod
-    def backward(ctx, *gouts):
-        spec = ctx.spec
-        n_in, ne, no = spec.n_in, len(spec.edges), len(spec.outs)
-        saved = ctx.saved_tensors
-        xs, ws, ts = saved[:n_in], saved[n_in:n_in + ne], saved[n_in + ne:]
-        gs = []
-        for j, (M, act, param) in enumerate(spec.outs):
-            g = gouts[j]
-            gs.append(None if g is None else act_backward(ts[j], g.contiguous(), act, param))
-        grads = [None] * (n_in + 2 * ne)
-        for i in range(n_in):
-            if not ctx.needs_input_grad[1 + i]:
-                continue
-            es = [(e, spec.edges[e]) for e in range(ne) if spec.edges[e][1] == i and gs[spec.edges[e][0]] is not None]
-            if not es:
-                continue
-            x = xs[i]
-            B, C = x.shape[:2]
-            adj = []
-            for e, (j, _, sg, lay) in es:
-                g = gs[j]
-                adj.append((e, adjoint_seg(sg, g.shape[1], g.shape[2], g.shape[3]), lay, g))
-            # one launch when the adjoint segments can share a job, else chained through the addend
-            groups = [adj]
-            try:
-                _plan.plan_job(B, C, tuple(a[1] for a in adj))
-            except ValueError:
-                groups = [[a] for a in adj]
-            dx = None
-            for grp in groups:
-                segs = tuple(a[1] for a in grp)
-                wts = [(ws[a[0]], 1 - a[2], a[1].k, a[1].k, None) for a in grp]
-                key = ("adj", i, tuple(a[0] for a in grp), spec.B, segs)
-                dx = conv_forward(spec.cache, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
-                                  addend=dx)
-            grads[i] = dx
-        for e, (j, i, sg, lay) in enumerate(spec.edges):
-            g = gs[j]
+
+def _edge_seg(e, x) -> _plan.Seg:
+    _, _, kind, k, s, p, d, op, _, _ = e
+    if kind == "pw":
+        return _plan.Seg("pw", x.shape[1], x.shape[2], x.shape[3])
+    return _plan.Seg(kind, x.shape[1], x.shape[2], x.shape[3], k, s, p, d, op)
+
+
+def conv_layer_out_shape(e, x, M):
+    """output shape of edge e (spec tuple) applied to x with M output channels (works on SymInts)"""
+    _, _, kind, k, s, p, d, op, _, _ = e
+    B, _, H, W = x.shape
+    if kind == "conv":
+        return (B, M, _plan.conv_out(H, k, s, p, d), _plan.conv_out(W, k, s, p, d))
+    if kind == "convT":
+        return (B, M, _plan.convT_out(H, k, s, p, d, op), _plan.convT_out(W, k, s, p, d, op))
+    return (B, M, H, W)
+
+
+def conv_layer_impl(xs, ws, bs, spec):
+    """ffc::conv_layer: -> outputs, then the pre-activation of every GELU output (the backward's input)"""
+    outs_s, edges = parse_conv_spec(spec)
+    rt.note_tensors(list(ws) + list(bs))
+    xs = [rt.require(x, "conv_layer input") for x in xs]
+    ws = [rt.require(w, "conv_layer weight") for w in ws]
+    bs = [rt.require(b, "conv_layer bias") for b in bs]
+    B = xs[0].shape[0]
+    segs = [_edge_seg(e, xs[e[1]]) for e in edges]
+    outs, pres = [], []
+    for j, (M, act, param) in enumerate(outs_s):
+        es = [e for e in range(len(edges)) if edges[e][0] == j]
+        sgs = tuple(segs[e] for e in es)
+        wts = [(ws[e], edges[e][8], edges[e][3], edges[e][3], bs[edges[e][9]] if edges[e][9] >= 0 else None)
+               for e in es]
+        fused = act if act != 5 else 0
+        y = conv_forward(_CL_CACHE, ("fwd", spec, j, B, sgs), B, M, sgs, wts, [xs[edges[e][1]] for e in es],
+                         act=(fused, param))
+        if act == 5:
+            pres.append(y)
+            y = _act_out(y, act, param, _stream(y))
+        if RECORD is not None and act in (1, 2):   # ReLU / LeakyReLU kinks (fgan128 Discriminator)
+            RECORD.append(y.detach())
+        outs.append(y)
+    return outs + pres
+
+
+def conv_layer_backward_impl(xs, ws, ts, gouts, needs, spec):
+    """ffc::conv_layer_backward: ts[j] = output j (its pre-activation for GELU); needs: per x, w, b.
+    -> [dx per x, dW per w, db per b] (empty tensors where not needed)"""
+    outs_s, edges = parse_conv_spec(spec)
+    n_in, ne = len(xs), len(ws)
+    nb = sum(1 for e in edges if e[9] >= 0)
+    gs = []
+    for j, (M, act, param) in enumerate(outs_s):
+        g = gouts[j]
+        gs.append(None if g is None else act_backward(ts[j], g.contiguous(), act, param))
+    B = xs[0].shape[0]
+    grads = [xs[0].new_empty(0) for _ in range(n_in + ne + nb)]   # distinct: op outputs may not alias
+    for i in range(n_in):
+        if not needs[i]:
+            continue
+        es = [(e, edges[e]) for e in range(ne) if edges[e][1] == i and gs[edges[e][0]] is not None]
+        x = xs[i]
+        if not es:
+            grads[i] = torch.zeros_like(x)
+            continue
+        C = x.shape[1]
+        adj = []
+        for e, ed in es:
+            g = gs[ed[0]]
+            adj.append((e, adjoint_seg(_edge_seg(ed, x), g.shape[1], g.shape[2], g.shape[3]), ed[8], g))
+        # one launch when the adjoint segments can share a job, else chained through the addend
+        groups = [adj]
+        try:
+            _plan.plan_job(B, C, tuple(a[1] for a in adj))
+        except ValueError:
+            groups = [[a] for a in adj]
+        dx = None
+        for grp in groups:
+            segs = tuple(a[1] for a in grp)
+            wts = [(ws[a[0]].contiguous(), 1 - a[2], a[1].k, a[1].k, None) for a in grp]
+            key = ("adj", spec, i, tuple(a[0] for a in grp), B, segs)
+            dx = conv_forward(_CL_CACHE, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
+                              addend=dx)
+        grads[i] = dx
+    for e, ed in enumerate(edges):
+        j, i, kind, k, s, p, d = ed[:7]
+        g = gs[j]
+        if needs[n_in + e]:
+            w, x = ws[e], xs[i].contiguous()
             if g is None:
-                continue
-            if ctx.needs_input_grad[1 + n_in + e]:
-                w = ws[e]
-                x = xs[i]
-                if sg.kind == "convT":
-                    grads[n_in + e] = conv_wgrad(x, g, sg.k, sg.s, sg.p, sg.d, tuple(w.shape))
-                else:
-                    grads[n_in + e] = conv_wgrad(g, x, sg.k, sg.s, sg.p, sg.d, tuple(w.shape))
-            if ctx.has_bias[e] and ctx.needs_input_grad[1 + n_in + ne + e]:
-                grads[n_in + ne + e] = channel_sum(g)
-        return (None, *grads)
+                grads[n_in + e] = torch.zeros_like(w)
+            elif kind == "convT":
+                grads[n_in + e] = conv_wgrad(x, g, k, s, p, d, tuple(w.shape))
+            else:
+                grads[n_in + e] = conv_wgrad(g, x, k, s, p, d, tuple(w.shape))
+        if ed[9] >= 0 and needs[n_in + ne + ed[9]]:
+            grads[n_in + ne + ed[9]] = channel_sum(g) if g is not None else xs[0].new_zeros(outs_s[j][0])
+    return grads
 
 
-def conv_layer(owner_cache, B, outs, edges, inputs):
-    """apply _ConvLayerFn.  edges: (out j, input i, Seg, module); modules' weight/bias are the params"""
-    spec_edges = [(j, i, sg, 1 if isinstance(m, nn.ConvTranspose2d) else 0) for j, i, sg, m in edges]
-    key = ("spec", B, tuple(outs), tuple((j, i, sg, lay) for j, i, sg, lay in spec_edges))
-    spec = owner_cache.get(key)
-    if spec is None:
-        spec = owner_cache[key] = ConvLayerSpec(owner_cache, B, list(outs), spec_edges, len(inputs))
-    for _, _, _, m in edges:
+def conv_layer(B, outs, edges, inputs):
+    """the ffc::conv_layer op over modules: edges (out j, input i, Seg, module) whose weight / bias
+    are the parameters (spectral norm refreshed first, as the module call would)"""
+    spec_edges, ws, bs = [], [], []
+    for j, i, sg, m in edges:
         rt.sn_refresh_train(m)
-    weights = [m.weight for _, _, _, m in edges]
-    biases = [m.bias for _, _, _, m in edges]
-    return _ConvLayerFn.apply(spec, *inputs, *weights, *biases)
+        b = -1
+        if m.bias is not None:
+            b = len(bs)
+            bs.append(m.bias)
+        spec_edges.append((j, i, sg, 1 if isinstance(m, nn.ConvTranspose2d) else 0, b))
+        ws.append(m.weight)
+    ys = torch.ops.ffc.conv_layer(list(inputs), ws, bs, conv_spec(outs, spec_edges))
+    return ys[:len(outs)]
 
 
 # --------------------------------------------------------------------------- BatchNorm2d + activation
-class _BNActFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, bn, act, param, x, gamma, beta):
-        x = x.contiguous()
-        B, C = x.shape[:2]
-        HW = x[0, 0].numel()
-        use_batch, update = rt.bn_mode(bn)
-        if bn.num_features != C:
-            raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
-        grp = rt._sync_group() if use_batch else None   # SyncBN: global-batch statistics (SURVEY §8f)
-        L = rt.lib()
-        dev, stream = x.device, _stream(x)
-        scale = torch.empty(C, device=dev, dtype=torch.float32)
-        shift = torch.empty(C, device=dev, dtype=torch.float32)
-        momentum = -1.0 if bn.momentum is None else float(bn.momentum)
-        g = gamma.detach() if gamma is not None else None
-        b = beta.detach() if beta is not None else None
-        rm, rv = bn.running_mean, bn.running_var
-        nbt = bn.num_batches_tracked
-        moments = None
-        rstats = (None, None)
-        if use_batch:
-            S = L.ffc_reduce_splits(B, C, HW)
-            ws = torch.empty(S * C * 2, device=dev, dtype=torch.float64)
-            moments = torch.empty((C, 3), device=dev, dtype=torch.float64)
-            with rt.observe("bn_moments", bytes=4.0 * x.numel()):
-                check(L.ffc_channel_moments(ptr(x), B, C, HW, ptr(ws), S, ptr(moments), stream), "ffc_channel_moments")
-            if grp is not None:
-                from .distributed import merge_moments
-                merge_moments(moments, group=grp)
-            check(L.ffc_bn_finalize(ptr(moments), C, ptr(g), ptr(b), ptr(rm), ptr(rv), ptr(nbt), 1, int(update),
-                                    momentum, float(bn.eps), 1.0, ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
-        else:
-            rstats = (rm.detach().clone(), rv.detach().clone())
-            check(L.ffc_bn_finalize(None, C, ptr(g), ptr(b), ptr(rm), ptr(rv), ptr(nbt), 0, 0, momentum,
-                                    float(bn.eps), 1.0, ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
-        y = torch.empty_like(x)
-        with rt.observe("bn_act", bytes=8.0 * x.numel()):
-            check(L.ffc_bn_act_apply(ptr(x), ptr(y), B, C, HW, ptr(scale), ptr(shift), act, float(param), stream),
-                  "ffc_bn_act_apply")
-        ctx.act, ctx.param, ctx.eps = act, param, float(bn.eps)
-        ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
-        ctx.save_for_backward(x, scale, shift, moments if moments is not None else torch.empty(0),
-                              rstats[0] if rstats[0] is not None else torch.empty(0),
-                              rstats[1] if rstats[1] is not None else torch.empty(0),
-                              g if g is not None else torch.empty(0))
-        ctx.use_batch = use_batch
-        ctx.grp = grp
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, scale, shift, moments, rmean, rvar, gamma = ctx.saved_tensors
-        dy = dy.contiguous()
-        B, C = x.shape[:2]
-        HW = x[0, 0].numel()
-        L = rt.lib()
+def bn_act_impl(x, gamma, beta, running_mean, running_var, use_batch, eps, act, param):
+    """ffc::bn_act: y = act(BN(x)) with nn.BatchNorm2d's normalisation (batch statistics when
+    use_batch, else the running ones).  -> [y, scale, shift, stats]: stats = the fp64 batch moments
+    [C][3] {n, sum x, sum x^2} (all-reduced under SyncBN) with batch statistics, the running
+    (mean, var) [2][C] otherwise -- the backward's input and ffc::bn_update_running's"""
+    x = rt.require(x, "x")
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    n_feat = running_mean.numel() if running_mean is not None else (gamma.numel() if gamma is not None else C)
+    if n_feat != C:
+        raise RuntimeError(f"running_mean should contain {C} elements not {n_feat}")
+    grp = rt._sync_group() if use_batch else None   # SyncBN: global-batch statistics (SURVEY §8f)
+    L = rt.lib()
+    dev, stream = x.device, _stream(x)
+    scale = torch.empty(C, device=dev, dtype=torch.float32)
+    shift = torch.empty(C, device=dev, dtype=torch.float32)
+    if use_batch:
         S = L.ffc_reduce_splits(B, C, HW)
-        ws = torch.empty(S * C * 2, device=x.device, dtype=torch.float64)
-        coef = torch.empty(C * 3, device=x.device, dtype=torch.float32)
-        dgamma = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.has_gamma else None
-        dbeta = torch.empty(C, device=x.device, dtype=torch.float32) if ctx.has_beta else None
-        dx = torch.empty_like(x) if ctx.needs_input_grad[3] else None
-        if ctx.grp is not None:
-            # torch.nn.SyncBatchNorm backward: dx from the all-reduced {sum g, sum g*x}, this rank's
-            # own sums for dgamma / dbeta (the caller's data-parallel wrapper reduces parameter grads)
-            import torch.distributed as dist
-            stream = _stream(x)
-            sums = torch.empty((C, 2), device=x.device, dtype=torch.float64)
-            with rt.observe("bn_bwd", bytes=8.0 * x.numel()):
-                check(L.ffc_bn_bwd_sums(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), ctx.act, float(ctx.param),
-                                        ptr(ws), S, ptr(sums), stream), "ffc_bn_bwd_sums")
-            gsums = sums.clone()
-            dist.all_reduce(gsums, group=ctx.grp)
-            g = ptr(gamma) if ctx.has_gamma else None
-            check(L.ffc_bn_bwd_coeff(ptr(sums), C, ptr(moments), ctx.eps, g, ptr(coef), ptr(dgamma), ptr(dbeta),
-                                     stream), "ffc_bn_bwd_coeff")
-            check(L.ffc_bn_bwd_coeff(ptr(gsums), C, ptr(moments), ctx.eps, g, ptr(coef), None, None, stream),
-                  "ffc_bn_bwd_coeff")
-            if dx is not None:
-                with rt.observe("bn_bwd", bytes=12.0 * x.numel()):
-                    check(L.ffc_bn_bwd_apply(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), ctx.act,
-                                             float(ctx.param), ptr(coef), ptr(dx), stream), "ffc_bn_bwd_apply")
-            return None, None, None, dx, dgamma, dbeta
+        ws = torch.empty(S * C * 2, device=dev, dtype=torch.float64)
+        stats = torch.empty((C, 3), device=dev, dtype=torch.float64)
+        with rt.observe("bn_moments", bytes=4.0 * x.numel()):
+            check(L.ffc_channel_moments(ptr(x), B, C, HW, ptr(ws), S, ptr(stats), stream), "ffc_channel_moments")
+        if grp is not None:
+            from .distributed import merge_moments
+            merge_moments(stats, group=grp)
+        check(L.ffc_bn_finalize(ptr(stats), C, ptr(gamma), ptr(beta), None, None, None, 1, 0, 0.1, float(eps), 1.0,
+                                ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
+    else:
+        stats = torch.stack((running_mean.detach(), running_var.detach()))
+        check(L.ffc_bn_finalize(None, C, ptr(gamma), ptr(beta), ptr(stats[0]), ptr(stats[1]), None, 0, 0, 0.1,
+                                float(eps), 1.0, ptr(scale), ptr(shift), stream), "ffc_bn_finalize")
+    y = torch.empty_like(x)
+    with rt.observe("bn_act", bytes=8.0 * x.numel()):
+        check(L.ffc_bn_act_apply(ptr(x), ptr(y), B, C, HW, ptr(scale), ptr(shift), act, float(param), stream),
+              "ffc_bn_act_apply")
+    return [y, scale, shift, stats]
+
+
+def bn_update_running_impl(running_mean, running_var, num_batches_tracked, stats, momentum, count_mult):
+    """ffc::bn_update_running: running stats <- batch moments (unbiased variance), nn.BatchNorm2d's rule"""
+    C = running_mean.numel()
+    scratch = torch.empty(2 * C, device=running_mean.device, dtype=torch.float32)
+    check(rt.lib().ffc_bn_finalize(ptr(stats), C, None, None, ptr(running_mean), ptr(running_var),
+                                   ptr(num_batches_tracked), 1, 1, float(momentum), 1e-5, float(count_mult),
+                                   ptr(scratch), ptr(scratch[C:]), _stream(running_mean)), "ffc_bn_finalize")
+
+
+def bn_act_backward_impl(x, dy, scale, shift, stats, gamma, use_batch, sync, eps, act, param, need_dx, has_gamma,
+                         has_beta):
+    """ffc::bn_act_backward -> [dx, dgamma, dbeta] (empty tensors where not needed / absent)"""
+    dy = dy.contiguous()
+    B, C = x.shape[:2]
+    HW = x[0, 0].numel()
+    L = rt.lib()
+    S = L.ffc_reduce_splits(B, C, HW)
+    ws = torch.empty(S * C * 2, device=x.device, dtype=torch.float64)
+    coef = torch.empty(C * 3, device=x.device, dtype=torch.float32)
+    dgamma = torch.empty(C, device=x.device, dtype=torch.float32) if has_gamma else None
+    dbeta = torch.empty(C, device=x.device, dtype=torch.float32) if has_beta else None
+    dx = torch.empty_like(x) if need_dx else None
+    stream = _stream(x)
+    grp = rt._sync_group() if sync else None
+    if grp is not None:
+        # torch.nn.SyncBatchNorm backward: dx from the all-reduced {sum g, sum g*x}, this rank's
+        # own sums for dgamma / dbeta (the caller's data-parallel wrapper reduces parameter grads)
+        import torch.distributed as dist
+        sums = torch.empty((C, 2), device=x.device, dtype=torch.float64)
+        with rt.observe("bn_bwd", bytes=8.0 * x.numel()):
+            check(L.ffc_bn_bwd_sums(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), act, float(param),
+                                    ptr(ws), S, ptr(sums), stream), "ffc_bn_bwd_sums")
+        gsums = sums.clone()
+        dist.all_reduce(gsums, group=grp)
+        g = ptr(gamma) if has_gamma else None
+        check(L.ffc_bn_bwd_coeff(ptr(sums), C, ptr(stats), float(eps), g, ptr(coef), ptr(dgamma), ptr(dbeta),
+                                 stream), "ffc_bn_bwd_coeff")
+        check(L.ffc_bn_bwd_coeff(ptr(gsums), C, ptr(stats), float(eps), g, ptr(coef), None, None, stream),
+              "ffc_bn_bwd_coeff")
+        if dx is not None:
+            with rt.observe("bn_bwd", bytes=12.0 * x.numel()):
+                check(L.ffc_bn_bwd_apply(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), act, float(param),
+                                         ptr(coef), ptr(dx), stream), "ffc_bn_bwd_apply")
+    else:
         with rt.observe("bn_bwd", bytes=12.0 * x.numel()):
-            check(L.ffc_bn_bwd(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), ctx.act, float(ctx.param),
-                               ptr(moments) if ctx.use_batch else None,
-                               None if ctx.use_batch else ptr(rmean), None if ctx.use_batch else ptr(rvar),
-                               ctx.eps, ptr(gamma) if ctx.has_gamma else None, ptr(ws), S, ptr(coef), ptr(dgamma),
-                               ptr(dbeta), ptr(dx), _stream(x)), "ffc_bn_bwd")
-        return None, None, None, dx, dgamma, dbeta
+            check(L.ffc_bn_bwd(ptr(x), ptr(dy), B, C, HW, ptr(scale), ptr(shift), act, float(param),
+                               ptr(stats) if use_batch else None,
+                               None if use_batch else ptr(stats[0]), None if use_batch else ptr(stats[1]),
+                               float(eps), ptr(gamma) if has_gamma else None, ptr(ws), S, ptr(coef), ptr(dgamma),
+                               ptr(dbeta), ptr(dx), stream), "ffc_bn_bwd")
+    return [t if t is not None else x.new_empty(0) for t in (dx, dgamma, dbeta)]
 
 
 RECORD = None   # tests: a list collecting every BN + activation output (kink patterns of the path)
 
 
 def bn_act(bn: nn.BatchNorm2d, x, act=(0, 0.0)):
-    y = _BNActFn.apply(bn, act[0], act[1], x, bn.weight, bn.bias)
+    """BatchNorm2d ``bn`` + activation on the ffc::bn_act op (the module's tensors as arguments), then
+    the running-statistics update in training mode (ffc::bn_update_running)"""
+    use_batch, update = rt.bn_mode(bn)
+    y, _, _, stats = torch.ops.ffc.bn_act(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, use_batch,
+                                          float(bn.eps), int(act[0]), float(act[1]))
+    if update:
+        torch.ops.ffc.bn_update_running(bn.running_mean, bn.running_var, bn.num_batches_tracked, stats,
+                                        -1.0 if bn.momentum is None else float(bn.momentum), 1.0)
     if RECORD is not None:
         RECORD.append(y.detach())
     return y
 
 
 # --------------------------------------------------------------------------- SELayer
-class _SEFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w1, w2):
-        x = x.contiguous()
-        B, C, H, W = x.shape
-        hid = w1.shape[0]
-        L = rt.lib()
-        stream = _stream(x)
-        w1d = w1.detach().contiguous() if hid else None
-        w2d = w2.detach().contiguous() if hid else None
-        gate = torch.empty((B, C), device=x.device, dtype=torch.float32)
-        with rt.observe("se_gate", bytes=4.0 * x.numel()):
-            check(L.ffc_se_gate(ptr(x), B, C, H, W, 0, ptr(w1d), ptr(w2d), hid, ptr(gate), stream), "ffc_se_gate")
-        zeros = torch.zeros(B * C, device=x.device, dtype=torch.float32)
-        y = torch.empty_like(x)
-        check(L.ffc_bn_act_apply(ptr(x), ptr(y), 1, B * C, H * W, ptr(gate), ptr(zeros), 0, 0.0, stream),
-              "ffc_bn_act_apply")
-        ctx.hid = hid
-        ctx.w_shapes = (tuple(w1.shape), tuple(w2.shape))
-        ctx.save_for_backward(x, w1d if hid else torch.empty(0), w2d if hid else torch.empty(0))
-        return y
+def se_scale_impl(x, w1, w2):
+    """ffc::se_scale: x * sigmoid(w2 . relu(w1 . mean_HW(x))) (hidden width w1.shape[0] may be 0)"""
+    x = rt.require(x, "x")
+    B, C, H, W = x.shape
+    hid = w1.shape[0]
+    L = rt.lib()
+    stream = _stream(x)
+    w1d = w1.contiguous() if hid else None
+    w2d = w2.contiguous() if hid else None
+    gate = torch.empty((B, C), device=x.device, dtype=torch.float32)
+    with rt.observe("se_gate", bytes=4.0 * x.numel()):
+        check(L.ffc_se_gate(ptr(x), B, C, H, W, 0, ptr(w1d), ptr(w2d), hid, ptr(gate), stream), "ffc_se_gate")
+    zeros = torch.zeros(B * C, device=x.device, dtype=torch.float32)
+    y = torch.empty_like(x)
+    check(L.ffc_bn_act_apply(ptr(x), ptr(y), 1, B * C, H * W, ptr(gate), ptr(zeros), 0, 0.0, stream),
+          "ffc_bn_act_apply")
+    return y
 
-    @staticmethod
-    def backward(ctx, dy):
-        x, w1, w2 = ctx.saved_tensors
-        dy = dy.contiguous()
-        B, C, H, W = x.shape
-        hid = ctx.hid
-        dev = x.device
-        dx = torch.empty_like(x)
-        vec = (lambda n: torch.empty((B, n, 1, 1), device=dev, dtype=torch.float32)) if hid else (lambda n: None)
-        dpre2, hact, dpre1, mean = vec(C), vec(hid), vec(hid), vec(C)
-        ws = torch.empty(4 * B * C, device=dev, dtype=torch.float32)
-        with rt.observe("se_bwd", bytes=(16.0 if hid else 8.0) * x.numel()):
-            check(rt.lib().ffc_se_bwd(ptr(x), ptr(dy), B, C, H, W, ptr(w1) if hid else None, ptr(w2) if hid else None,
-                                      hid, ptr(dx), ptr(dpre2), ptr(hact), ptr(dpre1), ptr(mean), ptr(ws), _stream(x)),
-                  "ffc_se_bwd")
-        dw1 = dw2 = None
-        if not hid:   # Linear(C, 0) / Linear(0, C): empty weights get empty gradients
-            dw1 = torch.zeros(ctx.w_shapes[0], device=dev) if ctx.needs_input_grad[1] else None
-            dw2 = torch.zeros(ctx.w_shapes[1], device=dev) if ctx.needs_input_grad[2] else None
-        if hid and ctx.needs_input_grad[1]:
-            dw1 = conv_wgrad(dpre1, mean, 1, 1, 0, 1, (hid, C))      # fc.0: (hid, C)
-        if hid and ctx.needs_input_grad[2]:
-            dw2 = conv_wgrad(dpre2, hact, 1, 1, 0, 1, (C, hid))      # fc.2: (C, hid)
-        return dx, dw1, dw2
+
+def se_scale_backward_impl(x, dy, w1, w2):
+    """ffc::se_scale_backward -> [dx, dw1, dw2]"""
+    dy = dy.contiguous()
+    B, C, H, W = x.shape
+    hid = w1.shape[0]
+    dev = x.device
+    dx = torch.empty_like(x)
+    if not hid:   # Linear(C, 0) / Linear(0, C): empty weights get empty gradients; the gate is 0.5
+        check(rt.lib().ffc_se_bwd(ptr(x), ptr(dy), B, C, H, W, None, None, 0, ptr(dx), None, None, None, None,
+                                  ptr(torch.empty(4 * B * C, device=dev)), _stream(x)), "ffc_se_bwd")
+        return [dx, torch.zeros_like(w1), torch.zeros_like(w2)]
+    vec = lambda n: torch.empty((B, n, 1, 1), device=dev, dtype=torch.float32)  # noqa: E731
+    dpre2, hact, dpre1, mean = vec(C), vec(hid), vec(hid), vec(C)
+    ws = torch.empty(4 * B * C, device=dev, dtype=torch.float32)
+    w1c, w2c = w1.contiguous(), w2.contiguous()
+    with rt.observe("se_bwd", bytes=16.0 * x.numel()):
+        check(rt.lib().ffc_se_bwd(ptr(x), ptr(dy), B, C, H, W, ptr(w1c), ptr(w2c), hid, ptr(dx), ptr(dpre2), ptr(hact),
+                                  ptr(dpre1), ptr(mean), ptr(ws), _stream(x)), "ffc_se_bwd")
+    dw1 = conv_wgrad(dpre1, mean, 1, 1, 0, 1, (hid, C))      # fc.0: (hid, C)
+    dw2 = conv_wgrad(dpre2, hact, 1, 1, 0, 1, (C, hid))      # fc.2: (C, hid)
+    return [dx, dw1, dw2]
 
 
 def se_layer(se, x):
     if se.fc[0].bias is not None or se.fc[2].bias is not None:
         raise NotImplementedError("SELayer with bias")
-    return _SEFn.apply(x, se.fc[0].weight, se.fc[2].weight)
+    return torch.ops.ffc.se_scale(x, se.fc[0].weight, se.fc[2].weight)
 
 
 # --------------------------------------------------------------------------- pool / upsample
-def _pool2(x, scale):
+def pool2_impl(x, scale):
+    """ffc::pool2: scale * (sum of each 2x2 block) -- AvgPool2d(2, 2) at scale 0.25 (spectral_transform.py:46-47)"""
+    x = rt.require(x, "x")
     B, C, H, W = x.shape
+    if H % 2 or W % 2:
+        raise NotImplementedError("AvgPool2d(2) downsample of an odd-sized input")
     y = torch.empty((B, C, H // 2, W // 2), device=x.device, dtype=torch.float32)
     check(rt.lib().ffc_pool2(ptr(x), B * C, H, W, float(scale), ptr(y), _stream(x)), "ffc_pool2")
     return y
 
 
-def _up2(x, scale):
+def up2_impl(x, scale):
+    """ffc::up2: scale * nearest x2 -- Upsample(scale_factor=2, mode='nearest') at scale 1 (:44-45)"""
+    x = rt.require(x, "x")
     B, C, h, w = x.shape
     y = torch.empty((B, C, 2 * h, 2 * w), device=x.device, dtype=torch.float32)
     check(rt.lib().ffc_up2(ptr(x), B * C, h, w, float(scale), ptr(y), _stream(x)), "ffc_up2")
     return y
 
 
-class _Pool2Fn(torch.autograd.Function):
-    """AvgPool2d(2, 2) (spectral_transform.py:46-47)"""
-
-    @staticmethod
-    def forward(ctx, x):
-        if x.shape[2] % 2 or x.shape[3] % 2:
-            raise NotImplementedError("AvgPool2d(2) downsample of an odd-sized input")
-        return _pool2(x.contiguous(), 0.25)
-
-    @staticmethod
-    def backward(ctx, dy):
-        return _up2(dy.contiguous(), 0.25)
-
-
-class _Up2Fn(torch.autograd.Function):
-    """Upsample(scale_factor=2, mode='nearest') (spectral_transform.py:44-45)"""
-
-    @staticmethod
-    def forward(ctx, x):
-        return _up2(x.contiguous(), 1.0)
-
-    @staticmethod
-    def backward(ctx, dy):
-        return _pool2(dy.contiguous(), 1.0)
-
-
 # --------------------------------------------------------------------------- NoiseInjection, Linear
-class _NoiseFn(torch.autograd.Function):
-    """NoiseInjection.forward (layers/noise_injection.py:25-32): x + weight * noise; backward
-    dx = g, dweight[c] = sum g[:, c] * noise (ffc_noise_wgrad)"""
+def noise_inject_impl(x, weight, noise):
+    """ffc::noise_inject: x + weight[c] * noise[b] (layers/noise_injection.py:25-32)"""
+    x = rt.require(x, "x")
+    B, C, H, W = x.shape
+    noise = rt.require(noise, "noise")
+    if tuple(noise.shape) != (B, 1, H, W) or (H * W) % 4:
+        raise NotImplementedError("NoiseInjection: noise must be (B, 1, H, W) with H*W % 4 == 0")
+    if weight.numel() != C:
+        raise RuntimeError(f"NoiseInjection has {weight.numel()} channels, tensor has {C}")
+    out = torch.empty_like(x)
+    with rt.observe("noise_inject", bytes=8.0 * x.numel() + 4.0 * noise.numel()):
+        check(rt.lib().ffc_noise_inject(ptr(x), ptr(weight.contiguous()), ptr(noise), ptr(out), B, C, H * W,
+                                        _stream(x)), "ffc_noise_inject")
+    return out
 
-    @staticmethod
-    def forward(ctx, x, weight, noise):
-        B, C, H, W = x.shape
-        x = x.contiguous()
-        out = torch.empty_like(x)
-        with rt.observe("noise_inject", bytes=8.0 * x.numel() + 4.0 * noise.numel()):
-            check(rt.lib().ffc_noise_inject(ptr(x), ptr(weight.detach().contiguous()), ptr(noise), ptr(out), B, C,
-                                            H * W, _stream(x)), "ffc_noise_inject")
-        ctx.save_for_backward(noise)
-        return out
 
-    @staticmethod
-    def backward(ctx, g):
-        (noise,) = ctx.saved_tensors
-        g = g.contiguous()
-        dw = None
-        if ctx.needs_input_grad[1]:
-            B, C, H, W = g.shape
-            dw = torch.empty(C, device=g.device, dtype=torch.float32)
-            check(rt.lib().ffc_noise_wgrad(ptr(g), ptr(noise), B, C, H * W, ptr(dw), _stream(g)), "ffc_noise_wgrad")
-            dw = dw.view(1, C, 1, 1)
-        return (g if ctx.needs_input_grad[0] else None), dw, None
+def noise_wgrad_impl(g, noise):
+    """ffc::noise_wgrad: dweight[c] = sum g[:, c] * noise -> (1, C, 1, 1)"""
+    g = g.contiguous()
+    B, C, H, W = g.shape
+    dw = torch.empty(C, device=g.device, dtype=torch.float32)
+    check(rt.lib().ffc_noise_wgrad(ptr(g), ptr(noise), B, C, H * W, ptr(dw), _stream(g)), "ffc_noise_wgrad")
+    return dw.view(1, C, 1, 1)
 
 
 def noise_inject(mod, x, noise=None):
-    """NoiseInjection ``mod`` applied to x on the training path (noise drawn with normal_() as the
-    reference does when not given)"""
+    """NoiseInjection ``mod`` on the ffc::noise_inject op (noise drawn with normal_() as the reference
+    does when not given)"""
     B, C, H, W = x.shape
     if noise is None:
         noise = x.new_empty(B, 1, H, W).normal_()
-    noise = rt.require(noise, "noise").contiguous()
-    if tuple(noise.shape) != (B, 1, H, W) or (H * W) % 4:
-        raise NotImplementedError("NoiseInjection: noise must be (B, 1, H, W) with H*W % 4 == 0")
-    if mod.weight.numel() != C:
-        raise RuntimeError(f"NoiseInjection has {mod.weight.numel()} channels, tensor has {C}")
-    return _NoiseFn.apply(x, mod.weight, noise)
+    return torch.ops.ffc.noise_inject(x, mod.weight, noise)
 
 
 class _LinearAs1x1:
@@ -570,62 +579,40 @@ class _LinearAs1x1:
         self.out_channels = lin.out_features
 
 
-def linear(owner_cache, lin: nn.Linear, z):
+def linear(lin: nn.Linear, z):
     """nn.Linear forward + backward (fgan128_complete.py:453-455 noise_to_feature, and the spectral-norm
     fc of the fgan128 Discriminator, :540) -> (B, N)"""
     B, K = z.shape
     rt.sn_refresh_train(lin)   # the 1x1 view below must see this call's W / sigma
-    (y,) = conv_layer(owner_cache, B, [(lin.out_features, 0, 0.0)], [(0, 0, _plan.Seg("pw", K, 1, 1), _LinearAs1x1(lin))],
+    (y,) = conv_layer(B, [(lin.out_features, 0, 0.0)], [(0, 0, _plan.Seg("pw", K, 1, 1), _LinearAs1x1(lin))],
                       [z.reshape(B, K, 1, 1)])
     return y.reshape(B, lin.out_features)
 
 
 # --------------------------------------------------------------------------- FFTs
-def _rfft2(x, iscale):
+def rfft2_impl(x, mirror_scale):
+    """ffc::rfft2: interleave(rfftn(x, ortho)) -> (B, 2C, H, W/2+1), mirrored bins x mirror_scale
+    (0.5: the adjoint of irfftn)"""
+    x = rt.require(x, "x")
     B, C, H, W = x.shape
     Z = torch.empty((B, 2 * C, H, W // 2 + 1), device=x.device, dtype=torch.float32)
     with rt.observe("rfft2", bytes=4.0 * x.numel() + 4.0 * Z.numel()):
-        check(rt.lib().ffc_rfft2_planes(ptr(x), B * C, H, W, float(iscale), ptr(Z), _stream(x)), "ffc_rfft2_planes")
+        check(rt.lib().ffc_rfft2_planes(ptr(x), B * C, H, W, float(mirror_scale), ptr(Z), _stream(x)),
+              "ffc_rfft2_planes")
     return Z
 
 
-def _irfft2(Z, H, W, iscale, addend=None):
+def irfft2_impl(Z, H, W, mirror_scale, r):
+    """ffc::irfft2: irfftn(deinterleave(Z), s=(H, W), ortho) [+ r], mirrored bins x mirror_scale
+    (2: the adjoint of rfftn)"""
+    Z = rt.require(Z, "Z")
     B, C2 = Z.shape[:2]
     y = torch.empty((B, C2 // 2, H, W), device=Z.device, dtype=torch.float32)
+    r = rt.require(r, "residual") if r is not None else None
     with rt.observe("irfft2", bytes=4.0 * Z.numel() + 4.0 * y.numel()):
-        check(rt.lib().ffc_irfft2_planes(ptr(Z), B * (C2 // 2), H, W, float(iscale), ptr(addend), ptr(y),
+        check(rt.lib().ffc_irfft2_planes(ptr(Z), B * (C2 // 2), H, W, float(mirror_scale), ptr(r), ptr(y),
                                          _stream(Z)), "ffc_irfft2_planes")
     return y
-
-
-class _RFFT2Fn(torch.autograd.Function):
-    """Z = interleave(rfftn(x, norm='ortho')) (fourier_unity.py:38-42)"""
-
-    @staticmethod
-    def forward(ctx, x):
-        ctx.hw = x.shape[2:]
-        return _rfft2(x.contiguous(), 1.0)
-
-    @staticmethod
-    def backward(ctx, dZ):
-        H, W = ctx.hw
-        return _irfft2(dZ.contiguous(), H, W, 0.5)
-
-
-class _IRFFT2Fn(torch.autograd.Function):
-    """y = irfftn(deinterleave(Z), s=(H, W), norm='ortho') [+ r] (fourier_unity.py:51-56; r: the
-    x + fu(x) residual of spectral_transform.py:108)"""
-
-    @staticmethod
-    def forward(ctx, Z, H, W, r):
-        ctx.has_r = r is not None
-        return _irfft2(Z.contiguous(), H, W, 1.0, r.contiguous() if r is not None else None)
-
-    @staticmethod
-    def backward(ctx, dy):
-        dy = dy.contiguous()
-        dZ = _rfft2(dy, 2.0) if ctx.needs_input_grad[0] else None
-        return dZ, None, None, (dy if ctx.has_r else None)
 
 
 def fourier_unit(fu, x, residual: bool):
@@ -637,12 +624,11 @@ def fourier_unit(fu, x, residual: bool):
                                   "mix is forward-only)")
     if (H > 64 or W > 64) and not (H == W and H in (128,)):
         raise NotImplementedError("training-path Fourier unit: planes up to 64x64, or square 128x128")
-    Z = _RFFT2Fn.apply(x)
-    cache = fu.__dict__.setdefault("_train_cache", {})
+    Z = torch.ops.ffc.rfft2(x, 1.0)
     seg = _plan.Seg("pw", 2 * C, H, W // 2 + 1)
-    (U,) = conv_layer(cache, B, [(2 * C, 0, 0.0)], [(0, 0, seg, fu.conv_layer)], [Z])
+    (U,) = conv_layer(B, [(2 * C, 0, 0.0)], [(0, 0, seg, fu.conv_layer)], [Z])
     R = bn_act(fu.bn, U, (1, 0.0))
-    return _IRFFT2Fn.apply(R, H, W, x if residual else None)
+    return torch.ops.ffc.irfft2(R, H, W, 1.0, x if residual else None)
 
 
 def spectral_v(st, x):
@@ -650,13 +636,12 @@ def spectral_v(st, x):
     if st.groups != 1:
         raise NotImplementedError("grouped SpectralTransform (groups != 1) is not on the hot path")
     if st.stride == 2 and st.upsample:
-        x = _Up2Fn.apply(x)
+        x = torch.ops.ffc.up2(x, 1.0)
     elif st.stride == 2:
-        x = _Pool2Fn.apply(x)
+        x = torch.ops.ffc.pool2(x, 0.25)
     x = se_layer(st.se_block, x)
     B, Cin, H, W = x.shape
-    cache = st.__dict__.setdefault("_train_cache", {})
     c = st.conv1.out_channels
-    (t,) = conv_layer(cache, B, [(c, 0, 0.0)], [(0, 0, _plan.Seg("pw", Cin, H, W), st.conv1)], [x])
+    (t,) = conv_layer(B, [(c, 0, 0.0)], [(0, 0, _plan.Seg("pw", Cin, H, W), st.conv1)], [x])
     s = bn_act(st.bn1, t, (1, 0.0))
     return fourier_unit(st.fu, s, residual=True)

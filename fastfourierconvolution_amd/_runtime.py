@@ -361,6 +361,13 @@ class PendingAct:
             self.noise_w, self.noise = w, noise
         self.shape = raw.shape
 
+    @classmethod
+    def from_tensors(cls, raw, scale, shift, act, param, noise_w=None, noise=None):
+        """a PendingAct from its tensors (the outputs / inputs of the deferred ffc::ffc_bn_act op)"""
+        p = cls(raw, scale, shift, act, param)
+        p.noise_w, p.noise = noise_w, noise
+        return p
+
     def struct(self):
         from ._lib import InTf
         return InTf(ptr(self.scale), ptr(self.shift), self.act, self.param, ptr(self.noise_w), ptr(self.noise))
@@ -384,9 +391,64 @@ def materialize(x):
     return x.materialize() if isinstance(x, PendingAct) else x
 
 
-# --------------------------------------------------------------------------- convolution jobs
+# --------------------------------------------------------------------------- packed-weight keys
+# Packed forms of weights (GEMM A panels, transposed mix / conv1 / Linear weights) are cached by
+# (pointer, version, epoch).  The custom ops (ops.py) are functional: the weights arrive as op
+# arguments, and one op's plan cache serves every module with the same structure.  Pointer +
+# version alone would then hit stale packs when a freed model's weight memory is reused by a new
+# model's weight at the same version count, so each weight tensor OBJECT (the view's base for
+# views) gets an epoch the first time an op sees it; a new object at a recycled address gets a
+# new epoch and is re-packed.
+_EPOCH = {"next": 1, "by_id": {}, "by_ptr": {}}
+_EPOCH_LOCK = __import__("threading").Lock()
+
+
+def note_tensors(ts):
+    """register the weight tensors an op was called with (see weight_key)"""
+    import weakref
+    with _EPOCH_LOCK:
+        by_id, by_ptr = _EPOCH["by_id"], _EPOCH["by_ptr"]
+        for t in ts:
+            if t is None or not isinstance(t, torch.Tensor):
+                continue
+            a = t._base if t._base is not None else t
+            e = by_id.get(id(a))
+            if e is None or e[0]() is not a:
+                k = id(a)
+                e = (weakref.ref(a, lambda _r, k=k: _EPOCH["by_id"].pop(k, None)), _EPOCH["next"])
+                _EPOCH["next"] += 1
+                by_id[k] = e
+            by_ptr[t.data_ptr()] = e[1]
+
+
+def weight_key(t):
+    """cache key of a weight's packed form: (pointer, version, epoch of the tensor object)"""
+    if t is None:
+        return None
+    return t.data_ptr(), t._version, _EPOCH["by_ptr"].get(t.data_ptr(), 0)
+
+
 def _wkey(ts):
-    return tuple((t.data_ptr(), t._version) if t is not None else None for t in ts)
+    return tuple(weight_key(t) for t in ts)
+
+
+class PackCache:
+    """a few packed forms of weights, keyed by weight_key of their sources (FIFO-bounded)"""
+
+    def __init__(self, cap: int = 16):
+        self.cap, self.d = cap, {}
+
+    def get(self, tag, sources, build):
+        key = (tag,) + _wkey(sources)
+        v = self.d.get(key)
+        if v is None:
+            if len(self.d) >= self.cap:
+                self.d.pop(next(iter(self.d)))
+            v = self.d[key] = build()
+        return v
+
+
+# --------------------------------------------------------------------------- convolution jobs
 
 
 def algorithmic_flops(plan) -> float:

@@ -670,10 +670,10 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float* __restrict__ Z
 // ran B workgroups: 1 ms per 128x128 fgan128 layer at B = 64):
 //   sums  one wave per (b, c) plane: ws.mean = mean_HW x, ws.dot = sum_HW dy * x
 //   gate  one workgroup per sample: g, dpre2 = d(W2 h), hact, dpre1 = d(W1 m), dmean = W1^T dpre1 / HW
-//   apply dx = dy * g + dmean (per plane), float4 where HW % 4 == 0
+//   apply dx = dy * g + dmean (per plane), float4 where vec4 (HW % 4 == 0 and x, dout, dx 16-byte aligned)
 // ws: 4 * B * C floats (mean, dot, gate, dmean).
 __global__ __launch_bounds__(256) void se_bwd_sums_kernel(const float* __restrict__ x, const float* __restrict__ dout,
-                                                          int P, int HW, float* __restrict__ ws_mean,
+                                                          int P, int HW, int vec4, float* __restrict__ ws_mean,
                                                           float* __restrict__ ws_dot) {
     const int lane = threadIdx.x & 63;
     const int pl = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(256) void se_bwd_sums_kernel(const float* __restric
     const float* xp = x + (size_t)pl * HW;
     const float* dp = dout + (size_t)pl * HW;
     float s = 0.0f, q = 0.0f;
-    if ((HW & 3) == 0) {
+    if (vec4) {
         const float4* x4 = reinterpret_cast<const float4*>(xp);
         const float4* d4 = reinterpret_cast<const float4*>(dp);
         for (int i = lane; i < HW / 4; i += 64) {
@@ -763,10 +763,10 @@ __global__ __launch_bounds__(256) void se_bwd_gate_kernel(int C, int HW, const f
 }
 
 __global__ __launch_bounds__(256) void se_bwd_apply_kernel(const float* __restrict__ dout, long long n, int HW,
-                                                           const float* __restrict__ gate,
+                                                           int vec4, const float* __restrict__ gate,
                                                            const float* __restrict__ dmean, float* __restrict__ dx) {
     const long long stride = (long long)gridDim.x * blockDim.x;
-    if ((HW & 3) == 0) {
+    if (vec4) {
         const int hw4 = HW / 4;
         const float4* d4 = reinterpret_cast<const float4*>(dout);
         float4* o4 = reinterpret_cast<float4*>(dx);
@@ -1056,14 +1056,18 @@ extern "C" int ffc_se_bwd(const float* x, const float* dout, int B, int C, int H
     float* ws_gate = ws + 2 * (size_t)P;
     float* ws_dmean = ws + 3 * (size_t)P;
     hipStream_t s = (hipStream_t)stream;
+    // float4 planes only where every plane starts 16-byte aligned (an offset pointer takes the scalar loops)
+    const int vec4 = (HW & 3) == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dout) |
+                                        reinterpret_cast<uintptr_t>(dx)) & 15) == 0;
     if (hidden > 0)
-        hipLaunchKernelGGL(se_bwd_sums_kernel, dim3((P + 3) / 4), dim3(256), 0, s, x, dout, P, HW, ws_mean, ws_dot);
+        hipLaunchKernelGGL(se_bwd_sums_kernel, dim3((P + 3) / 4), dim3(256), 0, s, x, dout, P, HW, vec4, ws_mean,
+                           ws_dot);
     hipLaunchKernelGGL(se_bwd_gate_kernel, dim3(B), dim3(256), lds, s, C, HW, w1, w2, hidden, ws_mean, ws_dot,
                        ws_gate, ws_dmean, dpre2, hact, dpre1, mean);
     const long long n = (long long)P * HW;
-    const long long units = (HW & 3) == 0 ? n / 4 : n;
+    const long long units = vec4 ? n / 4 : n;
     const int grid = (int)std::min<long long>((units + 255) / 256, 8192);
-    hipLaunchKernelGGL(se_bwd_apply_kernel, dim3(grid), dim3(256), 0, s, dout, n, HW, ws_gate, ws_dmean, dx);
+    hipLaunchKernelGGL(se_bwd_apply_kernel, dim3(grid), dim3(256), 0, s, dout, n, HW, vec4, ws_gate, ws_dmean, dx);
     return ffc::launch_status("ffc_se_bwd");
 }
 

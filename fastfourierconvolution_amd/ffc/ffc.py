@@ -1,6 +1,9 @@
 """Drop-in ``FFC`` (reference: layers/ffc/ffc.py:10-99) and the shared HIP executor that
 FFCTranspose (ffc_transpose.py) and FFC_BN_ACT (ffc_bn_act.py) also use.
 
+The module forwards go through the custom ops of ops.py (``ffc::ffc_bn_act`` for inference, the
+per-op training ops under autograd); _FFCExec is the executor those ops run.
+
 Each output branch is ONE implicit-GEMM launch (both branches share it):
   out_l = convl2l(x_l) + convg2l(x_g)                      segments: conv, conv
   out_g = convl2g(x_l) + conv2(v),  v = s + fu(s)          segments: conv, 1x1 at output res
@@ -16,11 +19,27 @@ import torch.nn as nn
 from .. import _autograd as ag
 from .. import _plan
 from .. import _runtime as rt
+from .. import ops
 from .spectral_transform import SpectralTransform
 
 
+def layer_call(mod, ffc, x, y, act_l=(0, 0.0), act_g=(0, 0.0), bn_l=None, bn_g=None, noise=None, defer=False):
+    """forward of FFC_BN_ACT / FFC / FFCTranspose ``mod`` whose FFC part is ``ffc``: the training ops
+    when autograd needs them, else the fused ffc::ffc_bn_act op"""
+    if y is not None and ffc.ratio_gout != 0:
+        # the reference passes y into SpectralTransform / FourierUnitSN, whose BatchNorm2d.forward()
+        # takes no label (fourier_unity.py:46-47), or into nn.Identity.forward (one argument)
+        raise TypeError("FFC: the conditional (y) path is not supported (the reference raises in "
+                        "FourierUnitSN, fourier_unity.py:46-47)")
+    x_l, x_g = x if type(x) is tuple else (x, 0)
+    if ag.wants_grad(mod, x_l, x_g):
+        x_l, x_g = rt.materialize(x_l), rt.materialize(x_g)
+        return ffc._run_train(x_l, x_g, None, act_l, act_g, bn_l, bn_g, noise)
+    return ops.layer_forward(mod, x, noise, defer)
+
+
 class _FFCExec:
-    """mixin: fused execution of an FFC / FFCTranspose layer"""
+    """mixin: fused execution of an FFC / FFCTranspose layer (run by the ffc::ffc_bn_act op)"""
 
     def _ffc_cache(self):
         c = self.__dict__.get("_exec_cache")
@@ -199,7 +218,7 @@ class _FFCExec:
             names.append((name, act, bn))
         res = {"l": 0, "g": 0}
         if outs:
-            ys = ag.conv_layer(self._ffc_cache(), B, outs, edges, inputs)
+            ys = ag.conv_layer(B, outs, edges, inputs)
             for (name, act, bn), yv in zip(names, ys):
                 res[name] = ag.bn_act(bn, yv, act) if bn is not None else yv
         for name, (mod, n) in (noise or {}).items():   # fgan128's NoiseInjection after FFC_BN_ACT
@@ -356,7 +375,7 @@ class _FFCExec:
         cache = self._ffc_cache()
         segs2, w2 = [], []
         for sg, (wt, lay, kh, kw, bias) in zip(segs, w):
-            key = ("outer", wt.data_ptr(), wt._version, None if bias is None else (bias.data_ptr(), bias._version))
+            key = ("outer", wt.data_ptr(), rt.weight_key(wt), rt.weight_key(bias))
             hit = cache.get(key)
             if hit is None:
                 for old in [kk for kk in cache if kk[0] == "outer" and kk[1] == wt.data_ptr()]:
@@ -382,8 +401,7 @@ class _FFCExec:
                 groups.append([d])
         for g in groups:
             wts = [d[1] for d in g]
-            key = ("dense",) + tuple((wt[0].data_ptr(), wt[0]._version,
-                                      None if wt[4] is None else (wt[4].data_ptr(), wt[4]._version)) for wt in wts)
+            key = ("dense",) + tuple((wt[0].data_ptr(), rt.weight_key(wt[0]), rt.weight_key(wt[4])) for wt in wts)
             hit = cache.get(key)
             if hit is None:
                 for old in [kk for kk in cache if kk[0] == "dense" and kk[1][0] == key[1][0]]:
@@ -433,8 +451,7 @@ class _FFCExec:
         if kind == "convT":
             # weights packed [C0 + C1][16 taps][4] by a HIP kernel, cached per (pointer, version)
             cache = self._ffc_cache()
-            key = ("ctpack", w[0][0].data_ptr(), w[0][0]._version,
-                   None if w1 is None else (w1.data_ptr(), w1._version))
+            key = ("ctpack", w[0][0].data_ptr(), rt.weight_key(w[0][0]), rt.weight_key(w1))
             wp = cache.get(key)
             if wp is None:
                 for old in [kk for kk in cache if kk[0] == "ctpack" and kk[1] == key[1]]:
@@ -498,6 +515,10 @@ class FFC(_FFCExec, nn.Module):
                  attention: bool = False, num_classes: int = 1):
         super().__init__()
         assert stride == 1 or stride == 2, "Stride should be 1 or 2."
+        self._ffc_ctor = ["FFC", dict(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
+                                      ratio_gin=ratio_gin, ratio_gout=ratio_gout, stride=stride, padding=padding,
+                                      dilation=dilation, groups=groups, bias=bias, enable_lfu=enable_lfu,
+                                      num_classes=num_classes)]
         self.stride = stride
         in_cg = int(in_channels * ratio_gin)
         in_cl = in_channels - in_cg
@@ -518,4 +539,4 @@ class FFC(_FFCExec, nn.Module):
                               num_classes)
 
     def forward(self, x, y=None):
-        return self._run(x, y)
+        return layer_call(self, self, x, y)

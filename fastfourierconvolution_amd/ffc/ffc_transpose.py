@@ -5,7 +5,7 @@ global branch: SpectralTransform with the x2 nearest upsample (upsample=True).
 """
 import torch.nn as nn
 
-from .ffc import _FFCExec
+from .ffc import _FFCExec, layer_call
 from .spectral_transform import SpectralTransform
 
 
@@ -16,6 +16,11 @@ class FFCTranspose(_FFCExec, nn.Module):
                  enable_lfu: bool = True, out_padding: int = 0, num_classes: int = 1):
         super().__init__()
         assert stride == 1 or stride == 2, "Stride should be 1 or 2."
+        self._ffc_ctor = ["FFCTranspose", dict(in_channels=in_channels, out_channels=out_channels,
+                                               kernel_size=kernel_size, ratio_gin=ratio_gin, ratio_gout=ratio_gout,
+                                               stride=stride, padding=padding, dilation=dilation, groups=groups,
+                                               bias=bias, enable_lfu=enable_lfu, out_padding=out_padding,
+                                               num_classes=num_classes)]
         self.stride = stride
         in_cg = int(in_channels * ratio_gin)
         in_cl = int(in_channels - in_cg)
@@ -41,4 +46,4 @@ class FFCTranspose(_FFCExec, nn.Module):
                                   groups=groups, bias=bias, dilation=dilation)
 
     def forward(self, x, y=None):
-        return self._run(x, y)
+        return layer_call(self, self, x, y)

@@ -1,8 +1,9 @@
 """Drop-in ``FourierUnitSN`` (reference: layers/ffc/fourier_unity.py:17-56).
 
 Same constructor, attribute names (``conv_layer``, ``bn``, ``relu``) and state_dict keys;
-forward runs the fused HIP Fourier unit (csrc/fu_kernels.hip) instead of
-rfftn -> 1x1 conv -> BatchNorm2d -> ReLU -> irfftn.
+forward runs the ffc::fourier_unit custom op -- the fused HIP Fourier unit (csrc/fu_kernels.hip,
+csrc/fu2d_kernels.hip) -- instead of rfftn -> 1x1 conv -> BatchNorm2d -> ReLU -> irfftn (the
+ffc::rfft2 / conv_layer / bn_act / irfft2 training ops under autograd).
 """
 import ctypes
 
@@ -11,19 +12,21 @@ import torch.nn as nn
 
 from .. import _autograd as ag
 from .. import _runtime as rt
+from .. import ops
 from .._lib import check, ptr
 
 
 class FourierUnitSN(nn.Module):
     def __init__(self, in_channels, out_channels, groups: int = 1, num_classes: int = 1):
         super().__init__()
+        self._ffc_ctor = ["FourierUnitSN", dict(in_channels=in_channels, out_channels=out_channels, groups=groups,
+                                                num_classes=num_classes)]
         self.groups = groups
         self.conv_layer = torch.nn.Conv2d(in_channels=in_channels * 2, out_channels=out_channels * 2,
                                           kernel_size=1, stride=1, padding=0, groups=self.groups, bias=False)
         self.bn = torch.nn.BatchNorm2d(out_channels * 2)
         self.relu = torch.nn.ReLU(inplace=True)
-        self._mix_key = None
-        self._mixT = None
+        self._packs = rt.PackCache()
         # "fp32" (exact, the reference's arithmetic) or "fp16": fp16 operands on the f16 MFMA with fp32
         # accumulation (BASELINE config 5); fp16 runs the staged FU (C in {16, 32, 64})
         self.mix_precision = "fp32"
@@ -36,16 +39,14 @@ class FourierUnitSN(nn.Module):
             raise NotImplementedError("FourierUnitSN with in_channels != out_channels")
 
     def _packed_mix(self, device, stream):
-        w = self.conv_layer.weight.detach()
-        w = rt.require(w, "conv_layer.weight")
-        key = (w.data_ptr(), w._version)
-        if key != self._mix_key or self._mixT is None or self._mixT.device != w.device:
+        w = rt.require(self.conv_layer.weight.detach(), "conv_layer.weight")
+
+        def build():
             C2 = w.shape[0]
-            mpad = -(-C2 // 32) * 32
-            self._mixT = torch.empty((C2, mpad), device=device, dtype=torch.float32)
-            check(rt.lib().ffc_fu_pack_mix(ptr(w), C2, ptr(self._mixT), stream), "ffc_fu_pack_mix")
-            self._mix_key = key
-        return self._mixT
+            mixT = torch.empty((C2, -(-C2 // 32) * 32), device=device, dtype=torch.float32)
+            check(rt.lib().ffc_fu_pack_mix(ptr(w), C2, ptr(mixT), stream), "ffc_fu_pack_mix")
+            return mixT
+        return self._packs.get("mix", [w], build)
 
     @staticmethod
     def _fold_ok(C, H, W):
@@ -118,13 +119,13 @@ class FourierUnitSN(nn.Module):
 
     def _packed_mix16(self, device, stream):
         w = rt.require(self.conv_layer.weight.detach(), "conv_layer.weight")
-        key = (w.data_ptr(), w._version)
-        if key != self.__dict__.get("_mix16_key"):
+
+        def build():
             C2 = w.shape[0]
-            self._mix16 = torch.empty((-(-C2 // 32) * 32, C2), device=device, dtype=torch.float16)
-            check(rt.lib().ffc_fu_pack_mix_f16(ptr(w), C2, ptr(self._mix16), stream), "ffc_fu_pack_mix_f16")
-            self.__dict__["_mix16_key"] = key
-        return self._mix16
+            mix16 = torch.empty((-(-C2 // 32) * 32, C2), device=device, dtype=torch.float16)
+            check(rt.lib().ffc_fu_pack_mix_f16(ptr(w), C2, ptr(mix16), stream), "ffc_fu_pack_mix_f16")
+            return mix16
+        return self._packs.get("mix16", [w], build)
 
     def _run2d(self, t, up, in_scale, in_shift, in_relu, residual):
         """large-plane FU: r2c -> mix (pass 0 stats, pass 1 BN/ReLU) -> c2r (include/ffc_amd.h ffc_fu2d_*)"""
@@ -196,4 +197,4 @@ class FourierUnitSN(nn.Module):
         x = rt.require(x, "x")
         if ag.wants_grad(self, x):
             return ag.fourier_unit(self, x, residual=False)
-        return self._run(x)
+        return ops.fu_forward(self, x)

@@ -21,6 +21,7 @@ import torch.nn as nn
 from .. import _autograd as ag
 from .. import _plan
 from .. import _runtime as rt
+from .. import ops
 from .._lib import check, ptr
 from .fourier_unity import FourierUnitSN
 
@@ -50,23 +51,17 @@ class SELayer(nn.Module):
         return g
 
     def forward(self, x):
-        """x * sigmoid(fc(avg_pool(x))) as one per-(b, c) scale launch."""
-        x = rt.require(x, "x")
-        if ag.wants_grad(self, x):
-            return ag.se_layer(self, x)
-        g = self.gate(x, False)
-        B, C, H, W = x.shape
-        zeros = torch.zeros(B * C, device=x.device, dtype=torch.float32)
-        out = torch.empty_like(x)
-        check(rt.lib().ffc_bn_act_apply(ptr(x), ptr(out), 1, B * C, H * W, ptr(g), ptr(zeros), 0, 0.0,
-                                        rt.stream_of(x)), "ffc_bn_act_apply")
-        return out
+        """x * sigmoid(fc(avg_pool(x))) on the ffc::se_scale op (gate + one per-(b, c) scale launch)."""
+        return ag.se_layer(self, rt.require(x, "x"))
 
 
 class SpectralTransform(nn.Module):
     def __init__(self, in_channels: int, out_channels: int, stride: int = 1, groups: int = 1,
                  enable_lfu: bool = False, upsample: bool = False, num_classes: int = 1):
         super().__init__()
+        self._ffc_ctor = ["SpectralTransform", dict(in_channels=in_channels, out_channels=out_channels, stride=stride,
+                                                    groups=groups, enable_lfu=enable_lfu, upsample=upsample,
+                                                    num_classes=num_classes)]
         self.enable_lfu = enable_lfu
         self.downsample = nn.Identity()
         if stride == 2 and upsample:
@@ -90,13 +85,13 @@ class SpectralTransform(nn.Module):
     def _conv1_T(self, stream):
         """conv1 weight transposed + zero padded for ffc_st_prologue (re-packed when it changes)"""
         w = rt.require(self.conv1.weight.detach(), "conv1.weight")
-        key = (w.data_ptr(), w._version)
-        if self.__dict__.get("_c1key") != key:
+
+        def build():
             c, cin = w.shape[0], w.shape[1]
-            self._c1T = torch.empty((cin, -(-c // 32) * 32), device=w.device, dtype=torch.float32)
-            check(rt.lib().ffc_pack_transpose(ptr(w), c, cin, ptr(self._c1T), stream), "ffc_pack_transpose")
-            self.__dict__["_c1key"] = key
-        return self._c1T
+            c1T = torch.empty((cin, -(-c // 32) * 32), device=w.device, dtype=torch.float32)
+            check(rt.lib().ffc_pack_transpose(ptr(w), c, cin, ptr(c1T), stream), "ffc_pack_transpose")
+            return c1T
+        return self.__dict__.setdefault("_packs", rt.PackCache()).get("conv1T", [w], build)
 
     def _mode(self):
         if self.stride == 2 and self.upsample:
@@ -172,10 +167,13 @@ class SpectralTransform(nn.Module):
                             "in FourierUnitSN, fourier_unity.py:46-47)")
         if ag.wants_grad(self, x):
             v = ag.spectral_v(self, rt.require(x, "x"))
-            cache = self.__dict__.setdefault("_train_cache", {})
-            (out,) = ag.conv_layer(cache, v.shape[0], [(self.conv2.out_channels, 0, 0.0)],
+            (out,) = ag.conv_layer(v.shape[0], [(self.conv2.out_channels, 0, 0.0)],
                                    [(0, 0, _plan.Seg("pw", v.shape[1], v.shape[2], v.shape[3]), self.conv2)], [v])
             return out
+        return ops.st_forward(self, x)
+
+    def _forward_fused(self, x):
+        """forward on the fused inference kernels (the ffc::spectral_transform op runs this)"""
         v = self.spectral(x)
         rt.sn_refresh(self.conv2)
         B, c, H, W = v.shape

@@ -77,11 +77,14 @@ def kfd_gpus(nodes_dir: str = KFD_NODES) -> int:
 def visible_gpus(nodes_dir: str = KFD_NODES) -> int:
     """GPUs this process could use, counted WITHOUT any HIP / HSA call (so a parent that spawns
     the ranks never opens /dev/kfd: ``torch.cuda.device_count()`` falls back to hipGetDeviceCount
-    when amdsmi discovery fails).  KFD topology, then ROCR_, HIP_ and CUDA_VISIBLE_DEVICES in the
-    order the ROCm stack applies them."""
-    n = kfd_gpus(nodes_dir)
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        n = _visible_filter(n, var)
+    when amdsmi discovery fails).  KFD topology, then ROCR_VISIBLE_DEVICES (ROCr), then ONE of the
+    HIP runtime's lists: HIP_VISIBLE_DEVICES when it is non-empty, else CUDA_VISIBLE_DEVICES when
+    that is non-empty (HIP reads the second only in place of the first, an empty value counting
+    as unset), as the ROCm stack applies them."""
+    n = _visible_filter(kfd_gpus(nodes_dir), "ROCR_VISIBLE_DEVICES")
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if os.environ.get(var):
+            return _visible_filter(n, var)
     return n
 
 

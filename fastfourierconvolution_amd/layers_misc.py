@@ -2,7 +2,7 @@
 (layers/print_layer.py:10-32), NoiseInjection (layers/noise_injection.py:20-32).
 
 Resizer / Print only move tuples around or print shapes.  NoiseInjection's add (fgan128 train
-mode) runs in the HIP library (ffc_noise_inject); the noise itself is drawn with torch's device
+mode) runs in the HIP library (the ffc::noise_inject op); the noise itself is drawn with torch's device
 RNG as the reference draws it with normal_() (or passed explicitly, as in the reference's
 ``forward(x, noise)``).
 """
@@ -58,21 +58,7 @@ class NoiseInjection(nn.Module):
         self.weight = nn.Parameter(torch.zeros(1, channels, 1, 1))
 
     def forward(self, x, noise=None):
-        from . import _runtime as rt
-        from ._lib import check, ptr
-        x = rt.require(x, "x")
-        batch, C, height, width = x.shape
-        if noise is None:
-            noise = x.new_empty(batch, 1, height, width).normal_()
-        noise = rt.require(noise, "noise")
-        if tuple(noise.shape) != (batch, 1, height, width) or (height * width) % 4:
-            raise NotImplementedError("NoiseInjection: noise must be (B, 1, H, W) with H*W % 4 == 0")
+        """x + weight * noise on the ffc::noise_inject op (its weight gradient on ffc::noise_wgrad)"""
         from . import _autograd as ag
-        if ag.wants_grad(self, x):   # training path: weight gradient through ffc_noise_wgrad
-            return ag.noise_inject(self, x, noise)
-        w = rt.require(self.weight.detach(), "weight")
-        out = torch.empty_like(x)
-        with rt.observe("noise_inject", bytes=8.0 * x.numel() + 4.0 * noise.numel()):
-            check(rt.lib().ffc_noise_inject(ptr(x), ptr(w), ptr(noise), ptr(out), batch, C, height * width,
-                                            rt.stream_of(x)), "ffc_noise_inject")
-        return out
+        from . import _runtime as rt
+        return ag.noise_inject(self, rt.require(x, "x"), noise)

@@ -160,8 +160,6 @@ class FGenerator(FFCModel):
         self.glb_noise6 = NoiseInjection(int(ngf * ratio_g))
         self.conv7 = FFC_BN_ACT(ngf, 3, 3, ratio_g, 0.0, stride=1, padding=1, activation_layer=nn.Tanh,
                                 norm_layer=nn.Identity, upsampling=False, uses_noise=True, uses_sn=True)
-        self._lin = {}
-        self._lin_train = {}
 
     def _noise_to_feature(self, z):
         """nn.Linear(z_size, 16*1024) (fgan128_complete.py:453-455) on the HIP dense GEMM"""
@@ -171,20 +169,8 @@ class FGenerator(FFCModel):
             raise RuntimeError(f"FGenerator: z must be (B, {lin.in_features}), got {tuple(z.shape)}")
         B = z.shape[0]
         if ag.wants_grad(self.noise_to_feature, z):   # training path: Linear as a 1x1 conv job with autograd
-            return ag.linear(self._lin_train, lin, z).view(B, -1, self.mg, self.mg)
-        w = rt.require(lin.weight.detach(), "noise_to_feature.0.weight")
-        b = rt.require(lin.bias.detach(), "noise_to_feature.0.bias") if lin.bias is not None else None
-        key = (w.data_ptr(), w._version)
-        if self._lin.get("key") != key:
-            self._lin["Wt"] = w.t().contiguous()
-            self._lin["key"] = key
-        Wt = self._lin["Wt"]
-        out = torch.empty((B, lin.out_features), device=z.device, dtype=torch.float32)
-        with rt.observe("dense", flops=2.0 * B * lin.in_features * lin.out_features):
-            check(rt.lib().ffc_dense_forward(ptr(z), ptr(Wt), ptr(b), B, lin.in_features, lin.out_features,
-                                             lin.out_features, ptr(out), None, 0, 0.0, rt.stream_of(z)),
-                  "ffc_dense_forward")
-        return out.view(B, -1, self.mg, self.mg)
+            return ag.linear(lin, z).view(B, -1, self.mg, self.mg)
+        return torch.ops.ffc.linear(z, lin.weight, lin.bias).view(B, -1, self.mg, self.mg)
 
     def forward_float(self, z, noises=None):
         """FGenerator.forward up to the float image (:491-515): the eval-mode uint8 quantization of
@@ -208,9 +194,7 @@ class FGenerator(FFCModel):
         fake = self.forward_float(z, noises)
         if self.training:
             return fake
-        out = torch.empty(fake.shape, device=fake.device, dtype=torch.uint8)   # :516-521
-        check(rt.lib().ffc_quantize_u8(ptr(fake), ptr(out), fake.numel(), rt.stream_of(fake)), "ffc_quantize_u8")
-        return out
+        return torch.ops.ffc.quantize_u8(fake)   # :516-521
 
 
 class Discriminator(FFCModel):
@@ -221,7 +205,7 @@ class Discriminator(FFCModel):
     state_dict are the reference's.
 
     Every conv is one implicit-GEMM launch of libffc_amd.so with bias + LeakyReLU in its epilogue
-    (_autograd.conv_layer: data / weight / bias gradients on the HIP kernels too); the spectral-norm
+    (the ffc::conv_layer op: data / weight / bias gradients on the HIP kernels too); the spectral-norm
     pre-hook runs before each launch as the reference's module call runs it (one power iteration per
     forward in train mode).  Input: (B, 3, 32*mg, 32*mg) fp32 on the GPU."""
 
@@ -237,7 +221,6 @@ class Discriminator(FFCModel):
         self.fc = sn_fn(nn.Linear(self.mg * self.mg * 512, 1))
         self.act = nn.LeakyReLU(0.1)
         self.last_act = nn.Sigmoid()
-        self._caches = {}
 
     def forward(self, x):
         x = rt.require(x, "x")
@@ -250,9 +233,8 @@ class Discriminator(FFCModel):
             conv = getattr(self, f"conv{i}")
             B, C, H, W = m.shape
             sg = _plan.Seg("conv", C, H, W, conv.kernel_size[0], conv.stride[0], conv.padding[0])
-            (m,) = ag.conv_layer(self._caches.setdefault(i, {}), B, [(conv.out_channels, act, param)],
-                                 [(0, 0, sg, conv)], [m])
-        return ag.linear(self._caches.setdefault("fc", {}), self.fc, m.reshape(m.shape[0], -1))   # :556
+            (m,) = ag.conv_layer(B, [(conv.out_channels, act, param)], [(0, 0, sg, conv)], [m])
+        return ag.linear(self.fc, m.reshape(m.shape[0], -1))   # :556
 
 
 FGanDiscriminator = Discriminator

@@ -64,7 +64,7 @@ def test_single_rank_plan():
 
 
 def test_more_gpus_than_visible_fails():
-    res = _bench("--gpus", "2", env={"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": ""})
+    res = _bench("--gpus", "2", env={"ROCR_VISIBLE_DEVICES": ""})
     if res.returncode == 0:
         pytest.fail("bench.py --gpus 2 with no visible GPU must not succeed")
     assert res.returncode == 3 and "visible" in res.stderr

@@ -148,3 +148,46 @@ def test_fgan128_train_step():
     opt.step()
     out2 = G.forward_float(z.cuda(), [(a.cuda(), b.cuda()) for a, b in noises])
     assert not torch.equal(out2.detach(), out.detach())
+
+
+def test_fgan128_train_iteration_graph_replay_matches_eager():
+    """the fgan128train bench step -- generator_step + discriminator_step (fgan128_complete.py:680-703)
+    with the spectral-norm Discriminator, AdamW(capturable), NoiseInjection and weight re-packs keyed by
+    weight version -- replayed from one captured hipGraph gives bit-identical G / D weights, BN buffers
+    and spectral-norm weight_u / weight_v to the same number of eager iterations"""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd.graphs import capture_step
+    from fastfourierconvolution_amd.training import discriminator_step, generator_step
+    B = 4
+    gen = torch.Generator().manual_seed(5)
+    z_g = torch.randn(B, 128, generator=gen).cuda()
+    z_d = torch.randn(B, 128, generator=gen).cuda()
+    real = (torch.rand(B, 3, 128, 128, generator=gen) * 2 - 1).cuda()
+    noises = [tuple(torch.randn(B, 1, s, s, generator=gen).cuda() for _ in range(2)) for s in (8, 16, 32, 64, 128)]
+    res = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        with contextlib.redirect_stdout(io.StringIO()):
+            G = F.FGenerator(128)
+        D = F.Discriminator()
+        G, D = G.cuda().train(), D.cuda().train()
+        kw = dict(lr=2e-4, betas=(0.5, 0.999), foreach=True, capturable=True)
+        optim_G, optim_D = torch.optim.AdamW(G.parameters(), **kw), torch.optim.AdamW(D.parameters(), **kw)
+
+        def step():
+            generator_step(G, D, optim_G, optim_D, z_g, noises)
+            discriminator_step(G, D, optim_G, optim_D, z_d, real, noises)
+        if graph:
+            g = capture_step(step, warmup=2)
+            assert g is not None, "capture failed"
+            for _ in range(2):
+                g.replay()
+        else:
+            for _ in range(4):
+                step()
+        torch.cuda.synchronize()
+        res.append({n + k: v.detach().cpu().clone() for n, m in (("G.", G), ("D.", D))
+                    for k, v in m.state_dict().items()})
+    assert any(k.endswith("weight_u") for k in res[0])
+    for k in res[0]:
+        assert torch.equal(res[0][k], res[1][k]), k

@@ -1,0 +1,145 @@
+"""torch.library.opcheck over every ffc:: custom op (schema / mutation declarations, fake vs real
+metadata, autograd registration, AOT dispatch with dynamic shapes) on real HIP tensors, plus the
+module forward through the op against a direct call of the op."""
+import contextlib
+import io
+
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _opcheck(op, args, **kw):
+    res = torch.library.opcheck(op, args, kw or None, raise_exception=False)
+    bad = {k: v for k, v in res.items() if v != "SUCCESS"}
+    assert not bad, f"{op}: {bad}"
+
+
+def _quiet(fn, *a, **k):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a, **k)
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+def test_opcheck_conv_layer():
+    from fastfourierconvolution_amd import _autograd as ag
+    from fastfourierconvolution_amd import _plan
+    x = torch.randn(4, 16, 8, 8, device=DEV, requires_grad=True)
+    x2 = torch.randn(4, 8, 8, 8, device=DEV, requires_grad=True)
+    w = (0.1 * torch.randn(16, 32, 4, 4, device=DEV)).requires_grad_()     # ConvTranspose2d(16, 32, 4, 2, 1)
+    w2 = (0.1 * torch.randn(8, 32, 4, 4, device=DEV)).requires_grad_()
+    b = torch.randn(32, device=DEV, requires_grad=True)
+    for act in (0, 2, 5):   # Identity, LeakyReLU (fused), GELU (pre-activation output too)
+        spec = ag.conv_spec([(32, act, 0.1)], [(0, 0, _plan.Seg("convT", 16, 8, 8, 4, 2, 1), 1, 0),
+                                               (0, 1, _plan.Seg("convT", 8, 8, 8, 4, 2, 1), 1, -1)])
+        _opcheck(torch.ops.ffc.conv_layer.default, ([x, x2], [w, w2], [b], spec))
+    wc = (0.1 * torch.randn(24, 16, 3, 3, device=DEV)).requires_grad_()   # Conv2d 3x3 s1 p1 into two outputs
+    spec = ag.conv_spec([(24, 1, 0.0), (24, 0, 0.0)], [(0, 0, _plan.Seg("conv", 16, 8, 8, 3, 1, 1), 0, -1),
+                                                       (1, 0, _plan.Seg("conv", 16, 8, 8, 3, 1, 1), 0, -1)])
+    _opcheck(torch.ops.ffc.conv_layer.default, ([x], [wc, wc], [], spec))
+
+
+@pytest.mark.parametrize("use_batch", [True, False])
+def test_opcheck_bn_act(use_batch):
+    x = torch.randn(4, 16, 8, 8, device=DEV, requires_grad=True)
+    g = (1 + 0.1 * torch.randn(16, device=DEV)).requires_grad_()
+    b = (0.1 * torch.randn(16, device=DEV)).requires_grad_()
+    rm, rv = 0.1 * torch.randn(16, device=DEV), 0.5 + torch.rand(16, device=DEV)
+    for act in (1, 5):
+        _opcheck(torch.ops.ffc.bn_act.default, (x, g, b, rm, rv, use_batch, 1e-5, act, 0.0))
+    _, _, _, stats = torch.ops.ffc.bn_act(x.detach(), g.detach(), b.detach(), rm, rv, True, 1e-5, 1, 0.0)
+    nbt = torch.tensor(3, device=DEV, dtype=torch.long)
+    _opcheck(torch.ops.ffc.bn_update_running.default, (rm.clone(), rv.clone(), nbt, stats, 0.1, 1.0))
+
+
+def test_opcheck_small_ops():
+    x = torch.randn(4, 16, 8, 8, device=DEV, requires_grad=True)
+    _opcheck(torch.ops.ffc.pool2.default, (x, 0.25))
+    _opcheck(torch.ops.ffc.up2.default, (x, 1.0))
+    _opcheck(torch.ops.ffc.rfft2.default, (x, 1.0))
+    Z = torch.randn(4, 32, 8, 5, device=DEV, requires_grad=True)
+    _opcheck(torch.ops.ffc.irfft2.default, (Z, 8, 8, 1.0, None))
+    _opcheck(torch.ops.ffc.irfft2.default, (Z, 8, 8, 1.0, x))
+    for hid in (1, 0):   # SELayer(16): hidden 16 // 16 = 1; SELayer(8): hidden 0 (gate 0.5)
+        w1 = (0.3 * torch.randn(hid, 16, device=DEV)).requires_grad_()
+        w2 = (0.3 * torch.randn(16, hid, device=DEV)).requires_grad_()
+        _opcheck(torch.ops.ffc.se_scale.default, (x, w1, w2))
+    w = (0.1 * torch.randn(1, 16, 1, 1, device=DEV)).requires_grad_()
+    _opcheck(torch.ops.ffc.noise_inject.default, (x, w, torch.randn(4, 1, 8, 8, device=DEV)))
+    z = torch.randn(8, 128, device=DEV)
+    _opcheck(torch.ops.ffc.linear.default, (z, torch.randn(256, 128, device=DEV), torch.randn(256, device=DEV)))
+    _opcheck(torch.ops.ffc.quantize_u8.default, (torch.randn(2, 3, 16, 16, device=DEV),))
+
+
+def _layer_args(m, x_l, x_g):
+    from fastfourierconvolution_amd import ops
+    spec = ops.layer_spec(m)
+    params, buffers = ops.layer_tensors(m, spec)
+    return (x_l, x_g, [p.detach() for p in params], [b.clone() for b in buffers], [], [], [], False, spec)
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_opcheck_layer_ops(train):
+    import fastfourierconvolution_amd as F
+    blk = _quiet(F.FFC_BN_ACT, 32, 32, 3, 0.5, 0.5, 1, 1, norm_layer=nn.BatchNorm2d,
+                 activation_layer=nn.ReLU).to(DEV).train(train)
+    xl, xg = torch.randn(4, 16, 32, 32, device=DEV), torch.randn(4, 16, 32, 32, device=DEV)
+    _opcheck(torch.ops.ffc.ffc_bn_act.default, _layer_args(blk, xl, xg))
+    up = _quiet(F.FFC_BN_ACT, 256, 128, 4, 0.5, 0.5, 2, 1, activation_layer=nn.LeakyReLU,
+                upsampling=True).to(DEV).train(train)                                 # FFCGenerator ffc2
+    _opcheck(torch.ops.ffc.ffc_bn_act.default, _layer_args(up, torch.randn(8, 128, 8, 8, device=DEV),
+                                                           torch.randn(8, 128, 8, 8, device=DEV)))
+    first = _quiet(F.FFC_BN_ACT, 100, 512, 4, 0, 0.5, 1, 0, activation_layer=nn.LeakyReLU,
+                   upsampling=True).to(DEV).train(train)                              # ffc0: x_g is the int 0
+    _opcheck(torch.ops.ffc.ffc_bn_act.default, _layer_args(first, torch.randn(8, 100, 1, 1, device=DEV), None))
+    from fastfourierconvolution_amd import ops
+    st = _quiet(F.SpectralTransform, 64, 64, 2, upsample=True).to(DEV).train(train)
+    spec = ops.layer_spec(st)
+    p, b = ops.layer_tensors(st, spec)
+    _opcheck(torch.ops.ffc.spectral_transform.default, (torch.randn(8, 64, 8, 8, device=DEV),
+                                                        [t.detach() for t in p], [t.clone() for t in b], spec))
+    fu = F.FourierUnitSN(16, 16).to(DEV).train(train)
+    spec = ops.layer_spec(fu)
+    p, b = ops.layer_tensors(fu, spec)
+    _opcheck(torch.ops.ffc.fourier_unit.default, (torch.randn(4, 16, 32, 32, device=DEV),
+                                                  [t.detach() for t in p], [t.clone() for t in b], spec))
+
+
+def test_module_forward_is_the_op():
+    """FFC_BN_ACT.forward under no_grad == the ffc::ffc_bn_act op on the module's tensors, bit for bit
+    (eval mode: no running-stat side effects between the calls)"""
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import ops
+    blk = _quiet(F.FFC_BN_ACT, 32, 32, 3, 0.5, 0.5, 1, 1, norm_layer=nn.BatchNorm2d,
+                 activation_layer=nn.ReLU).to(DEV).eval()
+    xl, xg = torch.randn(4, 16, 32, 32, device=DEV), torch.randn(4, 16, 32, 32, device=DEV)
+    with torch.no_grad():
+        ol, og = blk((xl, xg))
+        spec = ops.layer_spec(blk)
+        p, b = ops.layer_tensors(blk, spec)
+        rl, rg = torch.ops.ffc.ffc_bn_act(xl, xg, p, b, [], [], [], False, spec)[:2]
+    assert torch.equal(ol, rl) and torch.equal(og, rg)
+
+
+def test_two_models_same_structure_do_not_share_packed_weights():
+    """the layer ops' packed-weight caches are keyed by the weight tensor object (rt.weight_key): two
+    generators of one structure, built and freed in turn, never see each other's packs"""
+    import fastfourierconvolution_amd as F
+    z = torch.randn(16, 100, 1, 1, device=DEV)
+    outs = []
+    for seed in (1, 2, 1):
+        torch.manual_seed(seed)
+        g = _quiet(F.FFCGenerator, 100, 3, 32).to(DEV).eval()
+        with torch.no_grad():
+            outs.append(g(z).clone())
+        del g
+        torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[2]) and not torch.equal(outs[0], outs[1])

@@ -44,7 +44,13 @@ def _fake_topology(root, gpus, cpus=1):
     return str(root)
 
 
-@pytest.mark.parametrize("env,want", [({}, 8), ({"HIP_VISIBLE_DEVICES": "0,1"}, 2), ({"HIP_VISIBLE_DEVICES": ""}, 0),
+@pytest.mark.parametrize("env,want", [({}, 8), ({"HIP_VISIBLE_DEVICES": "0,1"}, 2),
+                                      # HIP reads CUDA_VISIBLE_DEVICES only when HIP_VISIBLE_DEVICES is
+                                      # unset or empty; the two lists are never combined
+                                      ({"HIP_VISIBLE_DEVICES": ""}, 8),
+                                      ({"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7", "CUDA_VISIBLE_DEVICES": "0"}, 8),
+                                      ({"HIP_VISIBLE_DEVICES": "", "CUDA_VISIBLE_DEVICES": "0,1"}, 2),
+                                      ({"ROCR_VISIBLE_DEVICES": ""}, 0),
                                       ({"ROCR_VISIBLE_DEVICES": "3"}, 1),
                                       ({"ROCR_VISIBLE_DEVICES": "0,1,2", "HIP_VISIBLE_DEVICES": "1,2"}, 2),
                                       ({"CUDA_VISIBLE_DEVICES": "0,9"}, 1),
