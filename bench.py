@@ -16,12 +16,13 @@ use batch statistics), synthetic z ~ N(0,1), weights from the reference's weight
 (fgan64_complete.py:22-31: conv N(0, 0.02), BN gamma N(1, 0.02), beta 0).
 One step = one generator forward over one batch; inputs resident in HBM.
 
-Scaling (``--scaling``, default weak): every GPU runs the configuration's batch (gen64 256,
+Scaling (``--scaling``, default strong): the configuration's batch split over the ranks, with the
+weak-scaling figure alongside at N > 1.  ``--scaling weak``: every GPU runs the configuration's batch (gen64 256,
 fgan128 512 = configs[3], fgan128sn 1024 = configs[4]); the job's global batch is N x that, drawn
 once from one seed and sliced per rank, and train-mode BN normalises over ALL of it (SyncBN: the
-BN moments are all-reduced over RCCL, so the sharded result equals the global-batch forward).
-``--scaling strong`` splits the configuration's batch over the ranks instead (the per-rank
-shard steps and the strong-scaling budget are in DESIGN.md §5).  One process per GPU; weights are
+BN moments are all-reduced over RCCL, so the sharded result equals the global-batch forward; the
+strong split does the same over the configuration's batch).  The per-rank shard steps and the
+strong-scaling budget are in DESIGN.md §5.  One process per GPU; weights are
 broadcast once at init.  The step is hipGraph-captured (thread-local capture, the RCCL
 all-reduces inside the graph; graphs.py).  At N > 1 the gen64 line also carries the gathered
 global-batch output's parity against the CPU reference.
@@ -121,8 +122,8 @@ def parse():
     p.add_argument("--workload", choices=["gen64", "fgan128", "fgan128sn", "gan64train", "fgan128train", "block"],
                    default="gen64",
                    help="gen64: FFCGenerator 64x64 (BASELINE metric, configs[1]/[2]); "
-                        "fgan128: fgan128 FGenerator 128x128x3 (configs[3], 64 per GPU = B 512 / 8); "
-                        "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4], 128 per GPU); "
+                        "fgan128: fgan128 FGenerator 128x128x3 (configs[3]: B 512, split over the GPUs); "
+                        "fgan128sn: its spectral-norm variant with the fp16 mix (configs[4]: B 1024, split); "
                         "gan64train: generator + discriminator 64x64x3 fwd+bwd + Adam (configs[2], B=256); "
                         "fgan128train: fgan128 training iteration, G update + D update (fgan128_complete.py:680-703, "
                         "B=64); "
@@ -134,10 +135,11 @@ def parse():
                         "WORLD_SIZE is unset")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--scaling", choices=["strong", "weak"], default="weak",
-                   help="weak (default): every GPU runs the configuration's batch (gen64 256, fgan128 512, "
-                        "fgan128sn 1024), global batch = N x that, SyncBN over all of it; strong: the "
-                        "configuration's batch split over the ranks")
+    p.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                   help="strong (default): the configuration's batch (gen64 256, fgan128 512, fgan128sn 1024) "
+                        "split over the ranks, as BASELINE configs[3]/[4] shard it; at N > 1 the line also "
+                        "carries the weak-scaling measurement (every GPU runs the configuration's batch) in "
+                        "'weak_scaling'.  weak: only that measurement")
     p.add_argument("--global-batch", type=int, default=None,
                    help="strong scaling global batch (gen64: 256, fgan128: 512, fgan128sn: 1024)")
     p.add_argument("--batch", type=int, default=None, help="weak scaling samples per GPU (gen64: 256, "
@@ -755,6 +757,29 @@ def main():
     value = global_batch * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
+    weak = None
+    if world > 1 and args.scaling == "strong":
+        # beside the strong split: every GPU runs the configuration's whole batch (SURVEY.md §8e "report
+        # weak scaling alongside"), z from the same seed, SyncBN over the N x larger global batch
+        per = WEAK_BATCH[args.workload]
+        zw = torch.randn((per * world, 128) if fgan else (per * world, args.nz, 1, 1),
+                         generator=torch.Generator(device="cpu").manual_seed(100))[rank * per:(rank + 1) * per].to(dev)
+
+        def step_w():
+            with torch.no_grad():
+                return G.forward_float(zw) if fgan else G(zw)
+        for _ in range(max(1, args.warmup)):
+            step_w()
+        gw = capture_step(step_w, warmup=1) if use_graph else None
+        run_w = gw.replay if gw is not None else step_w
+        for _ in range(max(1, args.warmup)):
+            run_w()
+        el_w, med_w = time_steps(run_w, args.steps, world)
+        weak = {"value": round(per * world * args.steps / el_w, 1), "unit": "images/s", "per_gpu_batch": per,
+                "global_batch": per * world, "ms_per_step": round(el_w * 1e3 / args.steps, 4),
+                "ms_per_step_median": round(med_w, 4), "hipgraph": gw is not None}
+        del gw
+
     # ---- live per-kernel roofline: one instrumented eager pass (HIP events on the launch stream)
     summ, out = profile_pass(step, args.profile_steps)
     kernels = {k: {"launches_per_step": v["launches"] / max(1, args.profile_steps),
@@ -844,6 +869,8 @@ def main():
             "roofline": roof, "fft_roofline": fft_roof, "cpu_baseline": cpu, "parity": parity,
             "kernels": kernels,
         }
+        if weak is not None:
+            line["weak_scaling"] = weak
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -95,6 +95,9 @@ def adjoint_seg(sg: _plan.Seg, M: int, OH: int, OW: int) -> _plan.Seg:
 def run_conv(cache, key, B, M, segs, weights, inputs, out_shape=None, act=(0, 0.0), addend=None):
     """one implicit-GEMM launch: out = act(sum_s conv_s(x_s) [+ addend]) (plans cached in ``cache``)"""
     dev = inputs[0].device
+    # the job's full shape and the plan switches are part of the key (a caller's key alone may leave
+    # out the output channels, and one cache serves every module of a structure)
+    key = (key, B, M, tuple(segs), str(dev), rt.plan_knobs())
     hit = cache.get(key)
     if hit is None:
         ex = rt.ConvExec(B, M, list(segs), weights, dev, pw_ok=True)
@@ -319,7 +322,7 @@ def conv_layer_backward_impl(xs, ws, ts, gouts, needs, spec):
         for grp in groups:
             segs = tuple(a[1] for a in grp)
             wts = [(ws[a[0]].contiguous(), 1 - a[2], a[1].k, a[1].k, None) for a in grp]
-            key = ("adj", spec, i, tuple(a[0] for a in grp), B, segs)
+            key = ("adj", spec, i, tuple(a[0] for a in grp), B, C, segs)
             dx = conv_forward(_CL_CACHE, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
                               addend=dx)
         grads[i] = dx

@@ -418,14 +418,18 @@ def note_tensors(ts):
                 e = (weakref.ref(a, lambda _r, k=k: _EPOCH["by_id"].pop(k, None)), _EPOCH["next"])
                 _EPOCH["next"] += 1
                 by_id[k] = e
-            by_ptr[t.data_ptr()] = e[1]
+            by_ptr[t.data_ptr()] = (e[0], e[1])
 
 
 def weight_key(t):
-    """cache key of a weight's packed form: (pointer, version, epoch of the tensor object)"""
+    """cache key of a weight's packed form: (pointer, version, epoch of the live tensor object noted at
+    that pointer; 0 when none is alive there)"""
     if t is None:
         return None
-    return t.data_ptr(), t._version, _EPOCH["by_ptr"].get(t.data_ptr(), 0)
+    p = t.data_ptr()
+    e = _EPOCH["by_ptr"].get(p)
+    a = e[0]() if e is not None else None
+    return p, t._version, e[1] if a is not None and a.data_ptr() == p else 0
 
 
 def _wkey(ts):
@@ -449,6 +453,13 @@ class PackCache:
 
 
 # --------------------------------------------------------------------------- convolution jobs
+
+
+def plan_knobs():
+    """the module-level switches plans depend on (tests and A/B runs flip them): part of every plan
+    cache key, so a changed switch never meets a plan made under another setting"""
+    return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
+            FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL)
 
 
 def algorithmic_flops(plan) -> float:

@@ -91,7 +91,7 @@ __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool l
                 const float g = f.gamma ? f.gamma[o2] : 1.0f;
                 const float b = f.beta ? f.beta[o2] : 0.0f;
                 const float scale = g * inv;
-                const float shift = b - mean * scale;
+                const float shift = fmaf(-mean, scale, b);   // as bn_se_kernels.hip finalize_channel
                 sc[o2] = scale;
                 sh[o2] = shift;
                 if (leader) {
@@ -100,8 +100,8 @@ __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool l
                         if (fm < 0.0f) fm = 1.0f / (float)(nbt + 1);   // momentum=None: cumulative average
                         const double nfull = N * (double)f.count_mult;
                         const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
-                        f.running_mean[o2] = (1.0f - fm) * f.running_mean[o2] + fm * mean;
-                        f.running_var[o2] = (1.0f - fm) * f.running_var[o2] + fm * (float)unb;
+                        f.running_mean[o2] = fmaf(fm, mean, (1.0f - fm) * f.running_mean[o2]);
+                        f.running_var[o2] = fmaf(fm, (float)unb, (1.0f - fm) * f.running_var[o2]);
                     }
                     if (f.scale_out) f.scale_out[o2] = scale;
                     if (f.shift_out) f.shift_out[o2] = shift;

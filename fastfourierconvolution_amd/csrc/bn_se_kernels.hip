@@ -117,8 +117,11 @@ __device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a,
             if (f < 0.0f) f = 1.0f / (float)(in.nbt + 1);  // momentum=None: cumulative average
             const double nfull = n * (double)a.count_mult;
             const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
-            a.running_mean[c] = (1.0f - f) * in.rm + f * mean;
-            a.running_var[c] = (1.0f - f) * in.rv + f * (float)unb;
+            // explicit fmaf: the single, batched and in-kernel-fold finalizes then round identically
+            // whatever contraction the compiler picks per kernel (a -fno-slp-vectorize build broke
+            // their bit-identity, profiles/r03/s2l/tests_noslp.log)
+            a.running_mean[c] = fmaf(f, mean, (1.0f - f) * in.rm);
+            a.running_var[c] = fmaf(f, (float)unb, (1.0f - f) * in.rv);
         }
     } else {
         mean = in.rm;
@@ -127,7 +130,7 @@ __device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a,
     const float inv = 1.0f / sqrtf(var + a.eps);
     const float sc = in.g * inv;
     a.scale[c] = sc;
-    a.shift[c] = in.bb - mean * sc;
+    a.shift[c] = fmaf(-mean, sc, in.bb);
 }
 
 __device__ void finalize_channel(const double* m3, int c, const FinalizeArgs& a) {

@@ -7,6 +7,22 @@ namespace {
 
 #include "twiddles.inc"
 
+// Lanes of ONE wave exchanging values through LDS (the line FFTs' stage B, the r2c half-spectrum
+// separation, the c2r row hand-off): a lane reads slots other lanes of its wave wrote, or overwrites
+// slots they still read.  The hardware keeps a wave's LDS operations in issue order, but the
+// compiler reasons per lane: with no synchronisation between the lanes the exchange is a data race
+// in the HIP memory model, and the compiler may move a lane's load past its own store to a slot it
+// believes unrelated (or the reverse).  The r03 -fno-slp-vectorize build did exactly that in
+// fu2d_kernels.hip: correct results depended on the vectorizer.  A wavefront-scope
+// release / acquire fence pair around wave_barrier orders the LDS accesses across the exchange for
+// the compiler; at wavefront scope the fences emit no instruction (AMDGPU memory model), so the
+// order costs nothing at run time.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n >> 1); }
 constexpr int brevc(int i, int bits) {
     int r = 0;

@@ -19,9 +19,10 @@
 //
 // Line FFTs of length N = N1*N2 are split over the N1 lanes of one wave: each lane runs an
 // N2-point FFT in registers, multiplies the twiddles W_N^{j k2}, and the lanes exchange through
-// the line's own LDS slots (same wave: LDS operations complete in issue order, no barrier) for
-// the N1-point FFTs.  The upsample identity lets r2c transform the 4x smaller t plane, and the
-// mix reads the 4x smaller T, so HBM carries: r2c t + T, mix T (+ Y), c2r Y + t + out.
+// the line's own LDS slots for the N1-point FFTs (same wave: no workgroup barrier; every exchange
+// is fenced for the compiler by wave_lds_sync, fft_common.h).  The upsample identity lets r2c
+// transform the 4x smaller t plane, and the mix reads the 4x smaller T, so HBM carries: r2c t + T,
+// mix T (+ Y), c2r Y + t + out.
 #include "ffc_internal.h"
 
 #include <algorithm>
@@ -94,8 +95,10 @@ __device__ __forceinline__ void stage_b(float2* line, int stride, const float (&
                                         float (&ore)[Split<N>::Q][Split<N>::N1],
                                         float (&oim)[Split<N>::Q][Split<N>::N1]) {
     constexpr int N1 = Split<N>::N1, N2 = Split<N>::N2, Q = Split<N>::Q;
+    wave_lds_sync();   // the group's earlier reads of this line precede these writes
 #pragma unroll
     for (int k2 = 0; k2 < N2; ++k2) line[(jj + N1 * k2) * stride] = make_float2(re[k2], im[k2]);
+    wave_lds_sync();   // every lane's stage-A results are in the line before anyone reads a column
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const int k2 = jj + N1 * q;
@@ -106,6 +109,7 @@ __device__ __forceinline__ void stage_b(float2* line, int stride, const float (&
             oim[q][n1] = v.y;
         }
     }
+    wave_lds_sync();   // every lane's reads are done before a caller overwrites the line
 #pragma unroll
     for (int q = 0; q < Q; ++q) fft_reg<N1, INV>(ore[q], oim[q]);
 }
@@ -231,6 +235,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
 #pragma unroll
                     for (int k1 = 0; k1 < N1; ++k1)
                         line[(jj + N1 * q) + N2 * k1] = make_float2(ore[q][k1], oim[q][k1]);
+                wave_lds_sync();   // the whole spectrum is in the line
                 // separate: A[k] = (Z[k] + conj Z[-k]) / 2, B[k] = (Z[k] - conj Z[-k]) / 2i, k = 0..w/2
                 constexpr int KPL = (WPt + N1 - 1) / N1;
                 float2 zk[KPL], zm[KPL];
@@ -242,6 +247,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
                         zm[i] = line[(w - k) & (w - 1)];
                     }
                 }
+                wave_lds_sync();   // every lane has read Z[k] and Z[-k] before the halves overwrite them
 #pragma unroll
                 for (int i = 0; i < KPL; ++i) {
                     const int k = jj + N1 * i;
@@ -471,6 +477,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
                         fa[x] = ore[q][k1];
                         fa[W + x] = oim[q][k1];
                     }
+                wave_lds_sync();   // both output rows are in LDS before the lanes read them as float4
                 // scale, residual, store (float4 per lane, the group covers both rows)
 #pragma unroll
                 for (int i = 0; i < (2 * W / 4 + N1 - 1) / N1; ++i) {
@@ -677,6 +684,7 @@ __global__ __launch_bounds__(FU2_THREADS, 4) void fu2d_c2r_fold_kernel(C2rArgs a
                         fa[x] = ore[q][k1];
                         fa[W + x] = oim[q][k1];
                     }
+                wave_lds_sync();   // both output rows are in LDS before the lanes read them as float4
 #pragma unroll
                 for (int i = 0; i < RITER; ++i) {
                     const int q4 = jj + N1 * i;
@@ -1195,6 +1203,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_rows_kernel(C2rArgs a) {
                 fa[x] = ore[q][k1];
                 fa[W + x] = oim[q][k1];
             }
+        wave_lds_sync();   // both output rows are in LDS before the lanes read them as float4
 #pragma unroll
         for (int i = 0; i < (2 * W / 4 + N1 - 1) / N1; ++i) {
             const int q4 = jj + N1 * i;

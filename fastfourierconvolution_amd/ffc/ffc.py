@@ -382,6 +382,7 @@ class _FFCExec:
                     del cache[old]
                 wr = wt.permute(1, 2, 3, 0).reshape(M * k * k, sg.C, 1, 1).contiguous()   # (C,M,k,k) -> (M k k, C)
                 br = bias.repeat_interleave(k * k).contiguous() if bias is not None else None
+                rt.note_tensors([wr, br])   # the dense launch's packed-weight key is taken from these
                 hit = cache[key] = (wr, br)
             segs2.append(_plan.Seg("pw", sg.C, 1, 1))
             w2.append((hit[0], 0, 1, 1, hit[1]))

@@ -484,8 +484,14 @@ class _Template:
                     getattr(sub, kind)[leaf] = t
 
 
-@functools.lru_cache(maxsize=512)
 def template(spec: str) -> _Template:
+    """the spec's template under the current plan switches (rt.plan_knobs: the templates' plan caches
+    are made under them)"""
+    return _template(spec, rt.plan_knobs())
+
+
+@functools.lru_cache(maxsize=512)
+def _template(spec: str, knobs) -> _Template:
     return _Template(spec)
 
 

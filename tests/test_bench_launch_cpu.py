@@ -50,11 +50,12 @@ def test_weak_scaling_plan():
     assert line["global_batch"] == 128 and line["per_gpu_batch"] == [64, 64]
 
 
-@pytest.mark.parametrize("workload,per", [("gen64", 256), ("fgan128", 512), ("fgan128sn", 1024)])
-def test_weak_scaling_is_default(workload, per):
-    """the default N-GPU line runs the configuration's batch on every GPU (weak scaling)"""
+@pytest.mark.parametrize("workload,gb", [("gen64", 256), ("fgan128", 512), ("fgan128sn", 1024)])
+def test_strong_scaling_is_default(workload, gb):
+    """the default N-GPU line splits the configuration's batch over the GPUs (BASELINE configs[3]/[4]:
+    "batch 512 / 1024 sharded across 8xMI355X")"""
     line = _line(_bench("--gpus", "2", "--dry-run", "--workload", workload))
-    assert line["scaling"] == "weak" and line["per_gpu_batch"] == [per, per] and line["global_batch"] == 2 * per
+    assert line["scaling"] == "strong" and line["per_gpu_batch"] == [gb // 2, gb // 2] and line["global_batch"] == gb
     assert line["tiles_global_batch"]
 
 

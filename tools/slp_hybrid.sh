@@ -2,13 +2,17 @@
 # Bisect a flag-dependent miscompare by source file: compile every csrc file of git revision <rev>
 # twice (default flags / the variant flags), then link one library per file group with only that
 # group built with the variant flags.
-# usage: VARIANT_FLAGS=-fno-slp-vectorize tools/slp_hybrid.sh <rev> <tag> "<group name>:<file> <file>" ...
+# usage: VARIANT_FLAGS=-fno-slp-vectorize tools/slp_hybrid.sh <rev | source dir> <tag> "<group name>:<file> <file>" ...
 #   -> fastfourierconvolution_amd/libffc_amd_<tag>_<group>.so, plus <tag>_all (every file) and <tag>_none
 set -eu
 rev=$1; tag=$2; shift 2
 root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
-git -C "$root" archive "$rev" fastfourierconvolution_amd/csrc include | tar -x -C "$tmp"
+if [ -d "$rev" ]; then   # a source tree (fastfourierconvolution_amd/csrc + include) instead of a revision
+  mkdir -p "$tmp/fastfourierconvolution_amd" && cp -r "$rev/fastfourierconvolution_amd/csrc" "$tmp/fastfourierconvolution_amd/" && cp -r "$rev/include" "$tmp/"
+else
+  git -C "$root" archive "$rev" fastfourierconvolution_amd/csrc include | tar -x -C "$tmp"
+fi
 src="$tmp/fastfourierconvolution_amd/csrc"
 mkdir -p "$tmp/a" "$tmp/b"
 pids=()
