@@ -40,10 +40,6 @@
 namespace {
 
 constexpr int QTHREADS = 512;   // 4 compute waves + 4 staging waves
-#ifndef FFC_CONVQ_PRIO
-#define FFC_CONVQ_PRIO 0   // static wave priority (A/B): 1 staging waves, 2 compute waves; both within
-                           // +-0.5 % of none on gen64 / fgan128 (profiles/r03/s2e)
-#endif
 #ifndef FFC_CONVQ_SLOTS
 #define FFC_CONVQ_SLOTS 2
 #endif
@@ -57,8 +53,6 @@ struct ConvQArgs {
     int ksplit;                // K splits per output tile (1: no split)
     float* part;               // ksplit > 1: per (slot, split, wave) fragment partial sums
     int ntiles;                // rows of the tile table (the grid may be smaller: persistent workgroups)
-    int epi_off;               // >= 0: byte offset of the epilogue hand-off area (the staging waves run the
-                               // epilogue of the previous tile); -1: the compute waves run it themselves
 };
 
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -216,42 +210,11 @@ __device__ __forceinline__ void convq_epilogue(const ffc_convp_job& J, int wave,
     if constexpr (MT > 1) epilogue(acc[1], m0 + 32 + 4 * h);
 }
 
-// Staging wave 4 + w: the epilogue of phase w of tile tix from the accumulators compute wave w left in
-// the hand-off area (the same fragment layout as store_partial)
-template <int MT, int NTW>
-__device__ __forceinline__ void epilogue_from_lds(const ConvQArgs& args, char* lds, int tix) {
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 3);
-    const int4 tile = args.tiles[tix];
-    const int ji = __builtin_amdgcn_readfirstlane(tile.x);
-    const int m0 = __builtin_amdgcn_readfirstlane(tile.y);
-    const int pb = __builtin_amdgcn_readfirstlane(tile.z);
-    const float* src = reinterpret_cast<const float*>(lds + args.epi_off) + (size_t)w * (MT * NTW * 1024);
-    floatx16 acc[MT][NTW];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt)
-#pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-                const floatx4 v = *reinterpret_cast<const floatx4*>(src + ((mt * NTW + nt) * 4 + r4) * 256 + lane * 4);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[mt][nt][4 * r4 + e] = v[e];
-            }
-    convq_epilogue<MT, NTW>(args.jobs[ji], w, lane, pb, m0, acc);
-}
-
-// The accumulators of compute wave w, MT x NTW x 4 floatx4 rows of 64 lanes, in the hand-off area
-__device__ __forceinline__ float* epi_slot(const ConvQArgs& args, char* lds, int w, int frag_floats) {
-    return reinterpret_cast<float*>(lds + args.epi_off) + (size_t)w * frag_floats;
-}
-
 // One output tile (one row of the tile table) of one workgroup; returns when the tile is done (the
-// staging waves after their last barrier of the tile, the compute waves after the epilogue or the
-// hand-off of their accumulators).  Every wave of the workgroup runs the same tiles, so the barrier
-// counts match tile by tile.  pend (staging waves): the tile whose epilogue they still owe.
+// staging waves after their last barrier of the tile, the compute waves after the epilogue).  Every
+// wave of the workgroup runs the same tiles, so the barrier counts match tile by tile.
 template <int MT, int NTW>
-__device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix, char* lds, int& pend) {
+__device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix, char* lds) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave_id = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stager = wave_id >= 4;
@@ -503,12 +466,6 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             for (int u = 0; u < QSLOTS; ++u) issue(sv[u], wbs[u], msk[u]);
             store_timed(sv[0], wbs[0], msk[0], lds);
             bar();
-            // the previous tile's epilogue (its accumulators were handed over in LDS before this barrier):
-            // the staging wave of phase w stores phase w's outputs while the compute waves run this tile
-            if (pend >= 0) {
-                epilogue_from_lds<MT, NTW>(args, lds, pend);
-                pend = -1;
-            }
             // periods 1 .. npad (nst rounded up to whole QSLOTS-period rounds: no exit in the middle of the
             // unrolled body, so every path into the loop head has the same loads in flight); periods past
             // nst issue nothing live, store nothing and only meet the compute waves' padding barriers
@@ -543,7 +500,6 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
                 tr[14] = qi;
             }
 #endif
-            pend = args.epi_off >= 0 && nsplit == 1 ? tix : -1;   // handed over at the next barrier
             return;   // no barrier follows
         }
         // A of the current chunk, refilled tap by tap with the next chunk's right after the tap's
@@ -696,11 +652,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
 #ifdef FFC_TRACE_Q
     QSTAMP(tq_d);
 #endif
-    if (args.epi_off >= 0) {   // hand the accumulators to the staging waves (they store at the next barrier)
-        store_partial<MT, NTW>(epi_slot(args, lds, wave, MT * NTW * 1024), lane, acc);
-    } else {
-        convq_epilogue<MT, NTW>(J, wave, lane, pb, m0, acc);
-    }
+    convq_epilogue<MT, NTW>(J, wave, lane, pb, m0, acc);
 #ifdef FFC_TRACE_Q
     {
         unsigned long long tq_e;
@@ -734,17 +686,7 @@ __global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
     const ConvQArgs& args = args_byval;
 #endif
     extern __shared__ __attribute__((aligned(16))) char lds[];
-#if FFC_CONVQ_PRIO == 1
-    if ((threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);   // staging waves win VALU arbitration
-#elif FFC_CONVQ_PRIO == 2
-    if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(1);    // compute waves win it
-#endif
-    int pend = -1;   // staging waves: the tile whose epilogue is still in the hand-off area
-    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW>(args, tix, lds, pend);
-    if (args.epi_off >= 0) {
-        __syncthreads();   // the last tile's accumulators are in LDS
-        if (pend >= 0) epilogue_from_lds<MT, NTW>(args, lds, pend);
-    }
+    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW>(args, tix, lds);
 }
 
 // K split, second pass: workgroup = one output tile (slot), wave w = phase w; adds the ksplit
@@ -979,24 +921,6 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
     }
     const size_t ebuf = ((size_t)npix_max * 96 + 255) / 256 * 256 + 256;   // + 256 B: buffers start on other banks
     size_t lds = npix_max > 0 ? 2 * ebuf : 16;
-    // FFC_CONVQ_EPI=1: the epilogue hand-off area (4 compute waves x MT x NTW fragments) behind the patch
-    // buffers, the staging waves store the previous tile's outputs.  Off by default: measured neutral
-    // to 1 % slower (gen64 0.473 vs 0.478-0.484 ms, fgan128 16.06 vs 16.11 ms, gpurun_out r03s) -- the
-    // staging waves are as close to the critical path as the compute waves' epilogue was
-    int epi_off = -1;
-    {
-        static const bool epi_on = [] {
-            const char* e = getenv("FFC_CONVQ_EPI");
-            return e && e[0] == '1';
-        }();
-        int MTc = 0, NTWc = 0;
-        ffc_convq_config(cfg, &MTc, &NTWc);
-        const size_t epi = (size_t)4 * MTc * NTWc * 1024 * sizeof(float);
-        if (epi_on && ksplit == 1 && npix_max > 0 && lds + epi <= 160 * 1024) {
-            epi_off = (int)lds;
-            lds += epi;
-        }
-    }
     FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_convq_forward: patch too large");
     ConvQArgs a;
     a.ebuf = (int)ebuf;
@@ -1006,7 +930,6 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
     a.ksplit = ksplit;
     a.part = part;
     a.ntiles = ntiles;
-    a.epi_off = epi_off;
     const int4* sl = reinterpret_cast<const int4*>(slot_tiles);
     hipStream_t s = (hipStream_t)stream;
     switch (cfg) {

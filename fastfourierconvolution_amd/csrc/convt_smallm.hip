@@ -621,10 +621,6 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0 && (reinterpret_cast<uintptr_t>(wpack) & 15) == 0,
                   "ffc_convt_k4s2_smallm: output / packed weights not 16-B aligned");
     FFC_CHECK_ARG(C0 + (x1 ? C1 : 0) <= CT_CMAX, "ffc_convt_k4s2_smallm: at most 256 input channels");
-    {
-        const int rc = ffc::smallm_mfma_convt(x0, C0, x1, C1, wpack, bias, B, IH, IW, M, out, act, act_param, stream);
-        if (rc != 1) return rc;
-    }
     SmallMArgs a;
     a.x[0] = x0;
     a.w[0] = nullptr;
@@ -722,11 +718,6 @@ static int conv3x3_smallm_launch(const float* x0, int C0, const float* w0, const
         FFC_CHECK_ARG(!t || !t->noise || (reinterpret_cast<uintptr_t>(t->noise) & 15) == 0,
                       "ffc_conv3x3_smallm_tf: noise not 16-B aligned");
         a.tf[s] = t ? *t : none;
-    }
-    {
-        const int rc = ffc::smallm_mfma_conv3(x0, C0, w0, x1, C1, w1, bias, B, H, W, M, out, act, act_param,
-                                              tfs[0], tfs[1], stream);
-        if (rc != 1) return rc;
     }
     const int nchunks = C0 + (x1 ? C1 : 0);
     const size_t lds = head3_lds_bytes(tr, nchunks);

@@ -113,14 +113,6 @@ int launch_status(const char* what);  // FFC_OK or FFC_E_LAUNCH after checking h
 int fft_planes_r2c(const float* x, int P, int H, int W, float iscale, float* Z, void* stream);
 int fft_planes_c2r(const float* Z, int P, int H, int W, float iscale, const float* addend, float* y, void* stream);
 
-// small-M convolutions on the MFMA (smallm_mfma.hip); 1 = shape not handled there (the VALU kernels of
-// convt_smallm.hip run), else FFC_OK or an error code.  Off unless FFC_SMALLM_MFMA=1 (measured slower).
-int smallm_mfma_conv3(const float* x0, int C0, const float* w0, const float* x1, int C1, const float* w1,
-                      const float* bias, int B, int H, int W, int M, float* out, int act, float act_param,
-                      const ffc_in_tf* tf0, const ffc_in_tf* tf1, void* stream);
-int smallm_mfma_convt(const float* x0, int C0, const float* x1, int C1, const float* wpack, const float* bias,
-                      int B, int IH, int IW, int M, float* out, int act, float act_param, void* stream);
-
 #define FFC_CHECK_ARG(cond, msg)              \
     do {                                      \
         if (!(cond)) {                        \

@@ -146,30 +146,3 @@ def test_c2r_packed_dc_nyquist_columns(H):
     ref = np.fft.irfftn(Y, s=(H, W)) * H * W
     np.testing.assert_allclose(rows, ref, rtol=0, atol=1e-9 * np.abs(ref).max())
 
-
-@pytest.mark.parametrize("H", [64, 128])
-def test_c2r_parity_fold(H):
-    """fu2d_c2r_fold_kernel: part p of a plane computes output rows 2r + p from the folded half plane
-    E[k] = Y[k] + Y[k + H/2] (p = 0) or O[k] = (Y[k] - Y[k + H/2]) e^{+2 pi i k/H} (p = 1), each with
-    length-H/2 column IFFTs, the packed DC / Nyquist column on the folded columns and the row C2R --
-    numpy emulation of the kernel's index and twiddle arithmetic against irfftn(Y, s=(H, W))"""
-    W = H
-    HH = H // 2
-    rng = np.random.default_rng(7 * H)
-    Y = rng.standard_normal((H, W // 2 + 1)) + 1j * rng.standard_normal((H, W // 2 + 1))
-    # the kernel's twiddle: c_twc / c_tws[r * (128 / H)] = cos / sin(2 pi r / H)
-    tw = np.cos(2 * np.pi * np.arange(HH) / H) + 1j * np.sin(2 * np.pi * np.arange(HH) / H)
-    out = np.empty((H, W))
-    for part in (0, 1):
-        F = Y[:HH] + Y[HH:] if part == 0 else (Y[:HH] - Y[HH:]) * tw[:, None]
-        cols = np.fft.ifft(F, axis=0) * HH
-        a, b = F[:, 0], F[:, W // 2]
-        neg = (-np.arange(HH)) % HH
-        zc = np.fft.ifft(0.5 * (a + np.conj(a[neg])) + 1j * 0.5 * (b + np.conj(b[neg]))) * HH
-        cols[:, 0] = zc.real
-        cols[:, W // 2] = zc.imag
-        edge = np.arange(W // 2 + 1) % (W // 2) == 0
-        rows = np.fft.irfft(np.where(edge, cols.real, cols), n=W, axis=1) * W
-        out[part::2] = rows
-    ref = np.fft.irfftn(Y, s=(H, W)) * H * W
-    np.testing.assert_allclose(out, ref, rtol=0, atol=1e-9 * np.abs(ref).max())

@@ -245,10 +245,9 @@ def test_smallm_convt_vs_oracle(M, H, W, bias):
 
 @pytest.mark.parametrize("cin,M,H,W,bias", [(64, 3, 32, 32, False), (64, 1, 32, 32, True), (32, 4, 12, 20, True),
                                               (16, 3, 8, 36, False), (128, 2, 16, 48, False)])
-def test_smallm_convt_mfma_vs_oracle(cin, M, H, W, bias):
-    """ConvT k4 s2 p1 with M <= 4 at shapes the MFMA small-M kernel takes (both segments a multiple of 8
-    channels, W even; smallm_mfma.hip, used under FFC_SMALLM_MFMA=1, see the subprocess test below) --
-    the FFC-DCGAN generator's last layer (models/ffc_generator.py:28) and ragged 8 x 32 tiles"""
+def test_smallm_convt_vs_oracle(cin, M, H, W, bias):
+    """ConvT k4 s2 p1 with M <= 4 on the direct small-M kernel (convt_smallm.hip) -- the FFC-DCGAN
+    generator's last layer (models/ffc_generator.py:28) and ragged 8 x 32 tiles"""
     import fastfourierconvolution_amd as F
     from oracle.ffc_oracle import ffc_bn_act
     cfg = dict(in_channels=cin, out_channels=M, kernel_size=4, ratio_gin=0.5, ratio_gout=0.0, stride=2, padding=1,
@@ -371,18 +370,3 @@ def test_pointwise_conv_kernels(B, C, M, H, patch):
         rt.USE_PATCH = old
     assert normwise_err(out.cpu(), ref.cpu()) <= TOL
 
-
-def test_smallm_mfma_kernels_in_subprocess():
-    """the MFMA small-M kernels (smallm_mfma.hip, off by default: measured slower than the VALU
-    kernels) still match the oracle: the ConvT and deferred-head parity tests rerun in a child
-    process with FFC_SMALLM_MFMA=1"""
-    import os
-    import subprocess
-    import sys
-    env = dict(os.environ, FFC_SMALLM_MFMA="1")
-    here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
-                        os.path.join(here, "test_gpu_parity.py") + "::test_smallm_convt_mfma_vs_oracle",
-                        os.path.join(here, "test_gpu_defer.py") + "::test_conv3x3_smallm_tf_ragged"],
-                       env=env, capture_output=True, text=True, timeout=240, cwd=os.path.dirname(here))
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
