@@ -459,7 +459,7 @@ def plan_knobs():
     """the module-level switches plans depend on (tests and A/B runs flip them): part of every plan
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
-            FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL)
+            FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH)
 
 
 def algorithmic_flops(plan) -> float:
@@ -511,6 +511,9 @@ CONVQ_FORCE = __import__("os").environ.get("FFC_CONVQ", "auto") in ("1", "force"
 USE_OUTER = True   # ConvT on a 1x1 input as one outer-product GEMM (ffc._FFCExec._outer_rewrite)
 USE_SMALLM = True  # direct VALU ConvT for <= 4 output channels (ffc_convt_k4s2_smallm)
 FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU applies (tests)
+# SpectralTransform prologue: "auto" = the fused per-sample kernel where the sample fits in LDS
+# (st_prologue.hip), else SE gate + gated 1x1 GEMM (st_pw.hip); "pw" forces the latter (A/B runs)
+ST_PATH = __import__("os").environ.get("FFC_ST_PATH", "auto")
 # Fourier-unit path where both apply: the fused one-workgroup-per-sample kernel fills the chip only
 # with B >= ~CUs/2 samples; smaller batches (fgan128's 64-sample shards) run the staged kernels,
 # which spread every sample over many workgroups.  "auto" | "fused" | "staged"

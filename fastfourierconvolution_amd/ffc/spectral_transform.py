@@ -121,7 +121,7 @@ class SpectralTransform(nn.Module):
         L = rt.lib()
         hid = self.se_block.fc[0].out_features
         t = torch.empty((B, c, h2, w2), device=dev, dtype=torch.float32)
-        if L.ffc_st_prologue_lds_bytes(Cin, H, W, int(pool), hid, c) > 0:
+        if rt.ST_PATH != "pw" and L.ffc_st_prologue_lds_bytes(Cin, H, W, int(pool), hid, c) > 0:
             # one fused launch: [pool] -> SE gate -> conv1 -> per-sample BN1 partials
             se1 = rt.require(self.se_block.fc[0].weight.detach(), "se.fc.0.weight") if hid > 0 else None
             se2 = rt.require(self.se_block.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None

@@ -370,3 +370,34 @@ def test_pointwise_conv_kernels(B, C, M, H, patch):
         rt.USE_PATCH = old
     assert normwise_err(out.cpu(), ref.cpu()) <= TOL
 
+
+
+def test_conv3x3_nonfinite_input_halo():
+    """Non-finite inputs: a 3x3 stride-1 conv runs as 4x4 taps whose 4th row / column has
+    zero weights but reads the real pixel one past the window (_plan.plan_patch_job), and the split-bf16
+    products turn an Inf operand into NaN pieces.  So an Inf input pixel P makes every output whose
+    padded 4x4 window holds P non-finite -- one row and one column more than the reference's 3x3
+    halo -- and leaves every other output finite and equal to the reference."""
+    import fastfourierconvolution_amd as F
+    from oracle.ffc_oracle import ffc_bn_act
+    cfg = dict(in_channels=16, out_channels=16, kernel_size=3, ratio_gin=0.0, ratio_gout=0.0, stride=1, padding=1,
+               norm_layer="Identity", activation_layer="Identity")
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = F.FFC_BN_ACT(16, 16, 3, 0.0, 0.0, 1, 1)
+    sd = {k: v.double() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 16, 32, 32, generator=torch.Generator().manual_seed(5))
+    y0, x0 = 9, 20
+    x[1, 3, y0, x0] = float("inf")
+    with torch.no_grad():
+        out = m.cuda().eval()(x.cuda())[0].cpu()
+    ref = ffc_bn_act(x.double(), sd, "", cfg, False)[0]
+    pad = torch.zeros(32, 32, dtype=torch.bool)
+    pad[max(0, y0 - 2):y0 + 2, max(0, x0 - 2):x0 + 2] = True     # outputs y, x with P in rows y-1..y+2, cols x-1..x+2
+    halo = torch.zeros(32, 32, dtype=torch.bool)
+    halo[y0 - 1:y0 + 2, x0 - 1:x0 + 2] = True                     # the reference's 3x3 halo
+    assert not torch.isfinite(ref[1][:, halo]).any() and torch.isfinite(ref[1][:, ~halo]).all()
+    assert not torch.isfinite(out[1][:, pad]).any()
+    ok = torch.ones_like(out, dtype=torch.bool)
+    ok[1][:, pad] = False
+    assert torch.isfinite(out[ok]).all()
+    assert normwise_err(torch.where(ok, out, torch.zeros_like(out)), torch.where(ok, ref, torch.zeros_like(ref))) <= TOL
