@@ -426,7 +426,8 @@ def convq_strides(NS, TR, TC, PR, PC, pad=True):
 
 
 def convq_lds_bytes(NS, strides):
-    return 2 * (((max(NS * qs for _, qs in strides) * 96 + 255) // 256) * 256 + 256)
+    """three chunk buffers (csrc/convq_kernels.hip convq_tile)"""
+    return 3 * (((max(NS * qs for _, qs in strides) * 96 + 255) // 256) * 256 + 256)
 
 
 def plan_convq_job(B: int, M: int, segs, cfg: int):
@@ -486,6 +487,10 @@ def plan_convq_job(B: int, M: int, segs, cfg: int):
     if os.environ.get("FFC_CONVQ_PAD") == "0":
         pad = False
     qstride = [convq_strides(NS, TR, TC, PR, PC, pad) for (PR, PC) in prc]
+    if staged and convq_lds_bytes(NS, [qstride[si] for si in range(len(segs)) if not direct[si]]) > 160 * 1024:
+        return None
+    if any(not direct[si] and B * sg.C * sg.IH * sg.IW * 4 >= 0x7FFFFFFF for si, sg in enumerate(segs)):
+        return None                        # staged through 32-bit buffer offsets
     phases, ktab, taptab = [], [], []
     a_total = 0
     Mpad = -(-M // MPAD) * MPAD

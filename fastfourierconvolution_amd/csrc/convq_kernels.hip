@@ -40,6 +40,9 @@
 namespace {
 
 constexpr int QTHREADS = 512;   // 4 compute waves + 4 staging waves
+#ifndef FFC_CONVQ_WPE
+#define FFC_CONVQ_WPE
+#endif
 #ifndef FFC_CONVQ_SLOTS
 #define FFC_CONVQ_SLOTS 2
 #endif
@@ -240,20 +243,8 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
     const int TRC = TR * TC;
     const int nseg = J.nseg;
 
-    // this lane's pixel of each N-tile (phase-grid coordinates inside the block)
-    int pns[NTW], pr_[NTW], pc_[NTW];
-    bool pv[NTW];
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-        const int q = nt * 32 + cl;
-        const int ns = q / TRC;
-        const int rem = q - ns * TRC;
-        const int r = rem / TC, c = rem - r * TC;
-        pns[nt] = ns;
-        pr_[nt] = r;
-        pc_[nt] = c;
-        pv[nt] = ns < NS && b0 + ns < J.B && r0 + r < P.PH && c0 + c < P.PW;
-    }
+    // this lane's pixel of each N-tile (q_geometry) is recomputed where it is needed (a segment
+    // change, the direct segments, the epilogue) rather than held in registers through the K loop
 
     floatx16 acc[MT][NTW];
 #pragma unroll
@@ -289,24 +280,31 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
     // stored at image column 4 g + e.  Image pixel (ns, row, col) of channel half h sits at
     // 48 * ((h * NS + ns) * qsample + row * qrow + col) bytes; the lane pixel (pc) of the compute
     // side is image column pc * mult_x + xoff, xoff = ix0 - xa.
+    // The loads go through a buffer descriptor of the segment (ffc::buf_rsrc): a lane's byte offset of
+    // its unit (sample, pixel group, channel half) is fixed for the whole segment and the chunk's
+    // channel offsets are wave-uniform (SGPR soffset), so a chunk's 8 loads need no per-lane address
+    // arithmetic; units outside the batch / input / unit range load at offset OOB and read zeros
+    // (no select at store time), and the per-chunk state lives in registers (a kernel-argument load
+    // per chunk made the wave wait for its own LDS stores: s_waitcnt lgkmcnt(0) covers both).
     struct {
-        const float* x;
-        long long sstride;         // floats per sample (C * IH * IW)
-        int C, IHW, nunits;
-        int sb;                    // sample of the unit (-1: outside the batch / input / unit range)
-        int off;                   // in-sample offset of channel 0 at the group's first pixel
-        int hu;                    // the unit's channel half
+        __amdgpu_buffer_rsrc_t rs;
+        unsigned voff;             // byte offset of the unit's first channel at its group's first pixel (OOB: none)
+        unsigned cstride;          // bytes per channel plane
+        int C, Cpad, cfull;        // cfull: C % 16 == 0 (every channel of every chunk exists)
+        int hu8;                   // 8 * the unit's channel half
         int wb;                    // LDS byte offset of the group's first pixel inside a buffer (-1: none)
     } st;
     auto stage_setup = [&](int s) {
         const ffc_convp_seg& S = J.seg[s];
-        st.x = S.x;
+        const int IHW = S.IH * S.IW;
+        st.rs = ffc::buf_rsrc(S.x, (unsigned long long)J.B * S.C * IHW * 4);
         st.C = S.C;
-        st.IHW = S.IH * S.IW;
-        st.sstride = (long long)S.C * st.IHW;
+        st.Cpad = S.Cpad;
+        st.cfull = (S.C & 15) == 0;
+        st.cstride = (unsigned)IHW * 4u;
         const int PR = S.PR, G = S.PC >> 2, QR = S.qrow, QS = S.qsample;
         const int ngrp = NS * PR * G;
-        st.nunits = 2 * ngrp;
+        const int nunits = 2 * ngrp;
         const int iy0 = r0 * S.mult_y + S.org_y;
         const int xa = (c0 * S.mult_x + S.org_x) & ~3;
         const int n = stid;
@@ -315,38 +313,27 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
         const int g = q % G, q1 = q / G;
         const int pr = q1 % PR, ns = q1 / PR;
         const int b = b0 + ns, iy = iy0 + pr, ix = xa + 4 * g;
-        const bool ok = n < st.nunits && b < J.B && (unsigned)iy < (unsigned)S.IH && (unsigned)ix < (unsigned)S.IW;
-        st.sb = ok ? b : -1;
-        st.off = iy * S.IW + ix;
-        st.hu = hu;
-        st.wb = n < st.nunits ? ((hu * NS + ns) * QS + pr * QR + 4 * g) * 48 : -1;
+        const bool ok = n < nunits && b < J.B && (unsigned)iy < (unsigned)S.IH && (unsigned)ix < (unsigned)S.IW;
+        st.voff = ok ? (unsigned)(((b * S.C + 8 * hu) * IHW + iy * S.IW + ix) * 4) : ffc::OOB;
+        st.hu8 = 8 * hu;
+        st.wb = n < nunits ? ((hu * NS + ns) * QS + pr * QR + 4 * g) * 48 : -1;
     };
-    // Every lane loads from a valid address (out-of-range units read the segment base) and the zero
-    // select happens at store time, on the returned lane mask: a select right behind the loads made
-    // the compiler wait for them at issue (s_waitcnt vmcnt), and conditional addresses compiled to
-    // divergent branches that reused the load registers (more waits) -- together they serialised the
-    // staging pipeline (r03 trace: "issue" 4.6k cycles per chunk on gen64 layer 0).
-    auto stage_load = [&](floatx4 (&sv)[8], int ch0) -> int {
-        const int cb = ch0 + 8 * st.hu;
-        const bool inb = st.sb >= 0;
-        const long long base = (long long)(inb ? st.sb : 0) * st.sstride + (inb ? st.off : 0);
-        int mask = 0;
+    auto stage_load = [&](floatx4 (&sv)[8], int ch0) {
+        const unsigned sbase = (unsigned)ch0 * st.cstride;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const bool ok = inb && cb + j < st.C;
-            mask |= ok ? (1 << j) : 0;
-            const long long o = base + (long long)(ok ? cb + j : 0) * st.IHW;
-            sv[j] = *reinterpret_cast<const floatx4*>(st.x + o);
+            const unsigned vo = (st.cfull || ch0 + st.hu8 + j < st.C) ? st.voff : ffc::OOB;
+            sv[j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     st.rs, (int)vo, (int)(sbase + (unsigned)j * st.cstride), 0));
         }
-        return mask;
     };
-    auto stage_store = [&](const floatx4 (&sv)[8], int wb, int mask, char* buf) {
+    auto stage_store = [&](const floatx4 (&sv)[8], int wb, char* buf) {
         if (wb >= 0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float v8[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v8[j] = (mask >> j) & 1 ? sv[j][e] : 0.0f;
+                for (int j = 0; j < 8; ++j) v8[j] = sv[j][e];
                 const Split3 sp = split3(v8);
                 u32x4* d = reinterpret_cast<u32x4*>(buf + wb + 48 * e);
                 d[0] = __builtin_bit_cast(u32x4, sp.hi);
@@ -358,22 +345,27 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
 
     // per-segment compute geometry: LDS byte offset of the lane's B fragment per (N-tile, tap);
     // staged segments always run 4 taps (the plan pads missing ones with zero weights)
-    int kseg = 0;
+    int kseg = 0, cpad = 0;
     int fb[NTW];        // per N-tile: byte offset of (h, lane pixel) inside a buffer
     int tb[4];          // per tap: byte offset of the tap's pixel shift
-    auto compute_setup = [&](int s) {
+    auto geom = [&](int s, int (&fbo)[NTW], int (&tbo)[4]) {
         const ffc_convp_seg& S = J.seg[s];
-        kseg = P.kseg[s];
+        const QGeom<NTW> g = q_geometry<NTW>(J, wave, lane, pb);
         const int QR = S.qrow, QS = S.qsample, nimg = NS * QS;
         const int ix0 = c0 * S.mult_x + S.org_x, xoff = ix0 - (ix0 & ~3);
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt)
-            fb[nt] = (h * nimg + pns[nt] * QS + pr_[nt] * S.mult_y * QR + pc_[nt] * S.mult_x + xoff) * 48;
+            fbo[nt] = (h * nimg + g.pns[nt] * QS + g.pr_[nt] * S.mult_y * QR + g.pc_[nt] * S.mult_x + xoff) * 48;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const int tt = P.tap[s][t];
-            tb[t] = ((tt >> 16) * QR + (tt & 0xFFFF)) * 48;
+            tbo[t] = ((tt >> 16) * QR + (tt & 0xFFFF)) * 48;
         }
+    };
+    auto compute_setup = [&](int s) {
+        kseg = P.kseg[s];
+        cpad = J.seg[s].Cpad;
+        geom(s, fb, tb);
     };
 
     // K = the staged segments' 16-channel chunks (in job order), then the direct segments' chunks;
@@ -398,53 +390,51 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             do { ++ss; } while (J.seg[ss].direct);
         }
         int cs = ss, sch = 16 * c0k, cch = 16 * c0k;   // stager / computer: segment and channel of their chunk
-        auto advance_stager = [&]() {
-            if (sch >= J.seg[ss].Cpad) {
-                do { ++ss; } while (ss < nseg && J.seg[ss].direct);
-                sch = 0;
-                if (ss < nseg) stage_setup(ss);
-            }
-        };
-        // two loops with the same barrier count: the staging and compute waves' registers are then
-        // disjoint live ranges (one loop with role branches inside keeps both sets alive)
+        // Three LDS buffers: chunk k is stored into buffer k % 3 two barrier periods before the compute
+        // waves finish chunk k - 1, so during chunk k - 1 both buffers k - 1 and k are complete and the
+        // compute waves read chunk k's first tap before the barrier (its LDS latency then sits under
+        // the last tap's MFMAs instead of at the head of every chunk).  Barrier B0 follows the
+        // staging of chunks 0 and 1; period c (1 .. npad) stores chunk c + 1 and ends with barrier Bc;
+        // the compute waves run chunk ci between B(ci) and B(ci + 1).
         if (stager) {
-            // two register slots: the loads of chunk c + 2 are in flight while chunk c + 1 is split and
-            // stored, so a chunk's load latency overlaps a whole chunk period of MFMAs
 #ifdef FFC_TRACE_Q
             unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0, qi = 0;
             QSTAMP(q0);
 #endif
             floatx4 sv[QSLOTS][8];
-            int wbs[QSLOTS], msk[QSLOTS];
+            int wbs[QSLOTS];
             stage_setup(ss);
             // the chunk at the load cursor (ss, sch); past the last chunk the loads still issue (the
-            // previous addresses, mask 0, no store): every period then has the same load / wait
-            // pattern, so the compiler's wait counts stay exact (a conditional issue made it wait for
-            // every outstanding load at the loop head, serialising the pipeline)
+            // previous addresses, no store): every period then has the same load / wait pattern, so
+            // the compiler's wait counts stay exact (a conditional issue made it wait for every
+            // outstanding load at the loop head, serialising the pipeline)
             int ic = 0;   // chunks issued (this workgroup's K range is chunks 0 .. nst - 1)
-            auto issue = [&](floatx4 (&dst)[8], int& wb, int& mask) {
+            auto issue = [&](floatx4 (&dst)[8], int& wb) {
                 const bool live = ss < nseg && ic < nst;
                 ++ic;
-                mask = stage_load(dst, live ? sch : 0);
-                mask = live ? mask : 0;
+                stage_load(dst, live ? sch : 0);
                 wb = live ? st.wb : -1;
                 if (live) {
                     sch += 16;
-                    advance_stager();
+                    if (sch >= st.Cpad) {   // next staged segment (kernel-argument loads only here)
+                        do { ++ss; } while (ss < nseg && J.seg[ss].direct);
+                        sch = 0;
+                        if (ss < nseg) stage_setup(ss);
+                    }
                 }
             };
-            auto store_timed = [&](const floatx4 (&src)[8], int wb, int mask, char* buf) {
+            auto store_timed = [&](const floatx4 (&src)[8], int wb, char* buf) {
 #ifdef FFC_TRACE_Q
                 QSTAMP(qa);
                 float chk = src[0][0] + src[7][3];
                 asm volatile("" ::"v"(chk));   // data arrived
                 QSTAMP(qb);
                 ql += qb - qa;
-                stage_store(src, wb, mask, buf);
+                stage_store(src, wb, buf);
                 QSTAMP(qa);
                 qs += qa - qb;
 #else
-                stage_store(src, wb, mask, buf);
+                stage_store(src, wb, buf);
 #endif
             };
             auto bar = [&]() {
@@ -452,39 +442,42 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
                 QSTAMP(qa);
 #endif
 #ifndef FFC_QPROBE_NOBAR
-                __syncthreads();   // next buffer written; everyone done reading the other
+                __syncthreads();   // chunk c + 1 written; everyone done reading chunk c - 1's buffer
 #endif
 #ifdef FFC_TRACE_Q
                 QSTAMP(qb);
                 qw += qb - qa;
 #endif
             };
-            // QSLOTS register slots: chunks c + 1 .. c + QSLOTS - 1 are in flight while chunk c is split
-            // and stored (slot of chunk c = c % QSLOTS; the loop is unrolled by QSLOTS so every slot
-            // index is a compile-time constant)
+            // QSLOTS register slots (chunk k in slot k % QSLOTS; the loop is unrolled by QSLOTS so
+            // every slot index is a compile-time constant): the loads of chunks c + 2 .. c + QSLOTS are
+            // in flight while chunk c + 1 is split and stored
 #pragma unroll
-            for (int u = 0; u < QSLOTS; ++u) issue(sv[u], wbs[u], msk[u]);
-            store_timed(sv[0], wbs[0], msk[0], lds);
-            bar();
+            for (int u = 0; u < QSLOTS; ++u) issue(sv[u], wbs[u]);
+            store_timed(sv[0], wbs[0], lds);
+            issue(sv[0], wbs[0]);                                   // chunk QSLOTS
+            store_timed(sv[1 % QSLOTS], wbs[1 % QSLOTS], lds + ebuf);
+            bar();   // B0
+            int wbuf = 2;   // buffer of the chunk stored next (chunk c + 1 of period c)
             // periods 1 .. npad (nst rounded up to whole QSLOTS-period rounds: no exit in the middle of the
-            // unrolled body, so every path into the loop head has the same loads in flight); periods past
-            // nst issue nothing live, store nothing and only meet the compute waves' padding barriers
+            // unrolled body, so every path into the loop head has the same loads in flight); periods
+            // past the last chunk issue nothing live, store nothing and only meet the compute waves'
+            // barriers
             for (int c0 = 1; c0 <= npad; c0 += QSLOTS) {
 #pragma unroll
-                for (int u = 0; u < QSLOTS; ++u) {
-                    const int c = c0 + u;    // the chunk stored in this period (c % QSLOTS == (u + 1) % QSLOTS)
+                for (int u = 0; u < QSLOTS; ++u) {   // period c = c0 + u: c % QSLOTS == (1 + u) % QSLOTS
 #ifndef FFC_QPROBE_NOSTAGE
 #ifdef FFC_TRACE_Q
                     QSTAMP(qa);
 #endif
-                    issue(sv[u], wbs[u], msk[u]);   // chunk c + QSLOTS - 1 into slot u (it held chunk c - 1)
+                    issue(sv[(1 + u) % QSLOTS], wbs[(1 + u) % QSLOTS]);   // chunk c + QSLOTS
 #ifdef FFC_TRACE_Q
                     QSTAMP(qb);
                     qi += qb - qa;
 #endif
-                    store_timed(sv[(u + 1) % QSLOTS], wbs[(u + 1) % QSLOTS], msk[(u + 1) % QSLOTS],
-                                lds + (c & 1) * ebuf);   // chunk c (past the last chunk: wb = -1, no store)
+                    store_timed(sv[(2 + u) % QSLOTS], wbs[(2 + u) % QSLOTS], lds + wbuf * ebuf);   // chunk c + 1
 #endif
+                    wbuf = wbuf == 2 ? 0 : wbuf + 1;
                     bar();
                 }
             }
@@ -507,52 +500,69 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
         // ~1-2K cycles; loading taps 1-3 at the chunk start exposed it), in the same registers
         Split3 a[4][MT];
         compute_setup(cs);
+        int pf[NTW];   // byte offsets of the next chunk's tap-0 fragments (its segment's geometry)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) pf[nt] = fb[nt] + tb[0];
 #pragma unroll
         for (int t = 0; t < 4; ++t) load_A(kseg + cch * 4 + 16 * t, a[t]);
+        // B fragments of a whole tap (NTW x 3 ds_read_b128) one tap ahead of its MFMAs
+        u32x4 bq[2][NTW][3];
+        auto read_frag = [&](const char* base, const int (&off)[NTW], int add, u32x4 (&dst)[NTW][3]) {
+#pragma unroll
+            for (int nt = 0; nt < NTW; ++nt) {
+                const char* p1 = base + off[nt] + add;
+                dst[nt][0] = lds_read16(p1, 0);
+                dst[nt][1] = lds_read16(p1, 16);
+                dst[nt][2] = lds_read16(p1, 32);
+            }
+        };
 #ifdef FFC_TRACE_Q
         QSTAMP(tq_a);
 #endif
-        __syncthreads();
+        __syncthreads();   // B0: chunks 0 and 1 stored
 #ifdef FFC_TRACE_Q
         QSTAMP(tq_b);
         tq_bar += tq_b - tq_a;
 #endif
+        read_frag(lds, pf, 0, bq[0]);   // chunk 0, tap 0
+        int rbuf = 0;
         for (int ci = 0; ci < nst; ++ci) {
 #ifdef FFC_TRACE_Q
             QSTAMP(tq_a);
 #endif
             const bool more = ci + 1 < nst;
-            const char* cur = lds + (ci & 1) * ebuf;
-            // the computer's next chunk (segment cn, channel chn) for the A prefetch
+            const int nbuf = rbuf == 2 ? 0 : rbuf + 1;
+            const char* cur = lds + rbuf * ebuf;
+            const char* nxt = lds + nbuf * ebuf;
+            // the next chunk (segment cn, channel chn): its K base for the A refill and, on a segment
+            // change, its tap-0 fragment offsets for the prefetch (kernel-argument loads only then)
             int cn = cs, chn = cch + 16;
-            if (chn >= J.seg[cs].Cpad && more) {
+            const bool segchg = more && chn >= cpad;
+            int kn;
+            if (segchg) {
                 do { ++cn; } while (J.seg[cn].direct);
                 chn = 0;
+                kn = P.kseg[cn];
+                int fbn[NTW], tbn[4];
+                geom(cn, fbn, tbn);
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt) pf[nt] = fbn[nt] + tbn[0];
+            } else {
+                // the last chunk reloads its own A: no branch around the loads
+                kn = kseg + (more ? chn : cch) * 4;
             }
-            // K base of the next chunk (chunk-major, then tap, then channel); the last chunk reloads
-            // its own: no branch around the loads
-            const int kn = more ? P.kseg[cn] + chn * 4 : kseg + cch * 4;
             __builtin_amdgcn_sched_barrier(0);
 #ifdef FFC_TRACE_Q
             QSTAMP(tq_b);
             tq_A += tq_b - tq_a;
 #endif
-            // B fragments of a whole tap (NTW x 3 ds_read_b128) one tap ahead of its MFMAs
-            u32x4 bq[2][NTW][3];
-            auto read_tap = [&](int t, u32x4 (&dst)[NTW][3]) {
-#pragma unroll
-                for (int nt = 0; nt < NTW; ++nt) {
-                    const char* p1 = cur + fb[nt] + tb[t];
-                    dst[nt][0] = lds_read16(p1, 0);
-                    dst[nt][1] = lds_read16(p1, 16);
-                    dst[nt][2] = lds_read16(p1, 32);
-                }
-            };
 #ifndef FFC_QPROBE_NOMFMA
-            read_tap(0, bq[0]);
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                if (t + 1 < 4) read_tap(t + 1, bq[(t + 1) & 1]);
+                // tap t + 1's fragments, or the next chunk's tap 0 (read from the other complete
+                // buffer; past the last chunk a harmless read of data nobody uses)
+                if (t + 1 < 4) read_frag(cur, fb, tb[t + 1], bq[(t + 1) & 1]);
+                else read_frag(nxt, pf, 0, bq[0]);
 #pragma unroll
                 for (int nt = 0; nt < NTW; ++nt) {
                     Split3 b;
@@ -565,11 +575,11 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
 #ifndef FFC_QPROBE_NOA   // timing probe only: A of the first chunk reused
                 load_A(kn + 16 * t, a[t]);   // refill: the next chunk's tap t
 #endif
-                // keep the next tap's reads ahead of this tap's MFMAs (the scheduler otherwise sinks
-                // each read to just before its first use and waits on it), the refill after them
-                if (t + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTW, 0);   // DS_READ
-                __builtin_amdgcn_sched_group_barrier(0x8, 6 * NTW * MT, 0);                // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x20, 3 * MT, 0);                     // VMEM_READ
+                // keep the next reads ahead of this tap's MFMAs (the scheduler otherwise sinks each
+                // read to just before its first use and waits on it), the refill after them
+                __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTW, 0);   // DS_READ
+                __builtin_amdgcn_sched_group_barrier(0x8, 6 * NTW * MT, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x20, 3 * MT, 0);       // VMEM_READ
                 __builtin_amdgcn_sched_barrier(0);
             }
 #endif
@@ -577,17 +587,19 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             QSTAMP(tq_a);
             tq_mf += tq_a - tq_b;
 #endif
-            cch += 16;
-            if (cch >= J.seg[cs].Cpad && more) {
+            if (segchg) {
                 cs = cn;
                 cch = 0;
                 compute_setup(cs);
+            } else {
+                cch += 16;
             }
+            rbuf = nbuf;
 #ifdef FFC_TRACE_Q
             QSTAMP(tq_a);
 #endif
 #ifndef FFC_QPROBE_NOBAR
-            __syncthreads();   // next buffer written; everyone done reading this one
+            __syncthreads();   // chunk ci + 2 written; everyone done reading chunk ci
 #endif
 #ifdef FFC_TRACE_Q
             QSTAMP(tq_b);
@@ -613,11 +625,13 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
         dbase += nch;
         if (c_lo >= c_hi) continue;
         const int IHW = S.IH * S.IW;
+        const QGeom<NTW> g = q_geometry<NTW>(J, wave, lane, pb);
+        const bool* pv = g.pv;
         const float* xp[NTW];
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) {
-            const int oy = (r0 + pr_[nt]) * J.Sy + P.py, ox = (c0 + pc_[nt]) * J.Sx + P.px;
-            const int b = pv[nt] ? b0 + pns[nt] : 0;
+            const int oy = (r0 + g.pr_[nt]) * J.Sy + P.py, ox = (c0 + g.pc_[nt]) * J.Sx + P.px;
+            const int b = pv[nt] ? b0 + g.pns[nt] : 0;
             xp[nt] = S.x + ((long long)b * S.C + 8 * h) * IHW + (pv[nt] ? oy * S.IW + ox : 0);
         }
         for (int ch0 = 16 * c_lo; ch0 < 16 * c_hi; ch0 += 16) {
@@ -679,7 +693,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
 // A tile's epilogue stores drain while the staging waves already load and split the next tile's
 // first chunk, and the next tile's MFMAs start without a fresh workgroup launch.
 template <int MT, int NTW>
-__global__ __launch_bounds__(QTHREADS) void convq_kernel(ConvQArgs args_byval) {
+__global__ __launch_bounds__(QTHREADS) FFC_CONVQ_WPE void convq_kernel(ConvQArgs args_byval) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
 #else
@@ -912,6 +926,8 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
                               "ffc_convq_forward: patch shape / LDS strides");
                 FFC_CHECK_ARG(S.vec4 && S.IW % 4 == 0 && (reinterpret_cast<uintptr_t>(S.x) & 15) == 0,
                               "ffc_convq_forward: staged segments need IW % 4 == 0 and a 16-byte aligned input");
+                FFC_CHECK_ARG((unsigned long long)J.B * S.C * S.IH * S.IW * 4 < 0x7FFFFFFFull,
+                              "ffc_convq_forward: staged segments are read through 32-bit buffer offsets (< 2 GiB)");
                 FFC_CHECK_ARG(2 * J.NS * S.PR * (S.PC / 4) <= 256,
                               "ffc_convq_forward: patch too large for the staging waves (one unit per thread)");
                 const int npix = J.NS * S.qsample;   // LDS image pixels per channel half
@@ -920,7 +936,7 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
         }
     }
     const size_t ebuf = ((size_t)npix_max * 96 + 255) / 256 * 256 + 256;   // + 256 B: buffers start on other banks
-    size_t lds = npix_max > 0 ? 2 * ebuf : 16;
+    size_t lds = npix_max > 0 ? 3 * ebuf : 16;   // three chunk buffers (convq_tile)
     FFC_CHECK_ARG(lds <= 160 * 1024, "ffc_convq_forward: patch too large");
     ConvQArgs a;
     a.ebuf = (int)ebuf;
