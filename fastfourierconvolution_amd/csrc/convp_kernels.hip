@@ -398,34 +398,41 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
 #endif
 
     // ---------------- epilogue: bias/addend, BN partials, activation, store
+    // The job fields are copied out of the kernel-argument struct first: the compiler cannot tell that
+    // the output / slab stores leave the argument memory alone and reloaded every field read through J
+    // after each store (an s_load + s_waitcnt per stored element, r04 ISA).
+    float* const eout = J.out;
+    const float* const ebias = J.bias;
+    const float* const eadd = J.addend;
+    float* const estats = J.stats;
+    const int eM = J.M;
     const size_t plane = (size_t)J.OH * J.OW;
-    int ob[NTW], oo[NTW];
+    long long obase[NTW];   // per N-tile: element offset of (sample, channel 0, pixel)
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-        ob[nt] = b0 + pns[nt];
-        oo[nt] = ((r0 + pr_[nt]) * J.Sy + P.py) * J.OW + ((c0 + pc_[nt]) * J.Sx + P.px);
-    }
+    for (int nt = 0; nt < NTW; ++nt)
+        obase[nt] = (long long)(b0 + pns[nt]) * eM * (long long)plane +
+                    ((r0 + pr_[nt]) * J.Sy + P.py) * J.OW + ((c0 + pc_[nt]) * J.Sx + P.px);
     const int mbase = m0 + 4 * h;
-    if (J.bias || J.addend) {
+    if (ebias || eadd) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = mbase + (r & 3) + 8 * (r >> 2);
-            if (m >= J.M) continue;
-            const float bv = J.bias ? J.bias[m] : 0.0f;
+            if (m >= eM) continue;
+            const float bv = ebias ? ebias[m] : 0.0f;
 #pragma unroll
             for (int nt = 0; nt < NTW; ++nt) {
                 float v = acc[nt][r] + bv;
-                if (J.addend && pv[nt]) v += J.addend[((size_t)ob[nt] * J.M + m) * plane + oo[nt]];
+                if (eadd && pv[nt]) v += eadd[obase[nt] + (long long)m * plane];
                 acc[nt][r] = v;
             }
         }
     }
-    if (J.stats) {
+    if (estats) {
         float cntl = 0.0f;
 #pragma unroll
         for (int nt = 0; nt < NTW; ++nt) cntl += pv[nt] ? 1.0f : 0.0f;
         const float cnt = ffc::half_wave_sum(cntl);
-        float4* stp = reinterpret_cast<float4*>(J.stats) + ((size_t)pb * 4 + wave) * J.M;
+        float4* stp = reinterpret_cast<float4*>(estats) + ((size_t)pb * 4 + wave) * eM;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = mbase + (r & 3) + 8 * (r >> 2);
@@ -440,17 +447,17 @@ __global__ __launch_bounds__(256) void convp_kernel(ConvPArgs args_byval) {
                 q += d * d;
             }
             const float m2 = ffc::half_wave_sum(q);
-            if (cl == 0 && m < J.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
+            if (cl == 0 && m < eM) stp[m] = make_float4(cnt, mean, m2, 0.0f);
         }
     }
     auto store = [&](auto actf) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = mbase + (r & 3) + 8 * (r >> 2);
-            if (m < J.M) {
+            if (m < eM) {
 #pragma unroll
                 for (int nt = 0; nt < NTW; ++nt)
-                    if (pv[nt]) J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = actf(acc[nt][r]);
+                    if (pv[nt]) eout[obase[nt] + (long long)m * plane] = actf(acc[nt][r]);
             }
         }
     };

@@ -31,6 +31,7 @@
 // slab rows [block*4 + wave], activation) as in convp.
 #include "ffc_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -101,12 +102,16 @@ __device__ __forceinline__ QGeom<NTW> q_geometry(const ffc_convp_job& J, int wav
     g.r0 = rb * TR;
     g.c0 = cb * TC;
     const int cl = lane & 31;
+    // q / TRC and rem / TC for q < 32 * NTW <= 128 through a reciprocal: (q + 0.5) / d stays >= 0.5 / d
+    // >= 1/256 away from every integer and the approximate reciprocal is off by < 2^-16 there, so the
+    // truncation is exact (the generic i32 division is ~30 instructions per quotient)
+    const float rTRC = __builtin_amdgcn_rcpf((float)TRC), rTC = __builtin_amdgcn_rcpf((float)TC);
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
         const int q = nt * 32 + cl;
-        const int ns = q / TRC;
+        const int ns = (int)(((float)q + 0.5f) * rTRC);
         const int rem = q - ns * TRC;
-        const int r = rem / TC, c = rem - r * TC;
+        const int r = (int)(((float)rem + 0.5f) * rTC), c = rem - r * TC;
         g.pns[nt] = ns;
         g.pr_[nt] = r;
         g.pc_[nt] = c;
@@ -114,6 +119,16 @@ __device__ __forceinline__ QGeom<NTW> q_geometry(const ffc_convp_job& J, int wav
     }
     return g;
 }
+
+// The epilogues apply only the piecewise-linear activations (identity, ReLU, LeakyReLU) as
+// v > 0 ? v : v * slope: one code path instead of an unrolled store loop per activation (the kernel
+// was ~200 KB of code, most of it epilogue variants run once per tile).  Tanh / Sigmoid / GELU run
+// as a separate in-place pass after the launch (ffc_convq_forward_split; no model layer on this
+// kernel uses them: BN follows the convolution, or the layer runs on convt_smallm).
+__device__ __forceinline__ float q_slope(const ffc_convp_job& J) {
+    return J.act == FFC_ACT_RELU ? 0.0f : J.act == FFC_ACT_LEAKY_RELU ? J.act_param : 1.0f;
+}
+__device__ __forceinline__ float q_act(float v, float slope) { return v > 0.0f ? v : v * slope; }
 
 // one wave's fragments as MT x NTW x 4 coalesced floatx4 rows of 64 lanes
 template <int MT, int NTW>
@@ -130,6 +145,60 @@ __device__ __forceinline__ void store_partial(float* dst, int lane, const floatx
             }
 }
 
+// The job fields an epilogue uses, copied out of the kernel-argument struct: the compiler cannot
+// tell that the output / slab stores leave the argument memory alone, so every field read through J
+// after a store was a fresh s_load + s_waitcnt lgkmcnt(0) -- per stored element (r04 ISA; ~6K
+// cycles of a tile's epilogue).
+struct QEpi {
+    float* out;
+    const float* bias;
+    const float* addend;
+    float* stats;
+    int M, B, OH, OW;
+    float slope;
+};
+__device__ __forceinline__ QEpi q_epi(const ffc_convp_job& J) {
+    QEpi e;
+    e.out = J.out;
+    e.bias = J.bias;
+    e.addend = J.addend;
+    e.stats = J.stats;
+    e.M = J.M;
+    e.B = J.B;
+    e.OH = J.OH;
+    e.OW = J.OW;
+    e.slope = q_slope(J);
+    return e;
+}
+
+// BN partial slab rows [pb * 4 + wave] of one compute wave's fragments (channels mbase + (r & 3) +
+// 8 (r >> 2)): {count, mean, M2} over the wave's valid pixels
+template <int NTW>
+__device__ __forceinline__ void q_stats(const QEpi& E, int wave, int cl, int pb, int mbase, const bool (&pv)[NTW],
+                                        const floatx16 (&tacc)[NTW]) {
+    float cntl = 0.0f;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) cntl += pv[nt] ? 1.0f : 0.0f;
+    const float cnt = ffc::half_wave_sum(cntl);
+    float4* stp = reinterpret_cast<float4*>(E.stats) + ((size_t)pb * 4 + wave) * E.M;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int m = mbase + (r & 3) + 8 * (r >> 2);
+        float sm = 0.0f;
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) sm += pv[nt] ? tacc[nt][r] : 0.0f;
+        const float mean = cnt > 0.0f ? ffc::half_wave_sum(sm) / cnt : 0.0f;
+        float q = 0.0f;
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+            const float d = pv[nt] ? tacc[nt][r] - mean : 0.0f;
+            q += d * d;
+        }
+        const float m2 = ffc::half_wave_sum(q);
+        if (cl == 0 && m < E.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
+    }
+}
+
 // Epilogue of one compute wave (phase `wave`) of output tile (pb, m0): bias / addend, the BN partial
 // slab rows [pb * 4 + wave], activation, scattered stores
 template <int MT, int NTW>
@@ -137,80 +206,71 @@ __device__ __forceinline__ void convq_epilogue(const ffc_convp_job& J, int wave,
                                                floatx16 (&acc)[MT][NTW]) {
     const QGeom<NTW> g = q_geometry<NTW>(J, wave, lane, pb);
     const ffc_convp_phase& P = J.ph[wave];
+    const QEpi E = q_epi(J);
+    const int py = P.py, px = P.px;
     const int h = lane >> 5, cl = lane & 31;
-    const int b0 = g.b0, r0 = g.r0, c0 = g.c0;
-    const int* pns = g.pns;
-    const int* pr_ = g.pr_;
-    const int* pc_ = g.pc_;
-    const bool* pv = g.pv;
-    const size_t plane = (size_t)J.OH * J.OW;
-    int ob[NTW], oo[NTW];
+    const size_t plane = (size_t)E.OH * E.OW;
+    long long obase[NTW];   // per N-tile: element offset of (sample, channel 0, pixel)
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt)
+        obase[nt] = (long long)(g.b0 + g.pns[nt]) * E.M * (long long)plane +
+                    ((g.r0 + g.pr_[nt]) * 2 + py) * E.OW + ((g.c0 + g.pc_[nt]) * 2 + px);
+    // full tile: all channels below M and every lane's pixels valid (wave-uniform); then the byte
+    // offset of each lane's element from the tile's (first sample, channel m) row fits 32 bits
+    // (checked on the host: NS * M * OH * OW * 4 < 2^32)
+    bool allv = m0 + 32 * MT <= E.M;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) allv = allv && g.pv[nt];
+    const bool full = __builtin_amdgcn_ballot_w64(allv) == ~0ull;
+    unsigned voff[NTW];
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
-        ob[nt] = b0 + pns[nt];
-        oo[nt] = ((r0 + pr_[nt]) * J.Sy + P.py) * J.OW + ((c0 + pc_[nt]) * J.Sx + P.px);
+        voff[nt] = ((unsigned)g.pns[nt] * (unsigned)E.M * (unsigned)plane + (unsigned)(4 * h) * (unsigned)plane +
+                    (unsigned)(((g.r0 + g.pr_[nt]) * 2 + py) * E.OW + ((g.c0 + g.pc_[nt]) * 2 + px))) * 4u;
+        asm volatile("" : "+v"(voff[nt]));   // computed once, kept (not re-derived at every store)
     }
-    auto epilogue = [&](floatx16 (&tacc)[NTW], const int mbase) {
-        if (J.bias || J.addend) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        floatx16 (&tacc)[NTW] = acc[mt];
+        const int mbase = m0 + 32 * mt + 4 * h;
+        if (E.bias || E.addend) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = mbase + (r & 3) + 8 * (r >> 2);
-                if (m >= J.M) continue;
-                const float bv = J.bias ? J.bias[m] : 0.0f;
+                if (m >= E.M) continue;
+                const float bv = E.bias ? E.bias[m] : 0.0f;
 #pragma unroll
                 for (int nt = 0; nt < NTW; ++nt) {
                     float v = tacc[nt][r] + bv;
-                    if (J.addend && pv[nt]) v += J.addend[((size_t)ob[nt] * J.M + m) * plane + oo[nt]];
+                    if (E.addend && g.pv[nt]) v += E.addend[obase[nt] + (long long)m * plane];
                     tacc[nt][r] = v;
                 }
             }
         }
-        if (J.stats) {
-            float cntl = 0.0f;
-#pragma unroll
-            for (int nt = 0; nt < NTW; ++nt) cntl += pv[nt] ? 1.0f : 0.0f;
-            const float cnt = ffc::half_wave_sum(cntl);
-            float4* stp = reinterpret_cast<float4*>(J.stats) + ((size_t)pb * 4 + wave) * J.M;
+        if (E.stats) q_stats<NTW>(E, wave, cl, pb, mbase, g.pv, tacc);
+        if (full) {
+            // every pixel and channel of the fragments exists: no per-element masks, the channel's
+            // row offset on the scalar side (saddr form: uniform base + the lane's 32-bit offset)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int m = mbase + (r & 3) + 8 * (r >> 2);
-                float s = 0.0f;
-#pragma unroll
-                for (int nt = 0; nt < NTW; ++nt) s += pv[nt] ? tacc[nt][r] : 0.0f;
-                const float mean = cnt > 0.0f ? ffc::half_wave_sum(s) / cnt : 0.0f;
-                float q = 0.0f;
+                float* sb = E.out + ((size_t)g.b0 * E.M + m0 + 32 * mt + (r & 3) + 8 * (r >> 2)) * plane;
 #pragma unroll
                 for (int nt = 0; nt < NTW; ++nt) {
-                    const float d = pv[nt] ? tacc[nt][r] - mean : 0.0f;
-                    q += d * d;
-                }
-                const float m2 = ffc::half_wave_sum(q);
-                if (cl == 0 && m < J.M) stp[m] = make_float4(cnt, mean, m2, 0.0f);
-            }
-        }
-        auto store = [&](auto actf) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = mbase + (r & 3) + 8 * (r >> 2);
-                if (m < J.M) {
-#pragma unroll
-                    for (int nt = 0; nt < NTW; ++nt)
-                        if (pv[nt]) J.out[((size_t)ob[nt] * J.M + m) * plane + oo[nt]] = actf(tacc[nt][r]);
+                    *reinterpret_cast<float*>(reinterpret_cast<char*>(sb) + voff[nt]) = q_act(tacc[nt][r], E.slope);
                 }
             }
-        };
-        const float ap = J.act_param;
-        switch (J.act) {
-            case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
-            case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
-            case FFC_ACT_TANH: store([](float v) { return tanhf(v); }); break;
-            case FFC_ACT_SIGMOID: store([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
-            case FFC_ACT_GELU: store([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
-            default: store([](float v) { return v; }); break;
+            continue;
         }
-    };
-    epilogue(acc[0], m0 + 4 * h);
-    if constexpr (MT > 1) epilogue(acc[1], m0 + 32 + 4 * h);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = mbase + (r & 3) + 8 * (r >> 2);
+            if (m < E.M) {
+#pragma unroll
+                for (int nt = 0; nt < NTW; ++nt)
+                    if (g.pv[nt]) E.out[obase[nt] + (long long)m * plane] = q_act(tacc[nt][r], E.slope);
+            }
+        }
+    }
 }
 
 // One output tile (one row of the tile table) of one workgroup; returns when the tile is done (the
@@ -814,6 +874,20 @@ int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const in
 }  // namespace
 
 namespace {
+// the transcendental activations of a convq job's output, in place (see q_slope)
+__global__ void q_act_inplace_kernel(float* __restrict__ x, long long n, int act) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        float y;
+        switch (act) {
+            case FFC_ACT_TANH: y = tanhf(v); break;
+            case FFC_ACT_SIGMOID: y = 1.0f / (1.0f + expf(-v)); break;
+            default: y = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); break;   // FFC_ACT_GELU
+        }
+        x[i] = y;
+    }
+}
+
 // A[phase][Mpad][Kpad] fp32 -> fragment-ordered split planes: element
 // 3 * a_off + ((mtile * Kpad/16 + kstep) * 3 + piece) * 512 + lane * 8 + j  holds piece `piece` of
 // A[m = 32 * mtile + (lane & 31)][k = 16 * kstep + 8 * (lane >> 5) + j]
@@ -906,6 +980,8 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
         FFC_CHECK_ARG(J.nphase == 4 && J.Sy == 2 && J.Sx == 2, "ffc_convq_forward: 4-phase (stride-2) jobs only");
         FFC_CHECK_ARG(J.nseg >= 1 && J.nseg <= FFC_MAX_SEG, "ffc_convq_forward: nseg out of range");
         FFC_CHECK_ARG(J.Mpad % 128 == 0 && J.Mpad >= J.M, "ffc_convq_forward: Mpad");
+        FFC_CHECK_ARG((unsigned long long)J.NS * J.M * J.OH * J.OW * 4 < 0xFFFFFFFFull,
+                      "ffc_convq_forward: a pixel block's output span must fit 32-bit offsets");
         FFC_CHECK_ARG(J.NS > 0 && J.TR > 0 && J.TC > 0 && J.nrb > 0 && J.ncb > 0 && J.NS * J.TR * J.TC <= 32 * NTW,
                       "ffc_convq_forward: pixel block");
         for (int p = 0; p < 4; ++p) FFC_CHECK_ARG(J.ph[p].Kpad % 16 == 0, "ffc_convq_forward: Kpad % 16");
@@ -948,12 +1024,32 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
     a.ntiles = ntiles;
     const int4* sl = reinterpret_cast<const int4*>(slot_tiles);
     hipStream_t s = (hipStream_t)stream;
-    switch (cfg) {
-        case 0: return launch_q<1, 4>(a, ntiles, lds, s, sl, nslots);
-        case 1: return launch_q<1, 2>(a, ntiles, lds, s, sl, nslots);
-        case 2: return launch_q<2, 2>(a, ntiles, lds, s, sl, nslots);
-        case 3: return launch_q<1, 1>(a, ntiles, lds, s, sl, nslots);
+    // Tanh / Sigmoid / GELU: the kernel stores the pre-activation, a second pass applies it (q_slope)
+    bool post[2] = {false, false};
+    for (int j = 0; j < 2; ++j) {
+        ffc_convp_job& Jc = a.jobs[j];
+        if (Jc.act == FFC_ACT_TANH || Jc.act == FFC_ACT_SIGMOID || Jc.act == FFC_ACT_GELU) {
+            post[j] = j < njobs;
+            Jc.act = FFC_ACT_IDENTITY;
+        }
     }
-    ffc::set_error("ffc_convq_forward: unknown cfg");
-    return FFC_E_INVALID;
+    int rc = FFC_E_INVALID;
+    switch (cfg) {
+        case 0: rc = launch_q<1, 4>(a, ntiles, lds, s, sl, nslots); break;
+        case 1: rc = launch_q<1, 2>(a, ntiles, lds, s, sl, nslots); break;
+        case 2: rc = launch_q<2, 2>(a, ntiles, lds, s, sl, nslots); break;
+        case 3: rc = launch_q<1, 1>(a, ntiles, lds, s, sl, nslots); break;
+        default: ffc::set_error("ffc_convq_forward: unknown cfg"); return FFC_E_INVALID;
+    }
+    if (rc != FFC_OK) return rc;
+    for (int j = 0; j < njobs; ++j) {
+        if (!post[j]) continue;
+        const long long n = (long long)jobs[j].B * jobs[j].M * jobs[j].OH * jobs[j].OW;
+        const long long blocks = (n + 255) / 256;
+        hipLaunchKernelGGL(q_act_inplace_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, s,
+                           jobs[j].out, n, jobs[j].act);
+        rc = ffc::launch_status("ffc_convq_forward (activation pass)");
+        if (rc != FFC_OK) return rc;
+    }
+    return FFC_OK;
 }

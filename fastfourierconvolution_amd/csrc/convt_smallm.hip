@@ -282,16 +282,21 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
     const int OH = 2 * a.IH, OW = 2 * a.IW;
     const int oy0 = 2 * (y0 + qy), ox0 = 2 * (x0 + qx);
     const bool xin = x0 + qx + 1 < a.IW;   // both input columns in range
+    // argument fields read before the stores (after a store the compiler reloads them: ISA r04)
+    float* const out = a.out;
+    float bvs[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) bvs[m] = a.bias ? a.bias[m] : 0.0f;
     auto store = [&](auto actf) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            const float bv = a.bias ? a.bias[m] : 0.0f;
+            const float bv = bvs[m];
             auto val = [&](int i, int j) { return actf(get(i * 4 + j, m) + bv); };
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int oy = oy0 + i;
                 if (oy >= OH) continue;
-                float* row = a.out + (((size_t)b * M + m) * OH + oy) * OW + ox0;
+                float* row = out + (((size_t)b * M + m) * OH + oy) * OW + ox0;
                 if (xin) {
                     *reinterpret_cast<float4*>(row) = make_float4(val(i, 0), val(i, 1), val(i, 2), val(i, 3));
                 } else {
@@ -552,24 +557,30 @@ __global__ __launch_bounds__(2 * Head3<TR3>::HT) void conv3x3_smallm_kernel(Smal
                 acc2[m][i][jp] += f2{part[((m * 4 + i) * 4 + 2 * jp) * HT + tid],
                                      part[((m * 4 + i) * 4 + 2 * jp + 1) * HT + tid]};
     const int oy0 = y0 + qy, ox0 = x0 + qx;
-    const bool xin = ox0 + 3 < a.IW;
+    // argument fields read before the stores (after a store the compiler reloads them: ISA r04)
+    float* const out = a.out;
+    const int IH = a.IH, IW = a.IW;
+    const bool xin = ox0 + 3 < IW;
+    float bvs[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) bvs[m] = (a.bias && m < M) ? a.bias[m] : 0.0f;
     auto store = [&](auto actf) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             if (m >= M) break;
-            const float bv = a.bias ? a.bias[m] : 0.0f;
+            const float bv = bvs[m];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int oy = oy0 + i;
-                if (oy >= a.IH) continue;
-                float* row = a.out + (((size_t)b * M + m) * a.IH + oy) * a.IW + ox0;
+                if (oy >= IH) continue;
+                float* row = out + (((size_t)b * M + m) * IH + oy) * IW + ox0;
                 if (xin) {
                     *reinterpret_cast<float4*>(row) = make_float4(actf(ACC(m, i, 0) + bv), actf(ACC(m, i, 1) + bv),
                                                                   actf(ACC(m, i, 2) + bv), actf(ACC(m, i, 3) + bv));
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        if (ox0 + j < a.IW) row[j] = actf(ACC(m, i, j) + bv);
+                        if (ox0 + j < IW) row[j] = actf(ACC(m, i, j) + bv);
                 }
             }
         }
