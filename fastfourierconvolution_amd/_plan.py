@@ -684,19 +684,6 @@ def build_patch_tiles(plans, nxcd: int = 8, ksplit: int = 1):
                         ordered.append((j, m0, pb, 0))
         remap = xcd_remap(len(ordered), nxcd)
         return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)
-    if os.environ.get("FFC_TILE_ORDER") == "group":
-        # (job, M-tile) major: an XCD's contiguous run covers one weight group's pixel blocks, so
-        # its L2 holds that group's A planes (every pixel block re-reads A) instead of all of them
-        slot = 0
-        for j in order:
-            pl = plans[j]
-            for m0 in range(0, pl.M, 32 * pl.mt):
-                for pb in range(pl.npb):
-                    for k in range(ksplit):
-                        ordered.append((j, m0, pb, slot * 8 + k if ksplit > 1 else 0))
-                    slot += 1
-        remap = xcd_remap(len(ordered), nxcd)
-        return np.asarray([ordered[i] for i in remap], dtype=np.int32).reshape(-1, 4)
     slot = 0
     for x in range(nxcd):
         lo, hi = npb * x // nxcd, npb * (x + 1) // nxcd

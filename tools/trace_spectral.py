@@ -44,7 +44,7 @@ def main():
     for f in (rfu, rst):
         f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     recs = []
-    ofu, ost = L.ffc_fu_forward, L.ffc_st_prologue
+    ofu, ost = L.ffc_fu_forward_ex, L.ffc_st_prologue
 
     def fu(*a):
         rc = ofu(*a)
@@ -64,10 +64,10 @@ def main():
         recs.append(("st", f"Cin={a[2]} {a[3]}x{a[4]} c={a[10]}", buf))
         return rc
 
-    L.ffc_fu_forward, L.ffc_st_prologue = fu, st
+    L.ffc_fu_forward_ex, L.ffc_st_prologue = fu, st
     with torch.no_grad():
         G(z)
-    L.ffc_fu_forward, L.ffc_st_prologue = ofu, ost
+    L.ffc_fu_forward_ex, L.ffc_st_prologue = ofu, ost
     for kind, desc, buf in recs:
         rt0, rt1 = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64)
         dur = (rt1 - rt0) / 100.0
