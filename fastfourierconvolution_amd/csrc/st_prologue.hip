@@ -97,25 +97,45 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
 
     // 2. SE gate.  Reductions run over 16-lane DPP rows (no shuffle chains): row q of the
     //    block (16 lanes, consecutive pixels / inputs: conflict-free LDS) owns one channel / unit.
+    // Every inner loop runs four independent LDS reads per step: one read per step made each
+    // lane's reduction a chain of dependent LDS round trips (fc1 over Cin = 256: 16 of them; the
+    // means over 16x16 planes: 16), ~5 us of the ST prologue at every batch size (r04 probe:
+    // st_prologue with the SE gate skipped, profiles/r04/w)
     const int row = tid >> 4, rl = tid & 15;
 #pragma unroll 4
     for (int ch = row; ch < Cin; ch += ST_THREADS / 16) {
-        float s = 0.0f;
-        for (int i = rl; i < hw; i += 16) s += xs[ch * hw + i];
+        const float* xc = xs + ch * hw;
+        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+        int i = rl;
+        for (; i + 48 < hw; i += 64) {
+            s0 += xc[i];
+            s1 += xc[i + 16];
+            s2 += xc[i + 32];
+            s3 += xc[i + 48];
+        }
+        for (; i < hw; i += 16) s0 += xc[i];
+        float s = (s0 + s1) + (s2 + s3);
         s = ffc::row16_sum(s);
         if (rl == 15) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
     }
     __syncthreads();
-    for (int j = row; j < hid; j += ST_THREADS / 16) {  // fc1: one 16-lane row per hidden unit
-        float s = 0.0f;
-        if (a.w1_off >= 0) {
-            const float* w1 = sm + a.w1_off + j * Cin;
-            for (int k = rl; k < Cin; k += 16) s = fmaf(w1[k], gate[k], s);
-        } else {
-            for (int k = rl; k < Cin; k += 16) s = fmaf(a.w1[(size_t)j * Cin + k], gate[k], s);
+    // fc1: one wave per hidden unit (64 lanes over the inputs)
+    for (int j = wave; j < hid; j += ST_WAVES) {
+        const float* w1 = a.w1_off >= 0 ? sm + a.w1_off + (size_t)j * Cin : a.w1 + (size_t)j * Cin;
+        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+        int k = lane;
+        for (; k + 192 < Cin; k += 256) {
+            s0 = fmaf(w1[k], gate[k], s0);
+            s1 = fmaf(w1[k + 64], gate[k + 64], s1);
+            s2 = fmaf(w1[k + 128], gate[k + 128], s2);
+            s3 = fmaf(w1[k + 192], gate[k + 192], s3);
         }
-        s = ffc::row16_sum(s);
-        if (rl == 15) hv[j] = fmaxf(s, 0.0f);
+        for (; k < Cin; k += 64) s0 = fmaf(w1[k], gate[k], s0);
+        // the two 32-lane halves' sums (DPP + permlane16 swap), added on the scalar side
+        const float hs = ffc::half_wave_sum((s0 + s1) + (s2 + s3));
+        const float s = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hs), 0)) +
+                        __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hs), 32));
+        if (lane == 0) hv[j] = fmaxf(s, 0.0f);
     }
     __syncthreads();
     // fc2 + sigmoid: one 16-lane row per input channel k (lanes over the hidden units)
