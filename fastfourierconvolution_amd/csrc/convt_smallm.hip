@@ -16,8 +16,9 @@
 //     py = 0: (ky=1, dy=0), (ky=3, dy=-1)      py = 1: (ky=0, dy=+1), (ky=2, dy=0)
 // A workgroup covers a 32x16 input tile (+1 halo) with four quarters of 128 threads that take
 // alternate channels and add their partial sums in a fixed order at the end; two workgroups per
-// CU.  All weights are staged once as [channel][tap][m 0..3], so the FMAs run as v_pk_fma_f32 on
-// output-channel pairs (one input value against two channels' weights).  Each quarter stages
+// CU.  The weights are packed once as [channel][tap][m 0..3] and read per channel by scalar loads,
+// so the FMAs run as v_pk_fma_f32 on output-channel pairs (one input value against two channels'
+// SGPR weights).  Each quarter stages
 // its next channel's patch through registers (float4 loads issued before the current channel's
 // FMAs, written to the other LDS buffer after them).
 #include "ffc_internal.h"
@@ -97,14 +98,10 @@ constexpr int CT_GT = (CT_CPQ * CT_G + CT_QT - 1) / CT_QT;   // groups per threa
 constexpr int CT_PB = CT_PR * CT_PS;         // floats per channel patch
 constexpr int CT_NQ = 4;                     // channel quarters
 constexpr int CT_THREADS = CT_QT * CT_NQ;
-constexpr int CT_CMAX = 256;                 // channels (both segments) whose weights fit in LDS
-// float offset of the staged weights: behind the patch double buffer (and the partial-sum combine
-// area, which reuses the patch buffers: CT_QT * 16 * 4 floats <= the patch buffers)
-constexpr int CT_WOFF = 2 * CT_NQ * CT_CPQ * CT_PB;
-static_assert(CT_QT * 16 * 4 <= CT_WOFF, "combine area must fit in the patch buffers");
+constexpr int CT_CMAX = 256;                 // channels (both segments)
 
 // MM output channels: pairs (m, m+1) run as v_pk_fma_f32, one input value against the two
-// channels' weights (LDS weight layout [channel][tap][m 0..3]); an odd last channel is scalar.
+// channels' weights (packed layout [channel][tap][m 0..3]); an odd last channel is scalar.
 // TR_ / NQ_: input tile rows and channel quarters.  The default 16 x 4 (512 threads) tiles large
 // batches; 8 x 8 (same 512 threads, half the rows, the channels split 8 ways) doubles the workgroups
 // when the grid would leave CUs idle (the small per-rank batches of strong scaling).
@@ -117,8 +114,8 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
     constexpr int CT_GT = (CT_CPQ * CT_G + CT_QT - 1) / CT_QT;
     constexpr int CT_PB = CT_PR * CT_PS;
     constexpr int CT_THREADS = CT_QT * CT_NQ;
-    constexpr int CT_WOFF = 2 * CT_NQ * CT_CPQ * CT_PB;
-    static_assert(CT_QT % 64 == 0 && CT_QT * 16 * 4 <= CT_WOFF, "quarters of whole waves; combine area fits");
+    // the partial-sum combine area reuses the patch double buffer
+    static_assert(CT_QT % 64 == 0 && CT_QT * 16 * 4 <= 2 * CT_NQ * CT_CPQ * CT_PB, "quarters of whole waves; combine area fits");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int q = __builtin_amdgcn_readfirstlane(threadIdx.x / CT_QT), tid = threadIdx.x % CT_QT;
     int bid = blockIdx.x;
@@ -135,13 +132,8 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
     const float* xs0 = a.x[0];
     const long long xd1 = a.nseg > 1 ? (long long)(a.x[1] - a.x[0]) : 0;   // segment 1 base - segment 0 base
     float* pbuf = lds;   // [2 stages][NQ][CPQ][PB]
-    // packed weights [Ct][16 taps][4 m] (ffc_convt_smallm_pack), staged once into LDS behind the
-    // patch buffers and read as wave-uniform (broadcast) ds_read_b128: scalar loads per channel
-    // would put an SMEM round trip (and an lgkmcnt(0) that also drains the LDS reads) in every
-    // channel step
+    // packed weights [Ct][16 taps][4 m] (ffc_convt_smallm_pack), read per channel by scalar loads
     typedef float fx4 __attribute__((ext_vector_type(4)));
-    fx4* wlds = reinterpret_cast<fx4*>(lds + CT_WOFF);
-    for (int i = threadIdx.x; i < Ct * 16; i += CT_THREADS) wlds[i] = reinterpret_cast<const fx4*>(a.wpack)[i];
 
     // step k of quarter q: channels CPQ (NQ k + q) + {0 .. CPQ-1}
     auto load = [&](int k, float4 (&r)[CT_GT]) {
@@ -220,13 +212,16 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
             v[i][2] = mid.y;
             v[i][3] = p[i * CT_PS + 3];
         }
-        const fx4* wc = wlds + ci * 16;
+        // the channel's weights are wave-uniform: scalar loads (s_load_dwordx16) into SGPRs, read by
+        // the FMAs directly.  Broadcast LDS reads of them (r03) returned 64 lanes x 16 B per tap and
+        // bounded the kernel on LDS bandwidth (45 -> 39 us at gen64 B = 256, profiles/r04/z)
+        const fx4* wg = reinterpret_cast<const fx4*>(a.wpack) + ci * 16;
 #pragma unroll
         for (int ky = 0; ky < 4; ++ky) {
             const int py = (ky & 1) ? 0 : 1, dy = ky == 0 ? 1 : (ky == 3 ? -1 : 0);
 #pragma unroll
             for (int kx = 0; kx < 4; ++kx) {
-                const fx4 wk = wc[ky * 4 + kx];
+                const fx4 wk = wg[ky * 4 + kx];
                 const int px = (kx & 1) ? 0 : 1, dx = kx == 0 ? 1 : (kx == 3 ? -1 : 0);
 #pragma unroll
                 for (int aa = 0; aa < 2; ++aa)
@@ -343,22 +338,27 @@ struct Head3 {
     static constexpr int PB3 = G3 * 4;                        // floats per patch buffer
     static_assert(HT * 4 * 16 <= 4 * PB3, "combine area fits in the patch buffers");
 };
-size_t head3_lds_bytes(int tr, int nchunks) {
-    const size_t w = ((size_t)nchunks * 48 + 63) / 64 * 64;
+size_t head3_lds_bytes(int tr) {
     const size_t pb = (size_t)(tr + 2) * (S3 / 4) * 4;
-    return (w + 4 * pb) * sizeof(float);
+    return 4 * pb * sizeof(float);
 }
 
 // TF: each segment is read through its deferred transform a.tf[s] (ffc_in_tf): the producer's
 // BN + activation + NoiseInjection applied as the patch goes to LDS, on in-image groups only (the
 // zero padding belongs to the transformed tensor).  The head is VALU-bound, so GELU uses the
 // branch-free gelu_as below instead of erff (whose two ranges diverge within a wave).
+// three waves per SIMD (<= 168 VGPRs, a few spilled outside the FMA loop) instead of two at 182:
+// fgan128 head 1.84 -> 1.77 ms (profiles/r04/aa)
+#ifndef FFC_HEAD_WPE
+#define FFC_HEAD_WPE 3
+#endif
+#define HEAD3_WPE __attribute__((amdgpu_waves_per_eu(FFC_HEAD_WPE)))
 template <int MM, bool TF, int TR3 = 64>
-__global__ __launch_bounds__(2 * Head3<TR3>::HT) void conv3x3_smallm_kernel(SmallMArgs a) {
+__global__ __launch_bounds__(2 * Head3<TR3>::HT) HEAD3_WPE void conv3x3_smallm_kernel(SmallMArgs a) {
     constexpr int R3 = Head3<TR3>::R3, G3 = Head3<TR3>::G3, HT = Head3<TR3>::HT, GT3 = Head3<TR3>::GT3;
     constexpr int PB3 = Head3<TR3>::PB3;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int half = threadIdx.x / HT, tid = threadIdx.x % HT;
+    const int half = __builtin_amdgcn_readfirstlane(threadIdx.x / HT), tid = threadIdx.x % HT;
     int bid = blockIdx.x;
     const int tx = bid % a.ntx;
     bid /= a.ntx;
@@ -368,25 +368,7 @@ __global__ __launch_bounds__(2 * Head3<TR3>::HT) void conv3x3_smallm_kernel(Smal
     const int qy = 4 * (tid >> 4), qx = 4 * (tid & 15);   // this thread's 4x4 outputs (tile coords)
     const int M = a.M;
     const int nchunks = a.C[0] + (a.nseg > 1 ? a.C[1] : 0);   // one channel per chunk
-    float* wl_all = lds;                                      // [nchunks][4][12]
-    float* pbuf = lds + (nchunks * 48 + 63) / 64 * 64;        // [2 buffers][2 halves][PB3]
-
-    for (int q0 = 0; q0 < nchunks * 48; q0 += 8 * 2 * HT) {   // 8 loads in flight per thread
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int q = q0 + u * 2 * HT + threadIdx.x;
-            const int ci = q / 48, m = (q / 12) & 3, t = q % 12;
-            const int s = ci < a.C[0] ? 0 : 1;
-            const int c = s == 0 ? ci : ci - a.C[0];
-            v[u] = (q < nchunks * 48 && t < 9 && m < M) ? a.w[s][((size_t)m * a.C[s] + c) * 9 + t] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int q = q0 + u * 2 * HT + threadIdx.x;
-            if (q < nchunks * 48) wl_all[q] = v[u];
-        }
-    }
+    float* pbuf = lds;                                        // [2 buffers][2 halves][PB3]
 
     auto inimg = [&](int j) {
         const int n = j * HT + tid;
@@ -495,15 +477,16 @@ __global__ __launch_bounds__(2 * Head3<TR3>::HT) void conv3x3_smallm_kernel(Smal
             v[i][1] = l4.x; v[i][2] = l4.y; v[i][3] = l4.z; v[i][4] = l4.w;
             v[i][5] = p[i * S3 + 5];
         }
-        const float* wl = wl_all + ci * 48;
+        // the channel's 9 M weights are wave-uniform: scalar loads straight from the (M, C_s, 3, 3)
+        // tensor into SGPRs (no LDS broadcast reads: they cost the LDS return path 64 lanes x 16 B each)
+        const int ws = ci < a.C[0] ? 0 : 1;
+        const float* wsg = a.w[ws] + (ws == 0 ? ci : ci - a.C[0]) * 9;
+        const int wms = a.C[ws] * 9;
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            float k9[12];
+            float k9[9];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const float4 t = reinterpret_cast<const float4*>(wl + m * 12)[q];
-                k9[4 * q] = t.x; k9[4 * q + 1] = t.y; k9[4 * q + 2] = t.z; k9[4 * q + 3] = t.w;
-            }
+            for (int t = 0; t < 9; ++t) k9[t] = wsg[m * wms + t];
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -655,8 +638,7 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     a.act = act;
     a.act_param = act_param;
 
-    const size_t woff = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PS;
-    const size_t lds = (woff + (size_t)(C0 + (x1 ? C1 : 0)) * 64) * sizeof(float);
+    const size_t lds = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PS * sizeof(float);   // patch double buffer
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
     typedef void (*CtKernel)(SmallMArgs);
@@ -731,7 +713,7 @@ static int conv3x3_smallm_launch(const float* x0, int C0, const float* w0, const
         a.tf[s] = t ? *t : none;
     }
     const int nchunks = C0 + (x1 ? C1 : 0);
-    const size_t lds = head3_lds_bytes(tr, nchunks);
+    const size_t lds = head3_lds_bytes(tr);
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
     typedef void (*C3Kernel)(SmallMArgs);
