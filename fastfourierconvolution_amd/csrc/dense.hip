@@ -74,26 +74,43 @@ __global__ __launch_bounds__(DN_THREADS) void dense_kernel(DenseArgs a) {
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    const int ku = (a.K + 1) >> 1;   // k-steps that hold data (k >= K: zero A and zero W)
+    // in groups of 4 k-steps, a group wholly past K skipped (wave-uniform branch): K = 100 runs 52
+    // of the 64 MFMAs
 #pragma unroll
-    for (int u = 0; u < KH; ++u)   // k >= K: zero A (padded rows) and zero W
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * u + hh], wa[u], acc, 0, 0, 0);
+    for (int u0 = 0; u0 < KH; u0 += 4) {
+        if (u0 < ku) {
+#pragma unroll
+            for (int u = u0; u < u0 + 4; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[2 * u + hh], wa[u], acc, 0, 0, 0);
+        }
+    }
     if (!nv) return;
     const float bv = a.bias ? a.bias[n] : 0.0f;
+    // argument fields read before the stores (after a store the compiler reloads them)
     float* dst;
-    int ld, nn;
+    int ld;
     if (n < a.N0) {
-        dst = a.out0;
+        dst = a.out0 + n;
         ld = a.N0;
-        nn = n;
     } else {
-        dst = a.out1;
+        dst = a.out1 + (n - a.N0);
         ld = a.N - a.N0;
-        nn = n - a.N0;
     }
+    const int Bn = a.B, act = a.act;
+    const float ap = a.act_param;
+    auto store = [&](auto actf) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int b = b0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (b < a.B) dst[(size_t)b * ld + nn] = ffc::apply_act(acc[r] + bv, a.act, a.act_param);
+        for (int r = 0; r < 16; ++r) {
+            const int b = b0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (b < Bn) dst[(size_t)b * ld] = actf(acc[r] + bv);
+        }
+    };
+    switch (act) {   // one branch per launch, not per element
+        case FFC_ACT_IDENTITY: store([](float v) { return v; }); break;
+        case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
+        case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
+        default: store([act, ap](float v) { return ffc::apply_act(v, act, ap); }); break;
     }
 }
 
