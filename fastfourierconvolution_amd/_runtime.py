@@ -252,6 +252,8 @@ BN_FOLD = __import__("os").environ.get("FFC_BN_FOLD", "1") != "0"
 # slab rows x channels up to which the fold beats the separate launch (each consumer workgroup
 # reads the whole slab; measured on MI355X, r02)
 BN_FOLD_MAX = int(__import__("os").environ.get("FFC_BN_FOLD_MAX", "4096"))
+# the fused ST prologue over several workgroups per sample at small batches (FFC_ST_SPLIT=0: one)
+ST_SPLIT = __import__("os").environ.get("FFC_ST_SPLIT", "1") != "0"
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
 FU_SPILL = __import__("os").environ.get("FFC_FU_SPILL", "1") != "0"
 
@@ -459,7 +461,8 @@ def plan_knobs():
     """the module-level switches plans depend on (tests and A/B runs flip them): part of every plan
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
-            FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH)
+            FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
+            ST_SPLIT)
 
 
 def algorithmic_flops(plan) -> float:

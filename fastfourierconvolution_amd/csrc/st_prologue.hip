@@ -26,6 +26,7 @@ struct StArgs {
     float* gate_out;     // optional (B, Cin) copy of the gate (tests / debugging), may be null
     int Cin, H, W, pool, hid, c;
     int x_dma;           // sample copied by LDS-DMA (no pooling, 16-byte aligned rows)
+    int split;           // workgroups per sample: each takes 1/split of conv1's output tiles
     // LDS layout (float offsets; -1: not staged, read from global)
     int gate_off, hv_off, st_off, red_off, scr_off, wt_off, w1_off, w2_off;
 };
@@ -52,7 +53,8 @@ __device__ unsigned long long g_st_trace[8 * 4096];
 
 __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x / a.split, sp = blockIdx.x % a.split;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int Cin = a.Cin, c = a.c;
     const int h = a.pool ? a.H / 2 : a.H, w = a.pool ? a.W / 2 : a.W;
     const int hw = h * w;
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         if (rl == 15) {
             const float gk = 1.0f / (1.0f + expf(-s));   // hidden = 0: sigmoid(0) = 0.5
             gate[k] = gk;
-            if (a.gate_out) a.gate_out[(size_t)b * Cin + k] = gk;
+            if (a.gate_out && sp == 0) a.gate_out[(size_t)b * Cin + k] = gk;
         }
     }
     __syncthreads();
@@ -160,9 +162,11 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
 
     // 3. conv1: t[o][p] = sum_k W[o][k] gate[k] x[k][p] on MFMA; lane half h carries k = 2s + h.
     //    With fewer than 4 output tiles the K range is split over the idle waves (LDS reduction).
+    //    With split > 1 this workgroup takes tiles [t0, t0 + tiles) of the sample's MT x NT (the
+    //    load and the SE gate are repeated per workgroup; small batches fill the CUs this way)
     const int h2 = lane >> 5, col = lane & 31;
     const int MT = Mpad / 32, NT = (hw + 31) / 32;
-    const int tiles = MT * NT;
+    const int tiles = MT * NT / a.split, t0 = sp * tiles;
     const int nsplit = tiles >= ST_WAVES ? 1 : ST_WAVES / tiles;
     const int KS = Cin / 2;
     const float* wa = a.wt_off >= 0 ? wt : a.wcT;
@@ -207,22 +211,22 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         }
     };
     if (nsplit == 1) {
-        for (int tile = wave; tile < tiles; tile += ST_THREADS / 64) {
-            const int mt = tile % MT, nt = tile / MT;
+        for (int tl = wave; tl < tiles; tl += ST_THREADS / 64) {
+            const int tile = t0 + tl, mt = tile % MT, nt = tile / MT;
             finish(mt, nt, mfma_range(mt, nt, 0, KS, true));
         }
     } else {
-        const int tile = wave / nsplit, part = wave % nsplit;
+        const int tl = wave / nsplit, part = wave % nsplit, tile = t0 + tl;
         const int mt = tile % MT, nt = tile / MT;
         const int per = (KS + nsplit - 1) / nsplit;
         floatx16 acc;
-        if (tile < tiles) acc = mfma_range(mt, nt, min(KS, part * per), min(KS, (part + 1) * per), part == 0);
-        if (tile < tiles && part > 0) {
+        if (tl < tiles) acc = mfma_range(mt, nt, min(KS, part * per), min(KS, (part + 1) * per), part == 0);
+        if (tl < tiles && part > 0) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
         }
         __syncthreads();
-        if (tile < tiles && part == 0) {
+        if (tl < tiles && part == 0) {
             for (int q = 1; q < nsplit; ++q)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] += red[((wave + q) * 16 + r) * 64 + lane];
@@ -231,9 +235,13 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     }
     __syncthreads();
     ST_STAMP(3);
+    // one slab row per (sample, workgroup); a channel none of this workgroup's tiles covers gets
+    // {0, 0, 0} (weightless in the moment sums of every consumer)
     for (int o = tid; o < c; o += ST_THREADS) {
         float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
         for (int nt = 0; nt < NT; ++nt) {
+            const int tile = (o >> 5) + MT * nt;
+            if (tile < t0 || tile >= t0 + tiles) continue;
             const float* e = st + (nt * c + o) * 3;
             const float tot = nn + e[0];
             const float delta = e[1] - mean;
@@ -241,7 +249,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
             m2 += e[2] + delta * delta * (nn * e[0] / tot);
             nn = tot;
         }
-        reinterpret_cast<float4*>(a.slab)[(size_t)b * c + o] = make_float4(nn, mean, m2, 0.0f);
+        reinterpret_cast<float4*>(a.slab)[((size_t)b * a.split + sp) * c + o] = make_float4(nn, mean, m2, 0.0f);
     }
 #ifdef FFC_TRACE
     __syncthreads();
@@ -319,10 +327,31 @@ extern "C" size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int
     return st_layout(Cin, H, W, pool, hidden, c).bytes;
 }
 
+extern "C" int ffc_st_prologue_split(int B, int Cin, int H, int W, int pool, int c) {
+    if (B <= 0 || Cin <= 0 || H <= 0 || W <= 0 || c <= 0 || c > 65536 || H > 65536 || W > 65536) return 1;
+    const long long hw = (long long)(pool ? H / 2 : H) * (pool ? W / 2 : W);
+    const long long T = (long long)((c + 31) / 32) * ((hw + 31) / 32);
+    // workgroups per sample: enough for one per CU (256), a divisor of the tile count
+    int s = 1;
+    while ((long long)B * s < 256 && T % (2 * s) == 0 && s < 8) s *= 2;
+    return s;
+}
+
 extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
                                const float* w2, int hidden, const float* wconv1T, int c, float* t, float* slab,
                                float* gate_out, void* stream) {
+    return ffc_st_prologue_ex(x, B, Cin, H, W, pool, w1, w2, hidden, wconv1T, c, 1, t, slab, gate_out, stream);
+}
+
+extern "C" int ffc_st_prologue_ex(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
+                                  const float* w2, int hidden, const float* wconv1T, int c, int split, float* t,
+                                  float* slab, float* gate_out, void* stream) {
     FFC_CHECK_ARG(x && wconv1T && t && slab && B > 0, "ffc_st_prologue: bad args");
+    {
+        const long long hw = (long long)(pool ? H / 2 : H) * (pool ? W / 2 : W);
+        const long long T = (long long)((c + 31) / 32) * ((hw + 31) / 32);
+        FFC_CHECK_ARG(split >= 1 && T % split == 0, "ffc_st_prologue: split must divide conv1's output tiles");
+    }
     FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_st_prologue: null SE weights");
     const size_t lds = ffc_st_prologue_lds_bytes(Cin, H, W, pool, hidden, c);
     FFC_CHECK_ARG(lds > 0, "ffc_st_prologue: sample does not fit in LDS (use se_gate + conv)");
@@ -361,11 +390,12 @@ extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int
     a.wt_off = L.wt_off;
     a.w1_off = L.w1_off;
     a.w2_off = L.w2_off;
+    a.split = split;
     a.x_dma = !pool && ((size_t)Cin * H * W) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     if (L.w1_off >= 0 && ((reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2)) & 15)) {
         a.w1_off = a.w2_off = -1;   // unaligned SE weights: read from global
     }
     if (L.wt_off >= 0 && (reinterpret_cast<uintptr_t>(wconv1T) & 15)) a.wt_off = -1;
-    hipLaunchKernelGGL(st_prologue_kernel, dim3(B), dim3(ST_THREADS), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(st_prologue_kernel, dim3((unsigned)B * split), dim3(ST_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_st_prologue");
 }

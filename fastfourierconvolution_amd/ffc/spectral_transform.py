@@ -126,11 +126,13 @@ class SpectralTransform(nn.Module):
             se1 = rt.require(self.se_block.fc[0].weight.detach(), "se.fc.0.weight") if hid > 0 else None
             se2 = rt.require(self.se_block.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None
             wc = self._conv1_T(stream)
-            slab = torch.empty((B, c, 4), device=dev, dtype=torch.float32)
+            # small batches: several workgroups per sample, each with a share of conv1's tiles
+            split = L.ffc_st_prologue_split(B, Cin, H, W, int(pool), c) if rt.ST_SPLIT else 1
+            nrows = B * split
+            slab = torch.empty((nrows, c, 4), device=dev, dtype=torch.float32)
             with rt.observe("st_prologue", flops=2.0 * B * c * Cin * h2 * w2):
-                check(L.ffc_st_prologue(ptr(x), B, Cin, H, W, int(pool), ptr(se1), ptr(se2), hid, ptr(wc), c, ptr(t),
-                                        ptr(slab), None, stream), "ffc_st_prologue")
-            nrows = B
+                check(L.ffc_st_prologue_ex(ptr(x), B, Cin, H, W, int(pool), ptr(se1), ptr(se2), hid, ptr(wc), c, split,
+                                           ptr(t), ptr(slab), None, stream), "ffc_st_prologue")
         elif not pool and L.ffc_pw_gate_lds_bytes(Cin, c) > 0:
             # large planes: SE gate (plane means + FCs), then conv1 with the gate folded into the
             # per-sample weights and the bn1 partials in the epilogue (csrc/st_pw.hip)

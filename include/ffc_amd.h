@@ -303,6 +303,15 @@ size_t ffc_st_prologue_lds_bytes(int Cin, int H, int W, int pool, int hidden, in
 int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
                     const float* w2, int hidden, const float* wconv1T, int c, float* t, float* slab,
                     float* gate_out, void* stream);
+/* The same over `split` workgroups per sample, each taking 1/split of conv1's output tiles
+ * (ceil32(c)/32 x ceil32(h*w)/32; split must divide that count) after its own pool + SE gate:
+ * small batches fill the CUs.  slab gets [B * split][c] rows (row b * split + s; channels a
+ * workgroup does not cover are {0, 0, 0}).  ffc_st_prologue_split() is the split the library
+ * picks for a batch (1 when B alone fills the GPU). */
+int ffc_st_prologue_split(int B, int Cin, int H, int W, int pool, int c);
+int ffc_st_prologue_ex(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
+                       const float* w2, int hidden, const float* wconv1T, int c, int split, float* t,
+                       float* slab, float* gate_out, void* stream);
 /* SpectralTransform conv1 with the SE gate for planes the fused prologue cannot hold
  * (spectral_transform.py:87-89): t[b,o,p] = sum_c w[o,c] * gate[b,c] * x[b,c,p], p < HW, plus
  * bn1 partials slab [B * ffc_pw_gate_blocks(HW)][M] float4 {n, mean, M2} (slab may be NULL).

@@ -57,6 +57,16 @@ def test_argument_validation_without_gpu():
     assert b"unsupported" in lib.ffc_last_error()
     rc = lib.ffc_conv_forward(None, 0, None, 0, 0, None)
     assert rc == -1
+    # ST prologue workgroups per sample: a power of two dividing conv1's output tiles
+    # (ceil32(c)/32 x ceil32(hw)/32), growing while the grid is below 256, at most 8
+    assert lib.ffc_st_prologue_split(32, 256, 8, 8, 1, 64) == 2     # 2 x 1 tiles
+    assert lib.ffc_st_prologue_split(32, 128, 16, 16, 1, 32) == 2   # 1 x 2 tiles
+    assert lib.ffc_st_prologue_split(32, 64, 32, 32, 1, 16) == 8    # 1 x 8 tiles
+    assert lib.ffc_st_prologue_split(256, 64, 32, 32, 1, 16) == 1   # the batch fills the GPU
+    assert lib.ffc_st_prologue_split(3, 16, 4, 4, 0, 16) == 1       # one tile
+    p = ctypes.c_void_p(16)   # never dereferenced: the split check fails first
+    rc = lib.ffc_st_prologue_ex(p, 4, 64, 32, 32, 1, None, None, 0, p, 16, 3, p, p, None, None)
+    assert rc == -1 and b"split" in lib.ffc_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

@@ -71,3 +71,38 @@ def test_folded_path_deterministic():
     assert torch.equal(a[0], b[0])
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+
+
+def _run_split(st, xs, split):
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.ST_SPLIT, rt.FU_PATH
+    rt.ST_SPLIT, rt.FU_PATH = split, "fused"
+    try:
+        with torch.no_grad():
+            outs = [st(x).clone() for x in xs]
+        torch.cuda.synchronize()
+    finally:
+        rt.ST_SPLIT, rt.FU_PATH = old
+    return outs, {k: v.detach().clone() for k, v in st.state_dict().items()}
+
+
+@pytest.mark.parametrize("cin,cout,hw,B", [(64, 128, 4, 8), (32, 32, 8, 5), (16, 16, 16, 3), (64, 32, 16, 32)])
+def test_st_prologue_split_matches_one_workgroup_per_sample(cin, cout, hw, B):
+    """ffc_st_prologue_ex over several workgroups per sample (each its share of conv1's output
+    tiles, B * split slab rows) against one workgroup per sample: the same outputs and BN buffers
+    up to the K-split summation order of conv1 (1e-6 normwise)"""
+    from fastfourierconvolution_amd import _lib
+    h = hw  # upsample=True: no pooling, conv1 on the input plane
+    assert _lib.load().ffc_st_prologue_split(B, cin, h, h, 0, cout // 2) > 1
+    base = _st(cin, cout, 0.1, seed=cin + hw + B)
+    g = torch.Generator().manual_seed(B)
+    xs = [torch.randn((B, cin, hw, hw), generator=g).cuda() for _ in range(2)]
+    ref_out, ref_sd = _run_split(copy.deepcopy(base), xs, False)
+    out, sd = _run_split(copy.deepcopy(base), xs, True)
+    for a, b in zip(out, ref_out):
+        assert normwise_err(a.double().cpu(), b.double().cpu()) <= 1e-6
+    for k, v in ref_sd.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(v), k
+        elif k.endswith("running_mean") or k.endswith("running_var"):
+            torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=k)
