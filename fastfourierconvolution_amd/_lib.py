@@ -90,7 +90,8 @@ class BnRfItem(ctypes.Structure):
 class BnApplyItem(ctypes.Structure):
     """ffc_bn_apply_item: one tensor of ffc_bn_act_apply_batch"""
     _fields_ = [("x", c_void_p), ("y", c_void_p), ("B", c_int), ("C", c_int), ("HW", c_int), ("scale", c_void_p),
-                ("shift", c_void_p), ("act", c_int), ("act_param", c_float), ("noise_w", c_void_p), ("noise", c_void_p)]
+                ("shift", c_void_p), ("act", c_int), ("act_param", c_float), ("noise_w", c_void_p), ("noise", c_void_p),
+                ("plane_sum", c_void_p)]
 
 
 # (name, restype, argtypes) for every entry point declared in include/ffc_amd.h
@@ -116,6 +117,8 @@ SIGNATURES = [
     ("ffc_bn_reduce_ws_doubles", c_size_t, [c_int, c_int]),
     ("ffc_bn_reduce_finalize_batch", c_int, [ctypes.POINTER(BnRfItem), c_int, c_void_p]),
     ("ffc_bn_act_apply_batch", c_int, [ctypes.POINTER(BnApplyItem), c_int, c_void_p]),
+    ("ffc_plane_chunks", c_int, [c_int]),
+    ("ffc_se_gate_sums", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_bn_reduce", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_bn_finalize", c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                 c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),

@@ -185,15 +185,19 @@ def _bn_finalize_batch(items, batch, device, stream):
 
 
 def bn_act_apply_batch(items):
-    """[(x, scale, shift, act, param, noise_w or None, noise or None)]: y = x in place, one launch
-    (ffc_bn_act_apply_batch; the l and g outputs of an FFC_BN_ACT, with fgan128's NoiseInjection)"""
+    """[(x, scale, shift, act, param, noise_w or None, noise or None[, plane_sum or None])]: y = x in
+    place, one launch (ffc_bn_act_apply_batch; the l and g outputs of an FFC_BN_ACT, with fgan128's
+    NoiseInjection).  plane_sum (B, C, ffc_plane_chunks(HW)) receives the chunk sums of y."""
     from ._lib import BnApplyItem
     arr = (BnApplyItem * len(items))()
     nbytes = 0.0
-    for k, (x, sc, sh, act, param, nw, nz) in enumerate(items):
+    for k, it in enumerate(items):
+        x, sc, sh, act, param, nw, nz = it[:7]
+        ps = it[7] if len(it) > 7 else None
         B, C = x.shape[:2]
         HW = x.numel() // (B * C)
-        arr[k] = BnApplyItem(ptr(x), ptr(x), B, C, HW, ptr(sc), ptr(sh), int(act), float(param), ptr(nw), ptr(nz))
+        arr[k] = BnApplyItem(ptr(x), ptr(x), B, C, HW, ptr(sc), ptr(sh), int(act), float(param), ptr(nw), ptr(nz),
+                             ptr(ps))
         nbytes += 8.0 * x.numel() + (4.0 * nz.numel() if nz is not None else 0.0)
     label = "bn_act_noise" if any(it[6] is not None for it in items) else "bn_act"
     with observe(label, bytes=nbytes):
@@ -252,6 +256,20 @@ BN_FOLD = __import__("os").environ.get("FFC_BN_FOLD", "1") != "0"
 # slab rows x channels up to which the fold beats the separate launch (each consumer workgroup
 # reads the whole slab; measured on MI355X, r02)
 BN_FOLD_MAX = int(__import__("os").environ.get("FFC_BN_FOLD_MAX", "4096"))
+# the SE means of a layer's global input taken from the previous layer's BN-apply pass (plane sums
+# written as it stores y) instead of a second read of y (FFC_SE_SUMS=0: se_mean_kernel)
+SE_SUMS = __import__("os").environ.get("FFC_SE_SUMS", "1") != "0"
+
+
+def plane_sums_for(x):
+    """(sums, chunks) attached to x by the BN-apply pass that wrote it, if x is unchanged since"""
+    at = getattr(x, "_ffc_plane_sums", None)
+    if at is None or not SE_SUMS:
+        return None
+    sums, chunks, version = at
+    return (sums, chunks) if x._version == version else None
+
+
 # the fused ST prologue over several workgroups per sample at small batches (FFC_ST_SPLIT=0: one)
 ST_SPLIT = __import__("os").environ.get("FFC_ST_SPLIT", "1") != "0"
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
@@ -462,7 +480,7 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT)
+            ST_SPLIT, SE_SUMS)
 
 
 def algorithmic_flops(plan) -> float:

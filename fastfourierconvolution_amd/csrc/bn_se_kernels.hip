@@ -440,6 +440,7 @@ struct ApplyBatch {
     const float* shift[FFC_MAX_BN_BATCH];
     const float* noise_w[FFC_MAX_BN_BATCH];
     const float4* noise[FFC_MAX_BN_BATCH];
+    float* psum[FFC_MAX_BN_BATCH];
     int C[FFC_MAX_BN_BATCH], HW4[FFC_MAX_BN_BATCH], chunks[FFC_MAX_BN_BATCH], act[FFC_MAX_BN_BATCH];
     float p[FFC_MAX_BN_BATCH];
     int off[FFC_MAX_BN_BATCH + 1];
@@ -462,6 +463,8 @@ __global__ __launch_bounds__(256) void bn_act_plane_batch_kernel(ApplyBatch a) {
     const float4* nz = a.noise[it] ? a.noise[it] + (size_t)b * HW4 : nullptr;
     const float4* x = a.x[it];
     float4* y = a.y[it];
+    float* const psum = a.psum[it];
+    float ts = 0.0f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const int i = chunk * PLANE_CHUNK4 + u * 256 + threadIdx.x;
@@ -477,7 +480,49 @@ __global__ __launch_bounds__(256) void bn_act_plane_batch_kernel(ApplyBatch a) {
                 r.w = fmaf(nw, n.w, r.w);
             }
             y[base + i] = r;
+            ts += (r.x + r.y) + (r.z + r.w);
         }
+    }
+    if (psum) {   // the chunk's sum of y: waves' halves (DPP), then the 8 half sums in a fixed order
+        __shared__ float hsum[8];
+        const float hs = ffc::half_wave_sum(ts);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0 || lane == 32) hsum[2 * wave + (lane >> 5)] = hs;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float s = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += hsum[k];
+            psum[(size_t)plane * chunks + chunk] = s;
+        }
+    }
+}
+
+// SE gate from the plane-chunk sums of ffc_bn_act_apply_batch: one block per sample
+__global__ void se_fc_sums_kernel(const float* __restrict__ sums, int chunks, int C, float inv,
+                                  const float* __restrict__ w1, const float* __restrict__ w2, int hid,
+                                  float* __restrict__ gate) {
+    extern __shared__ float sm[];
+    float* mean = sm;
+    float* hv = sm + C;
+    const int b = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float* q = sums + ((size_t)b * C + c) * chunks;
+        float s = 0.0f;
+        for (int k = 0; k < chunks; ++k) s += q[k];
+        mean[c] = s * inv;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < hid; j += blockDim.x) {
+        float s = 0.0f;
+        for (int c = 0; c < C; ++c) s = fmaf(w1[(size_t)j * C + c], mean[c], s);
+        hv[j] = fmaxf(s, 0.0f);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (int j = 0; j < hid; ++j) s = fmaf(w2[(size_t)c * hid + j], hv[j], s);
+        gate[(size_t)b * C + c] = 1.0f / (1.0f + expf(-s));
     }
 }
 
@@ -678,6 +723,7 @@ extern "C" int ffc_bn_act_apply_batch(const ffc_bn_apply_item* items, int n, voi
         const bool plane = t.HW % 4 == 0 && t.HW >= 256 &&
                            ((reinterpret_cast<uintptr_t>(t.x) | reinterpret_cast<uintptr_t>(t.y) |
                              reinterpret_cast<uintptr_t>(t.noise)) & 15) == 0;
+        FFC_CHECK_ARG(plane || !t.plane_sum, "ffc_bn_act_apply_batch: plane_sum needs HW % 4 == 0, HW >= 256, aligned");
         if (!plane) {   // the single forms' other paths
             const int rc = t.noise ? ffc_bn_act_noise_apply(t.x, t.y, t.B, t.C, t.HW, t.scale, t.shift, t.act,
                                                             t.act_param, t.noise_w, t.noise, stream)
@@ -693,6 +739,7 @@ extern "C" int ffc_bn_act_apply_batch(const ffc_bn_apply_item* items, int n, voi
         a.shift[k] = t.shift;
         a.noise_w[k] = t.noise ? t.noise_w : nullptr;
         a.noise[k] = reinterpret_cast<const float4*>(t.noise);
+        a.psum[k] = t.plane_sum;
         a.C[k] = t.C;
         a.HW4[k] = t.HW / 4;
         a.chunks[k] = (t.HW / 4 + PLANE_CHUNK4 - 1) / PLANE_CHUNK4;
@@ -706,4 +753,16 @@ extern "C" int ffc_bn_act_apply_batch(const ffc_bn_apply_item* items, int n, voi
     a.off[a.n] = (int)blocks;
     hipLaunchKernelGGL(bn_act_plane_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_bn_act_apply_batch");
+}
+
+extern "C" int ffc_plane_chunks(int HW) { return HW > 0 ? (HW / 4 + PLANE_CHUNK4 - 1) / PLANE_CHUNK4 : 0; }
+
+extern "C" int ffc_se_gate_sums(const float* sums, int chunks, int B, int C, int HW, const float* w1, const float* w2,
+                                int hidden, float* gate, void* stream) {
+    FFC_CHECK_ARG(sums && gate && B > 0 && C > 0 && HW > 0 && hidden >= 0 && chunks == ffc_plane_chunks(HW),
+                  "ffc_se_gate_sums: bad args");
+    FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_se_gate_sums: null weights");
+    hipLaunchKernelGGL(se_fc_sums_kernel, dim3(B), dim3(256), sizeof(float) * (C + hidden), (hipStream_t)stream, sums,
+                       chunks, C, 1.0f / (float)HW, w1, w2, hidden, gate);
+    return ffc::launch_status("ffc_se_gate_sums");
 }

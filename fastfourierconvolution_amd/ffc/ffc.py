@@ -346,13 +346,22 @@ class _FFCExec:
                 outs[name] = rt.PendingAct(out, sc, sh, act[0], act[1], *(nz if nz is not None else (None, None)))
                 done.add(name)
                 continue
-            if nz is not None and out.shape[2] * out.shape[3] % 4 == 0:
+            # the global output's plane sums for the next layer's SE gate (large planes, where the
+            # SpectralTransform reads y twice otherwise: spectral_transform.py pw path)
+            HW = out.shape[2] * out.shape[3]
+            ps = None
+            if name == "g" and rt.SE_SUMS and HW % 4 == 0 and HW >= 256:
+                chunks = rt.lib().ffc_plane_chunks(HW)
+                ps = torch.empty((out.shape[0], out.shape[1], chunks), device=dev, dtype=torch.float32)
+            if nz is not None and HW % 4 == 0:
                 # the noise drawn here, in branch order, as the single pass does; applied below
                 p = rt.PendingAct(out, sc, sh, act[0], act[1], *nz)
-                applies.append((out, sc, sh, act[0], act[1], p.noise_w, p.noise))
+                applies.append((out, sc, sh, act[0], act[1], p.noise_w, p.noise, ps))
                 done.add(name)
             else:
-                applies.append((out, sc, sh, act[0], act[1], None, None))
+                applies.append((out, sc, sh, act[0], act[1], None, None, ps))
+            if ps is not None:
+                out._ffc_plane_sums = (ps, chunks, out._version)
         if applies:   # the layer's BN + activation (+ noise) passes in one launch
             rt.bn_act_apply_batch(applies)
         for name, (mod, n) in noise.items():   # branches without a BN/activation pass of their own

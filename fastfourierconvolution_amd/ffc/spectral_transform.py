@@ -45,6 +45,12 @@ class SELayer(nn.Module):
         w1 = rt.require(self.fc[0].weight.detach(), "se.fc.0.weight") if hid > 0 else None
         w2 = rt.require(self.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None
         g = torch.empty((B, C), device=x.device, dtype=torch.float32)
+        ps = None if pool else rt.plane_sums_for(x)
+        if ps is not None:   # plane sums from the BN-apply pass that wrote x: no second read of x
+            with rt.observe("se_gate"):
+                check(rt.lib().ffc_se_gate_sums(ptr(ps[0]), ps[1], B, C, H * W, ptr(w1), ptr(w2), hid, ptr(g),
+                                                rt.stream_of(x)), "ffc_se_gate_sums")
+            return g
         with rt.observe("se_gate", bytes=4.0 * x.numel()):
             check(rt.lib().ffc_se_gate(ptr(x), B, C, H, W, int(pool), ptr(w1), ptr(w2), hid, ptr(g), rt.stream_of(x)),
                 "ffc_se_gate")

@@ -285,8 +285,16 @@ typedef struct ffc_bn_apply_item {    /* ffc_bn_act_noise_apply arguments (noise
     float act_param;
     const float* noise_w;
     const float* noise;
+    float* plane_sum;   /* optional [B][C][ffc_plane_chunks(HW)]: the sums of y over each chunk of each
+                           plane (the SE means of the next layer without a second read of y); needs
+                           HW % 4 == 0, HW >= 256 and 16-byte aligned x / y / noise */
 } ffc_bn_apply_item;
 int ffc_bn_act_apply_batch(const ffc_bn_apply_item* items, int n, void* stream);
+int ffc_plane_chunks(int HW);
+/* SELayer gate from ffc_bn_act_apply_batch's plane sums (spectral_transform.py:12-28):
+ * mean[b][c] = sum_k sums[b][c][k] / HW (k < chunks, fixed order), then the FCs as ffc_se_gate. */
+int ffc_se_gate_sums(const float* sums, int chunks, int B, int C, int HW, const float* w1, const float* w2,
+                     int hidden, float* gate, void* stream);
 
 /* ------------------------------------------------------------------ spectral branch
  * SELayer gate (spectral_transform.py:12-28): gate[b][c] = sigmoid(W2 relu(W1 mean_hw x)),
