@@ -272,6 +272,7 @@ def plane_sums_for(x):
 
 # the fused ST prologue over several workgroups per sample at small batches (FFC_ST_SPLIT=0: one)
 ST_SPLIT = __import__("os").environ.get("FFC_ST_SPLIT", "1") != "0"
+ST_SPLIT_MAX = int(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "8"))   # cap (a power of two)
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
 FU_SPILL = __import__("os").environ.get("FFC_FU_SPILL", "1") != "0"
 
@@ -480,7 +481,7 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT, SE_SUMS)
+            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS)
 
 
 def algorithmic_flops(plan) -> float:
