@@ -229,14 +229,16 @@ def fgan_cpu_baseline(args, G, z_cpu, sn):
     return cpu, parity
 
 
-def sharded_parity(args, step, cpu_state, z_glob, global_batch, rank):
+def sharded_parity(args, step, cpu_state, z_glob, global_batch, rank, timed_out=None):
     """N > 1 (gen64, train-mode BN; every rank calls it): one more sharded forward on every rank,
     outputs gathered to the global batch (all_gather over RCCL), compared on rank 0 with the fp32
     CPU reference path run on the global z.  This checks the SyncBN all-reduces end to end: a naive
     shard differs from the global-batch forward by ~3e-1 normwise.  (Eval mode
     needs the GPU's running stats and no collective: the caller skips it on every rank.)"""
     from fastfourierconvolution_amd.distributed import gather_batch
-    out = gather_batch(step().contiguous(), global_batch)
+    torch.cuda.synchronize()
+    mine = timed_out if timed_out is not None else step()   # the graph's output after the timed replays
+    out = gather_batch(mine.contiguous(), global_batch)
     if rank != 0:
         return None
     from oracle.ffc_oracle import ffc_generator, normwise_err
@@ -245,7 +247,9 @@ def sharded_parity(args, step, cpu_state, z_glob, global_batch, rank):
         ref = ffc_generator(z_glob, {k: v.clone() for k, v in cpu_state.items()}, args.nz, args.nc, args.ngf,
                             args.bn_mode == "train", fft="torch")
     return {"normwise_err_vs_cpu_ref": normwise_err(out.cpu(), ref), "mode": f"train, global B={global_batch}, "
-            "sharded + SyncBN, outputs gathered", "tolerance": 1e-4}
+            "sharded + SyncBN, outputs gathered", "tolerance": 1e-4,
+            "checked": "captured hipGraphs' outputs after the timed replays" if timed_out is not None else
+            "eager forward"}
 
 
 def weights_init(m):
@@ -820,8 +824,11 @@ def main():
     # ---- CPU baseline + parity (rank 0, N=1 only); N > 1: the gathered sharded output (SyncBN)
     cpu = None
     parity = None
+    # the timed artifact: the captured graph's static output after the timed replays (train-mode
+    # BN: every replay computes the same output from the batch's own statistics)
+    timed_out = getattr(graph, "ffc_output", None) if use_graph else None
     if world > 1 and not fgan and args.bn_mode == "train" and not args.no_cpu_baseline:
-        parity = sharded_parity(args, step, cpu_state, z_glob, global_batch, rank)
+        parity = sharded_parity(args, step, cpu_state, z_glob, global_batch, rank, timed_out)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and fgan:
         cpu, parity = fgan_cpu_baseline(args, G, z_cpu, sn)
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -840,9 +847,14 @@ def main():
                 iters += 1
             cpu_el = time.perf_counter() - t0
         with torch.no_grad():
-            gpu_out = step().cpu()
+            if timed_out is not None and training:
+                torch.cuda.synchronize()
+                gpu_out, source = timed_out.cpu(), "captured hipGraph's output after the timed replays"
+            else:   # eval mode: the profile pass moved nothing, any forward is the timed one
+                gpu_out, source = step().cpu(), "eager forward" if timed_out is None else \
+                    "eager forward (eval-mode BN: the same kernels and running statistics as the graph)"
         parity = {"normwise_err_vs_cpu_ref": normwise_err(gpu_out, ref),
-                  "max_abs_diff": float((gpu_out - ref).abs().max()), "tolerance": 1e-4}
+                  "max_abs_diff": float((gpu_out - ref).abs().max()), "tolerance": 1e-4, "checked": source}
         cpu = {"value": round(args.batch * (iters - 1) / cpu_el, 2), "unit": "images/s", "cores": threads,
                "kind": "port",
                "sample": f"oracle fp32 torch-CPU FFCGenerator fwd (op-for-op reference path), B={args.batch}, "

@@ -226,7 +226,10 @@ def channel_sum(g):
 # spec (JSON): {"outs": [[M, act, param], ...], "edges": [[j, i, kind, k, s, p, d, op, layout, bias], ...]}:
 # output j = act_j(sum over its edges of conv(kind, k, s, p, d, op)(xs[i]) with ws[e] (+ bs[bias])).
 # Shapes come from the tensors, so one spec serves every batch size.
-_CL_CACHE = {}   # plans / packed weights of every conv_layer op, keyed by (spec, shapes)
+# plans / packed weights of every conv_layer op, keyed by (spec, shapes): a pool of caches, each
+# held by one caller at a time (rt.StreamPool: a plan's packed weights and split-K partials are
+# written on its holder's stream)
+_CL_POOL = rt.StreamPool(dict)
 
 
 @functools.lru_cache(maxsize=4096)
@@ -276,8 +279,9 @@ def conv_layer_impl(xs, ws, bs, spec):
         wts = [(ws[e], edges[e][8], edges[e][3], edges[e][3], bs[edges[e][9]] if edges[e][9] >= 0 else None)
                for e in es]
         fused = act if act != 5 else 0
-        y = conv_forward(_CL_CACHE, ("fwd", spec, j, B, sgs), B, M, sgs, wts, [xs[edges[e][1]] for e in es],
-                         act=(fused, param))
+        with _CL_POOL.hold() as cache:
+            y = conv_forward(cache, ("fwd", spec, j, B, sgs), B, M, sgs, wts, [xs[edges[e][1]] for e in es],
+                             act=(fused, param))
         if act == 5:
             pres.append(y)
             y = _act_out(y, act, param, _stream(y))
@@ -323,8 +327,9 @@ def conv_layer_backward_impl(xs, ws, ts, gouts, needs, spec):
             segs = tuple(a[1] for a in grp)
             wts = [(ws[a[0]].contiguous(), 1 - a[2], a[1].k, a[1].k, None) for a in grp]
             key = ("adj", spec, i, tuple(a[0] for a in grp), B, C, segs)
-            dx = conv_forward(_CL_CACHE, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
-                              addend=dx)
+            with _CL_POOL.hold() as cache:
+                dx = conv_forward(cache, key, B, C, segs, wts, [a[3] for a in grp], out_shape=tuple(x.shape),
+                                  addend=dx)
         grads[i] = dx
     for e, ed in enumerate(edges):
         j, i, kind, k, s, p, d = ed[:7]
@@ -408,7 +413,10 @@ def bn_update_running_impl(running_mean, running_var, num_batches_tracked, stats
 
 def bn_act_backward_impl(x, dy, scale, shift, stats, gamma, use_batch, sync, eps, act, param, need_dx, has_gamma,
                          has_beta):
-    """ffc::bn_act_backward -> [dx, dgamma, dbeta] (empty tensors where not needed / absent)"""
+    """ffc::bn_act_backward -> [dx, dgamma, dbeta] (empty tensors where not needed / absent).
+    x is the op's raw input (the saved tensor, not the forward's contiguous copy): the kernels read
+    and write dense NCHW, so x is made contiguous here and dx is allocated NCHW-contiguous"""
+    x = x.contiguous()
     dy = dy.contiguous()
     B, C = x.shape[:2]
     HW = x[0, 0].numel()
@@ -488,7 +496,9 @@ def se_scale_impl(x, w1, w2):
 
 
 def se_scale_backward_impl(x, dy, w1, w2):
-    """ffc::se_scale_backward -> [dx, dw1, dw2]"""
+    """ffc::se_scale_backward -> [dx, dw1, dw2] (x as saved by the op: made contiguous, as the forward's
+    rt.require copy was)"""
+    x = x.contiguous()
     dy = dy.contiguous()
     B, C, H, W = x.shape
     hid = w1.shape[0]
@@ -558,6 +568,9 @@ def noise_wgrad_impl(g, noise):
     """ffc::noise_wgrad: dweight[c] = sum g[:, c] * noise -> (1, C, 1, 1)"""
     g = g.contiguous()
     B, C, H, W = g.shape
+    noise = noise.contiguous()   # the saved op input: a strided view (e.g. n[:, :1]) reads as dense (B, 1, H, W)
+    if tuple(noise.shape) != (B, 1, H, W):
+        raise RuntimeError(f"noise must be {(B, 1, H, W)}, got {tuple(noise.shape)}")
     dw = torch.empty(C, device=g.device, dtype=torch.float32)
     check(rt.lib().ffc_noise_wgrad(ptr(g), ptr(noise), B, C, H * W, ptr(dw), _stream(g)), "ffc_noise_wgrad")
     return dw.view(1, C, 1, 1)
@@ -569,7 +582,7 @@ def noise_inject(mod, x, noise=None):
     B, C, H, W = x.shape
     if noise is None:
         noise = x.new_empty(B, 1, H, W).normal_()
-    return torch.ops.ffc.noise_inject(x, mod.weight, noise)
+    return torch.ops.ffc.noise_inject(x, mod.weight, rt.require(noise, "noise"))
 
 
 class _LinearAs1x1:

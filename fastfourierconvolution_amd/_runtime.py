@@ -272,7 +272,15 @@ def plane_sums_for(x):
 
 # the fused ST prologue over several workgroups per sample at small batches (FFC_ST_SPLIT=0: one)
 ST_SPLIT = __import__("os").environ.get("FFC_ST_SPLIT", "1") != "0"
-ST_SPLIT_MAX = int(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "8"))   # cap (a power of two)
+
+
+def _pow2_floor(v: int) -> int:
+    """the largest power of two <= max(v, 1) (the prologue split must divide conv1's tile count)"""
+    v = max(int(v), 1)
+    return 1 << (v.bit_length() - 1)
+
+
+ST_SPLIT_MAX = _pow2_floor(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "8"))   # cap, rounded to 2^k
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
 FU_SPILL = __import__("os").environ.get("FFC_FU_SPILL", "1") != "0"
 
@@ -457,6 +465,76 @@ def _wkey(ts):
     return tuple(weight_key(t) for t in ts)
 
 
+class StreamPool:
+    """Objects that own device buffers (layer templates with their plan caches, packed weights and
+    split-K partials; the conv_layer plan cache) handed to ONE caller at a time.
+
+    Concurrent callers -- nn.DataParallel-style threads, each on its own stream (SURVEY.md §8b
+    "Threading", /root/reference/train_cond.py:66-68) -- get different objects, and the pool's lock
+    covers only the check-out and the return, never the launches.  An object's previous holder may
+    have been another thread whose kernels are still queued on ITS stream and read or write the
+    object's buffers, so a caller that takes an object last used by another thread makes its current
+    stream wait for that stream first.  One thread alone never records or waits on anything (graph
+    capture and the timed loops are unaffected)."""
+
+    def __init__(self, factory):
+        import threading
+        self._factory = factory
+        self._free, self._all = [], []
+        self._lock = threading.Lock()
+        self._last = {}   # id(object) -> (thread id, stream) of its previous holder
+
+    def take(self):
+        import threading
+        me = threading.get_ident()
+        with self._lock:
+            obj = self._free.pop() if self._free else None
+        if obj is None:
+            obj = self._factory()   # built outside the lock (only this caller can see it)
+            with self._lock:
+                self._all.append(obj)
+        last = self._last.get(id(obj))
+        if last is not None and last[0] != me:
+            torch.cuda.current_stream().wait_stream(last[1])
+        return obj
+
+    def give(self, obj):
+        import threading
+        if torch.cuda.is_initialized():
+            self._last[id(obj)] = (threading.get_ident(), torch.cuda.current_stream())
+        with self._lock:
+            self._free.append(obj)
+
+    @property
+    def instances(self) -> int:
+        return len(self._all)
+
+    def first(self):
+        """an object of the pool for read-only inspection (built if none exists yet)"""
+        with self._lock:
+            if self._all:
+                return self._all[0]
+        obj = self.take()
+        self.give(obj)
+        return obj
+
+    class _Hold:
+        def __init__(self, pool):
+            self.pool = pool
+
+        def __enter__(self):
+            self.obj = self.pool.take()
+            return self.obj
+
+        def __exit__(self, *exc):
+            self.pool.give(self.obj)
+            return False
+
+    def hold(self):
+        """``with pool.hold() as obj:`` -- obj held exclusively for the block"""
+        return StreamPool._Hold(self)
+
+
 class PackCache:
     """a few packed forms of weights, keyed by weight_key of their sources (FIFO-bounded)"""
 
@@ -594,17 +672,56 @@ class ConvExec:
         self.device = device
         self.ktab = torch.from_numpy(self.plan.ktab.copy()).to(device)
         # + tail padding: the patch kernel loads all 4 tap groups of a chunk, used or not
-        self.A = torch.zeros(max(1, self.plan.a_size) + 256, device=device, dtype=torch.float32)
+        self.a_floats = max(1, self.plan.a_size) + 256
         # split-bf16 patch conv: A pre-split into three exact bf16 planes (ffc_split_bf16) after every
         # pack, so the kernel loads the pieces instead of splitting each chunk's A in registers
-        self.a3_stride = -(-self.A.numel() // 8) * 8
-        self.A3 = (torch.zeros(3 * self.a3_stride, device=device, dtype=torch.int16)
-                   if self.kind == "patch" and CONV_ARITH == "split" and (PRESPLIT_A or self.plan.q) else None)
+        self.a3_stride = -(-self.a_floats // 8) * 8
+        self.use_a3 = self.kind == "patch" and CONV_ARITH == "split" and (PRESPLIT_A or self.plan.q)
         self.has_bias = any(w[4] is not None for w in weights)
-        self.bias = torch.empty(M, device=device, dtype=torch.float32) if self.has_bias else None
+        self.M = M
+        # packed buffers per weight identity: modules of one structure share this plan,
+        # and alternating them must neither re-pack every call nor overwrite a buffer in use
+        self._slots = {}   # identity -> (key, A, A3, bias)
         self._packed = None
+        self.A = self.A3 = self.bias = None
         self.flops = algorithmic_flops(self.plan)
         self.ensure_packed(weights)
+
+    PACK_SLOTS = 4   # distinct weight sets kept packed per plan
+
+    def _new_buffers(self):
+        A = torch.zeros(self.a_floats, device=self.device, dtype=torch.float32)
+        A3 = torch.zeros(3 * self.a3_stride, device=self.device, dtype=torch.int16) if self.use_a3 else None
+        bias = torch.empty(self.M, device=self.device, dtype=torch.float32) if self.has_bias else None
+        return A, A3, bias
+
+    def check_launch(self, inputs, out, addend=None):
+        """host-side launch guard: the tensors must have exactly the extents this plan was made for.
+        The C ABI takes raw pointers and cannot check them, so a plan reused for another shape (a
+        cache-key collision: DESIGN.md §10b) would write past ``out`` instead of failing."""
+        pl = self.plan
+        want = (pl.B, pl.M, pl.OH, pl.OW)
+
+        def fits(t, n):   # (B, ...) fp32, dense, exactly n elements (a view such as (B, M, k, k) for
+            return (t.dim() >= 1 and t.shape[0] == pl.B and t.numel() == n and t.is_contiguous()   # (B, M k k, 1, 1)
+                    and t.dtype == torch.float32)
+        n_out = pl.B * pl.M * pl.OH * pl.OW
+        if not fits(out, n_out):
+            raise FFCError(f"conv launch guard: output {tuple(out.shape)} ({out.dtype}, contiguous="
+                           f"{out.is_contiguous()}) does not match the plan's {want}")
+        if addend is not None and not fits(addend, n_out):
+            raise FFCError(f"conv launch guard: addend {tuple(addend.shape)} does not match the plan's {want}")
+        if len(inputs) != len(pl.segs):
+            raise FFCError(f"conv launch guard: {len(inputs)} inputs for {len(pl.segs)} segments")
+        for i, ((x, gate), sg) in enumerate(zip(inputs, pl.segs)):
+            n_in = pl.B * sg.C * sg.IH * sg.IW * (4 if sg.pool else 1)   # pooled: the 2x2-pool input
+            if not fits(x, n_in):
+                raise FFCError(f"conv launch guard: segment {i} input {tuple(x.shape)} (contiguous="
+                               f"{x.is_contiguous()}) does not match the plan's ({pl.B}, {sg.C}, "
+                               f"{sg.IH * (2 if sg.pool else 1)}, {sg.IW * (2 if sg.pool else 1)})")
+            if gate is not None and gate.numel() != pl.B * sg.C:
+                raise FFCError(f"conv launch guard: segment {i} gate has {gate.numel()} values, "
+                               f"the plan needs {pl.B * sg.C}")
 
     def pack_job(self):
         """ffc_conv_job describing the packed-weight layout (used by ffc_conv_pack for both kinds)"""
@@ -667,6 +784,23 @@ class ConvExec:
         key = _wkey([w[0] for w in weights] + [w[4] for w in weights])
         if key == self._packed:
             return
+        # identity = the weight objects (pointer, epoch) without their versions: an updated weight
+        # re-packs into its own slot, another model's weights get a slot of their own
+        ident = tuple(None if k is None else (k[0], k[2]) for k in key)
+        slot = self._slots.pop(ident, None)
+        if slot is not None and slot[0] == key:
+            self._slots[ident] = slot
+            _, self.A, self.A3, self.bias = slot
+            self._packed = key
+            return
+        if slot is not None:
+            bufs = slot[1:]
+        elif len(self._slots) >= self.PACK_SLOTS:
+            bufs = self._slots.pop(next(iter(self._slots)))[1:]   # oldest slot's buffers
+        else:
+            bufs = self._new_buffers()
+        self.A, self.A3, self.bias = bufs
+        self._slots[ident] = (key,) + tuple(bufs)
         n = len(weights)
         job = self.pack_job()
         wp = (ctypes.c_void_p * _lib.MAX_SEG)(*[w[0].data_ptr() for w in weights], *([None] * (_lib.MAX_SEG - n)))
@@ -687,6 +821,7 @@ class ConvExec:
         self._packed = key
 
     def job(self, inputs, out, act=0, act_param=0.0, addend=None, stats=None):
+        self.check_launch(inputs, out, addend)
         job = self.base_job()
         for i, (x, gate) in enumerate(inputs):
             if self.kind == "patch" and self.plan.vec4[i] and x.data_ptr() % 16:

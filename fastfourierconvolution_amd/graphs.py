@@ -52,7 +52,8 @@ def _forced_failure() -> bool:
 
 def capture_step(step, group=None, warmup: int = 1, capture=None):
     """Warm ``step`` up on a side stream, synchronise, capture it into a CUDAGraph (thread-local
-    mode) and return the graph -- or None on EVERY rank if any rank's capture failed.  ``capture``
+    mode) and return the graph (``graph.ffc_output``: what the captured step returned, rewritten by
+    every replay) -- or None on EVERY rank if any rank's capture failed.  ``capture``
     replaces the capture itself (``capture(step) -> graph``; CPU tests)."""
     graph, err = None, None
     try:
@@ -70,7 +71,10 @@ def capture_step(step, group=None, warmup: int = 1, capture=None):
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-                step()
+                out = step()
+            # the captured step's output tensors: every replay rewrites them in place (bench.py
+            # checks the timed artifact itself against the oracle after the timed replays)
+            g.ffc_output = out
             graph = g
     except Exception as e:          # capture unsupported here: the caller times eagerly
         err = e

@@ -352,12 +352,13 @@ def linear(z: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
     rt.note_tensors([weight, bias])
     w = rt.require(weight.detach(), "weight")
     b = rt.require(bias.detach(), "bias") if bias is not None else None
-    Wt = _PACKS.get("linearT", [w], lambda: w.t().contiguous())
-    B = z.shape[0]
-    out = torch.empty((B, N), device=z.device, dtype=torch.float32)
-    with rt.observe("dense", flops=2.0 * B * K * N):
-        rt.check(rt.lib().ffc_dense_forward(rt.ptr(z), rt.ptr(Wt), rt.ptr(b), B, K, N, N, rt.ptr(out), None, 0, 0.0,
-                                            rt.stream_of(z)), "ffc_dense_forward")
+    with _PACKS.hold() as packs:
+        Wt = packs.get("linearT", [w], lambda: w.t().contiguous())
+        B = z.shape[0]
+        out = torch.empty((B, N), device=z.device, dtype=torch.float32)
+        with rt.observe("dense", flops=2.0 * B * K * N):
+            rt.check(rt.lib().ffc_dense_forward(rt.ptr(z), rt.ptr(Wt), rt.ptr(b), B, K, N, N, rt.ptr(out), None, 0,
+                                                0.0, rt.stream_of(z)), "ffc_dense_forward")
     return out
 
 
@@ -366,7 +367,7 @@ def _(z, weight, bias):
     return z.new_empty((z.shape[0], weight.shape[0]))
 
 
-_PACKS = rt.PackCache(64)
+_PACKS = rt.StreamPool(lambda: rt.PackCache(64))   # transposed Linear weights
 
 
 @torch.library.custom_op("ffc::quantize_u8", mutates_args=())
@@ -460,7 +461,6 @@ class _Template:
         self._slots = [self._slot(mod, n, "_parameters") for n in self.param_names] + \
                       [self._slot(mod, n, "_buffers") for n in self.buffer_names]
         self._meta = [getattr(sub, kind)[leaf] for sub, kind, leaf in self._slots]
-        self.lock = threading.RLock()
 
     @staticmethod
     def _slot(mod, name, kind):
@@ -469,30 +469,57 @@ class _Template:
 
     @contextlib.contextmanager
     def bound(self, params, buffers):
-        """the template with the op's tensors in place of its parameters and buffers"""
+        """this instance with the op's tensors in place of its parameters and buffers (the caller
+        holds the instance exclusively: _TemplatePool.bound)"""
         ts = list(params) + list(buffers)
         if len(ts) != len(self._slots):
             raise RuntimeError(f"layer op: {len(ts)} tensors for {len(self._slots)} slots")
-        rt.note_tensors(params)
-        with self.lock:
-            for (sub, kind, leaf), t in zip(self._slots, ts):
+        for (sub, kind, leaf), t in zip(self._slots, ts):
+            getattr(sub, kind)[leaf] = t
+        try:
+            yield self.module
+        finally:
+            for (sub, kind, leaf), t in zip(self._slots, self._meta):
                 getattr(sub, kind)[leaf] = t
-            try:
-                yield self.module
-            finally:
-                for (sub, kind, leaf), t in zip(self._slots, self._meta):
-                    getattr(sub, kind)[leaf] = t
 
 
-def template(spec: str) -> _Template:
-    """the spec's template under the current plan switches (rt.plan_knobs: the templates' plan caches
-    are made under them)"""
+class _TemplatePool:
+    """the template instances of one spec (an rt.StreamPool).  A layer op checks an instance out for
+    the whole forward -- binding, launches, unbinding -- and returns it afterwards; the pool's lock
+    covers only the check-out and the return.  Concurrent callers (nn.DataParallel-style threads,
+    each on its own stream: SURVEY.md §8b "Threading", /root/reference/train_cond.py:66-68) therefore
+    run on different instances, and an instance's plan caches, packed weights and split-K partial
+    buffers (all kept on its modules) are used by one thread at a time, in stream order."""
+
+    def __init__(self, spec: str):
+        self.spec = spec
+        self.pool = rt.StreamPool(lambda: _Template(spec))
+        first = self.pool.first()
+        # structure shared by every instance (fake impls, layer_tensors)
+        self.kind, self.module = first.kind, first.module
+        self.param_names, self.buffer_names = first.param_names, first.buffer_names
+
+    @property
+    def instances(self) -> int:
+        return self.pool.instances
+
+    @contextlib.contextmanager
+    def bound(self, params, buffers):
+        """a template instance of this spec held exclusively, with the op's tensors bound in"""
+        rt.note_tensors(params)
+        with self.pool.hold() as inst, inst.bound(params, buffers) as m:
+            yield m
+
+
+def template(spec: str) -> _TemplatePool:
+    """the spec's template pool under the current plan switches (rt.plan_knobs: the templates' plan
+    caches are made under them)"""
     return _template(spec, rt.plan_knobs())
 
 
 @functools.lru_cache(maxsize=512)
-def _template(spec: str, knobs) -> _Template:
-    return _Template(spec)
+def _template(spec: str, knobs) -> _TemplatePool:
+    return _TemplatePool(spec)
 
 
 def layer_tensors(m: nn.Module, spec: str):

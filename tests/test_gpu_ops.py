@@ -143,3 +143,121 @@ def test_two_models_same_structure_do_not_share_packed_weights():
         del g
         torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[2]) and not torch.equal(outs[0], outs[1])
+
+
+# --------------------------------------------------------------------------- round 5: ADVICE r04 regressions
+def test_noise_wgrad_strided_noise():
+    """ffc::noise_inject saves the caller's noise; a strided view (a channel slice of a wider tensor)
+    must give the same weight gradient as its dense copy (noise_wgrad assumed dense)"""
+    from fastfourierconvolution_amd.layers_misc import NoiseInjection
+    mod = NoiseInjection(8).to(DEV)
+    with torch.no_grad():
+        mod.weight.copy_(torch.randn_like(mod.weight))
+    x = torch.randn(4, 8, 16, 16, device=DEV)
+    wide = torch.randn(4, 3, 16, 16, device=DEV)
+    g = torch.randn(4, 8, 16, 16, device=DEV)
+    grads = []
+    for n in (wide[:, 1:2], wide[:, 1:2].contiguous()):
+        mod.weight.grad = None
+        xs = x.clone().requires_grad_()
+        y = torch.ops.ffc.noise_inject(xs, mod.weight, n)
+        (y * g).sum().backward()
+        grads.append(mod.weight.grad.clone())
+    assert not wide[:, 1:2].is_contiguous()
+    assert torch.equal(grads[0], grads[1])
+    ref = (g * wide[:, 1:2]).sum(dim=(0, 2, 3)).view_as(grads[0])
+    torch.testing.assert_close(grads[0], ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("op", ["bn_act", "se_scale"])
+def test_backward_channels_last_input(op):
+    """ffc::bn_act / ffc::se_scale called directly with a channels_last x: dx and the parameter
+    gradients equal those of the same values in NCHW (the backward read the saved raw x)"""
+    x0 = torch.randn(4, 32, 8, 8, device=DEV)
+    dy = torch.randn(4, 32, 8, 8, device=DEV)
+    res = []
+    for x in (x0.clone(), x0.clone().to(memory_format=torch.channels_last)):
+        x.requires_grad_()
+        if op == "bn_act":
+            gm = torch.ones(32, device=DEV).requires_grad_()
+            bt = torch.zeros(32, device=DEV).requires_grad_()
+            y = torch.ops.ffc.bn_act(x, gm, bt, None, None, True, 1e-5, 2, 0.1)[0]
+            params = (gm, bt)
+        else:
+            gm = (0.3 * torch.randn(2, 32, device=DEV)).requires_grad_()
+            bt = (0.3 * torch.randn(32, 2, device=DEV)).requires_grad_()
+            y = torch.ops.ffc.se_scale(x, gm, bt)
+            params = (gm, bt)
+        (y * dy).sum().backward()
+        res.append([x.grad.contiguous()] + [p.grad.clone() for p in params])
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+# --------------------------------------------------------------------------- round 5: threaded callers
+def test_threaded_replicas_bitwise_equal_serial():
+    """SURVEY.md §8b "Threading": nn.DataParallel runs module replicas concurrently, one thread each
+    (/root/reference/train_cond.py:66-68).  Two threads, each with its own FFCGenerator replica and
+    its own stream on cuda:0, run forwards concurrently: every output is bitwise equal to the same
+    replica's serial run, and the two threads held different template instances (ops._TemplatePool:
+    no plan cache or packed-weight buffer is shared across threads)."""
+    import threading
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import ops
+    reps, zs = [], []
+    for seed in (11, 12):
+        torch.manual_seed(seed)
+        g = _quiet(F.FFCGenerator, 100, 3, 32).to(DEV).train()
+        reps.append(g)
+        zs.append(torch.randn(24, 100, 1, 1, device=DEV))
+    n_iter = 6
+    # serial references: a fresh copy of each replica's state (train-mode BN moves the running stats)
+    init = [{k: v.clone() for k, v in g.state_dict().items()} for g in reps]
+    serial = []
+    with torch.no_grad():
+        for g, z in zip(reps, zs):
+            serial.append([g(z).clone() for _ in range(n_iter)])
+    torch.cuda.synchronize()
+    after_serial = [{k: v.clone() for k, v in g.state_dict().items()} for g in reps]
+    for g, sd in zip(reps, init):
+        g.load_state_dict(sd)
+    torch.cuda.synchronize()
+    held = {}
+    orig_take = ops._TemplatePool._take
+
+    def spy_take(self):
+        inst = orig_take(self)
+        held.setdefault(threading.get_ident(), set()).add(id(inst))
+        return inst
+    ops._TemplatePool._take = spy_take
+    outs = [[None] * n_iter for _ in reps]
+    errors = []
+    bar = threading.Barrier(2)
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s), torch.no_grad():
+                bar.wait()
+                for i in range(n_iter):
+                    outs[k][i] = reps[k](zs[k]).clone()
+            s.synchronize()
+        except Exception as e:   # reported by the main thread
+            errors.append(e)
+    try:
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=120)
+    finally:
+        ops._TemplatePool._take = orig_take
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for k in range(2):
+        for i in range(n_iter):
+            assert torch.equal(outs[k][i], serial[k][i]), (k, i)
+        for key, v in reps[k].state_dict().items():
+            assert torch.equal(v, after_serial[k][key]), key
+    ids = list(held.values())
+    assert len(ids) == 2 and not (ids[0] & ids[1]), "the two threads shared a template instance"

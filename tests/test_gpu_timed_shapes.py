@@ -255,3 +255,74 @@ def test_block_config0_b16(mode):
         for k, v in blk.state_dict().items():
             if k.endswith(("running_mean", "running_var")):
                 assert normwise_err(v.cpu(), sd[k]) <= TOL, k
+
+
+# --------------------------------------------------------------------------- round 5: the timed artifact itself
+def test_gen64_train_graph_replays_vs_oracle():
+    """bench.py's timed artifact: the train-mode B = 256 generator forward captured into one hipGraph
+    (graphs.capture_step, as bench.py captures it: one warm-up on a side stream, then the capture)
+    and replayed twice.  The graph's static output after the replays equals the fp64 oracle's train
+    forward, and the BN running statistics / num_batches_tracked advanced exactly as three
+    nn.BatchNorm2d train steps on the same batch (warm-up + 2 replays; the capture runs nothing):
+    the in-graph BN slab resets and folds are checked, not just an eager forward
+    (/root/reference/models/ffc_generator.py:30-44)."""
+    from fastfourierconvolution_amd.graphs import capture_step
+    G = _gen64()
+    sd = _sd64(G)
+    G = G.cuda().train()
+    z = torch.randn((256, 100, 1, 1), generator=torch.Generator().manual_seed(100)).cuda()
+
+    def step():
+        with torch.no_grad():
+            return G(z)
+    graph = capture_step(step, warmup=1)
+    assert graph is not None and getattr(graph, "ffc_output", None) is not None
+    out = graph.ffc_output
+    with torch.no_grad():
+        out.fill_(float("nan"))
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    got = out.cpu()
+    with torch.no_grad():
+        for _ in range(3):
+            ref = ffc_generator(z.cpu().double(), sd, 100, 3, 64, True)
+    err = normwise_err(got, ref)
+    print(f"gen64 train B=256 graph replay: {err:.2e}")
+    assert err <= TOL, err
+    gsd = G.state_dict()
+    n_bn = 0
+    for k, v in sd.items():
+        if k.endswith(("running_mean", "running_var")):
+            torch.testing.assert_close(gsd[k].cpu().double(), v, rtol=2e-4, atol=1e-5, msg=k)
+            n_bn += 1
+        elif k.endswith("num_batches_tracked"):
+            assert int(gsd[k]) == int(v) == 3, k
+    assert n_bn == 12   # bn1 + fu.bn of ffc1..ffc3, mean and var each
+
+
+def test_fgan128_full_job_distinct_samples_eval():
+    """configs[3] at B = 512 with 512 DISTINCT samples (the train-mode full-job test replicates 8):
+    eval-mode BN makes every row a function of its own sample alone, so rows picked at random are
+    checked against the oracle's forward of just those samples -- an indexing error between samples
+    of the big batch (tile tables, fused FU rows, head tiles) shows up here"""
+    G = _fgan(False, "fp32", seed=4321)
+    G = G.cuda().train()
+    for m in G.modules():   # realistic running statistics: one train batch with momentum 1
+        if isinstance(m, nn.BatchNorm2d):
+            m.momentum = 1.0
+    gen = torch.Generator().manual_seed(9)
+    with torch.no_grad():
+        G.forward_float(torch.randn((64, 128), generator=gen).cuda())
+    G.eval()
+    sd = _sd64(G)
+    z = torch.randn((512, 128), generator=gen)
+    with torch.no_grad():
+        got = G.forward_float(z.cuda()).cpu()
+    rows = torch.randperm(512, generator=gen)[:6]
+    from oracle.ffc_oracle import fgan128_generator
+    with torch.no_grad():
+        ref = fgan128_generator(z[rows].double(), sd, False, None)
+    err = normwise_err(got[rows], ref)
+    print(f"fgan128 eval B=512 distinct samples, rows {rows.tolist()}: {err:.2e}")
+    assert err <= TOL, err

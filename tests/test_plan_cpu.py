@@ -272,3 +272,100 @@ def test_patch_cfg_policy_min_blocks():
     p128 = _plan.pick_patch_cfg(256, 64, segs, 128)
     assert p512.cfg == 1 and p128.cfg == 0
     assert 128 <= p128.npb * 2 < 512   # cfg 0: pixel blocks x 2 M-tiles, between the two thresholds
+
+
+# --------------------------------------------------------------------------- round 5: plan keys and launch guard
+def test_conv_layer_backward_plans_distinct_per_channel_count(monkeypatch):
+    """the r04b illegal memory access: two conv_layer backward (adjoint) jobs of one
+    layer structure that differ only in the input channel count C -- i.e. in the adjoint's output
+    channels M -- must get two plans.  Before 144747e the adjoint key ("adj", spec, i, edges, B, segs)
+    had no C, so the second job reused the first one's plan and its kernel wrote B*C1*H*W outputs
+    into a B*C2*H*W tensor.  run_conv now keys every plan by (caller key, B, M, segments, device,
+    plan switches), whatever the caller's key holds."""
+    from fastfourierconvolution_amd import _autograd as ag
+    from fastfourierconvolution_amd import _runtime as rt
+    made = []
+
+    class FakeExec:
+        def __init__(self, B, M, segs, weights, dev, pw_ok=False, convq_cfg=None):
+            self.plan = _plan.plan_job(B, M, segs)
+            self.flops, self.kind = 0.0, "gemm"
+            made.append((B, M, tuple(segs)))
+
+        def ensure_packed(self, weights):
+            pass
+
+        job = rt.ConvExec.job
+        check_launch = rt.ConvExec.check_launch
+
+        def base_job(self):
+            return None
+
+    class FakeLaunch:
+        def __init__(self, execs, dev):
+            pass
+
+        def launch(self, jobs, stream, flops=0.0):
+            pass
+
+    class FakeJob:
+        def __init__(self):
+            self.seg = [FakeJob.Seg() for _ in range(4)]
+
+        class Seg:
+            pass
+    monkeypatch.setattr(rt, "ConvExec", FakeExec)
+    monkeypatch.setattr(rt, "LaunchPlan", FakeLaunch)
+    monkeypatch.setattr(FakeExec, "base_job", lambda self: FakeJob())
+    monkeypatch.setattr(ag, "_stream", lambda t: 0)
+    cache = {}
+    B, H = 2, 8
+    g = torch.zeros(B, 16, 2 * H, 2 * H)            # the gradient of a ConvT(C -> 16, k4 s2 p1) output
+    adj = _plan.Seg("conv", 16, 2 * H, 2 * H, 4, 2, 1)   # its adjoint: Conv2d k4 s2 p1 back to H x H
+    outs = []
+    for C in (8, 24):                                # same structure and gradient, different C
+        key = ("adj", "spec", 0, (0,), B, (adj,))    # the round-4 key: no C
+        w = (torch.zeros(C, 16, 4, 4), 0, 4, 4, None)
+        outs.append(ag.run_conv(cache, key, B, C, (adj,), [w], [g], out_shape=(B, C, H, H)))
+    assert [m[1] for m in made] == [8, 24], made     # two plans, one per output channel count
+    assert len(cache) == 2
+    assert [tuple(o.shape) for o in outs] == [(B, 8, H, H), (B, 24, H, H)]
+
+
+def test_conv_launch_guard_rejects_mismatched_tensors():
+    """ConvExec.check_launch (the host-side guard before every conv launch): a plan used with an output,
+    addend or input of other extents raises FFCError instead of launching a kernel that would write
+    (or read) past the tensor; (B, M, k, k) views of a (B, M k k, 1, 1) output are accepted"""
+    from fastfourierconvolution_amd import _runtime as rt
+    ex = rt.ConvExec.__new__(rt.ConvExec)
+    segs = (_plan.Seg("convT", 16, 8, 8, 4, 2, 1), _plan.Seg("pw", 12, 16, 16))
+    ex.plan = _plan.plan_job(4, 32, segs)
+    x0, x1 = torch.zeros(4, 16, 8, 8), torch.zeros(4, 12, 16, 16)
+    out = torch.zeros(4, 32, 16, 16)
+    ex.check_launch([(x0, None), (x1, None)], out, addend=torch.zeros(4, 32, 16, 16))
+    bad = [
+        ([(x0, None), (x1, None)], torch.zeros(4, 24, 16, 16), None),      # fewer output channels
+        ([(x0, None), (x1, None)], torch.zeros(4, 40, 16, 16), None),      # more
+        ([(x0, None), (x1, None)], torch.zeros(4, 32, 16, 16)[:, :, :, :8], None),   # strided view
+        ([(x0, None), (x1, None)], out, torch.zeros(4, 32, 8, 8)),          # addend
+        ([(torch.zeros(4, 8, 8, 8), None), (x1, None)], out, None),         # input channels
+        ([(torch.zeros(2, 16, 8, 8), None), (x1, None)], out, None),        # batch
+        ([(x0, None)], out, None),                                          # segment count
+        ([(x0, torch.zeros(4, 15)), (x1, None)], out, None),                # gate size
+    ]
+    for inputs, o, add in bad:
+        with pytest.raises(rt.FFCError):
+            ex.check_launch(inputs, o, add)
+    ex1 = rt.ConvExec.__new__(rt.ConvExec)
+    ex1.plan = _plan.plan_job(4, 32 * 16, (_plan.Seg("pw", 100, 1, 1),))   # ffc0's outer-product form
+    ex1.check_launch([(torch.zeros(4, 100, 1, 1), None)], torch.zeros(4, 32, 4, 4))
+    pool = rt.ConvExec.__new__(rt.ConvExec)                # a 2x2-pooled segment reads the 2x input
+    pool.plan = _plan.plan_job(4, 8, (_plan.Seg("pw", 12, 8, 8, pool=True),))
+    pool.check_launch([(torch.zeros(4, 12, 16, 16), None)], torch.zeros(4, 8, 8, 8))
+    with pytest.raises(rt.FFCError):
+        pool.check_launch([(torch.zeros(4, 12, 8, 8), None)], torch.zeros(4, 8, 8, 8))
+
+
+def test_st_split_max_rounds_to_power_of_two():
+    from fastfourierconvolution_amd import _runtime as rt
+    assert [rt._pow2_floor(v) for v in ("0", "1", "3", "6", "8", "12", -4)] == [1, 1, 2, 4, 8, 8, 1]

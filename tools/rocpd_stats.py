@@ -28,15 +28,20 @@ def last_step(path, first_kernel="dense_kernel"):
     c = sqlite3.connect(path)
     rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
     i0 = max(i for i, r in enumerate(rows) if first_kernel in r[0])
-    out = [((e - s) / 1e3, g // max(1, w), n) for n, s, e, g, w in rows[i0:]]
+    out = []
+    for k, (n, s, e, g, w) in enumerate(rows[i0:]):
+        gap = (s - rows[i0 + k - 1][2]) / 1e3 if k else 0.0   # from the previous kernel's end
+        out.append(((e - s) / 1e3, g // max(1, w), n, gap))
     return out
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--step":
         seq = last_step(sys.argv[2], *(sys.argv[3:4]))
-        for us, wg, name in seq:
-            print(f"{us:8.2f} us {wg:7d} WG  {name[:90]}")
-        print(f"{sum(s[0] for s in seq):8.2f} us total, {len(seq)} launches")
+        for us, wg, name, gap in seq:
+            print(f"{us:8.2f} us (gap {gap:5.2f}) {wg:7d} WG  {name[:90]}")
+        span = sum(s[0] + s[3] for s in seq)
+        print(f"{sum(s[0] for s in seq):8.2f} us in kernels, {span:8.2f} us first start -> last end, "
+              f"{len(seq)} launches")
     else:
         main(sys.argv[1])

@@ -34,7 +34,7 @@ def main():
     with contextlib.redirect_stdout(io.StringIO()):
         G = F.FFCGenerator(100, 3, 64)
     G = G.cuda().train()
-    z = torch.randn(256, 100, 1, 1, device="cuda")
+    z = torch.randn(int(os.environ.get("TRACE_B", "256")), 100, 1, 1, device="cuda")
     with torch.no_grad():
         for _ in range(3):
             G(z)
@@ -44,7 +44,7 @@ def main():
     for f in (rfu, rst):
         f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     recs = []
-    ofu, ost = L.ffc_fu_forward_ex, L.ffc_st_prologue
+    ofu, ost = L.ffc_fu_forward_ex, L.ffc_st_prologue_ex
 
     def fu(*a):
         rc = ofu(*a)
@@ -58,16 +58,16 @@ def main():
     def st(*a):
         rc = ost(*a)
         torch.cuda.synchronize()
-        B = a[1]
+        B = a[1] * a[11]   # workgroups: samples x split
         buf = np.zeros((B, 8), dtype=np.uint64)
         assert rst(buf.ctypes.data, buf.nbytes) == 0
-        recs.append(("st", f"Cin={a[2]} {a[3]}x{a[4]} c={a[10]}", buf))
+        recs.append(("st", f"Cin={a[2]} {a[3]}x{a[4]} c={a[10]} split={a[11]}", buf))
         return rc
 
-    L.ffc_fu_forward_ex, L.ffc_st_prologue = fu, st
+    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex = fu, st
     with torch.no_grad():
         G(z)
-    L.ffc_fu_forward_ex, L.ffc_st_prologue = ofu, ost
+    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex = ofu, ost
     for kind, desc, buf in recs:
         rt0, rt1 = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64)
         dur = (rt1 - rt0) / 100.0
