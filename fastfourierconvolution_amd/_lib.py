@@ -161,6 +161,10 @@ SIGNATURES = [
                              c_int, c_void_p, c_void_p]),
     ("ffc_fu2d_c2r_bn", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                 c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("ffc_fu2d_r2c_ex", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                ctypes.POINTER(BnFold), c_void_p, c_void_p]),
+    ("ffc_fu2d_c2r_fold", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                  c_int, ctypes.POINTER(BnFold), c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("ffc_noise_wgrad", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),

@@ -292,6 +292,7 @@ class BnFoldDesc:
     def __init__(self, bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device):
         _, update = bn_mode(bn)
         self.slab = slab
+        self.channel_only = False   # made by bn_fold_channels: too many rows for a whole-slab fold
         self.scale = torch.empty(C, device=device, dtype=torch.float32)
         self.shift = torch.empty(C, device=device, dtype=torch.float32)
         self.bn = bn
@@ -321,6 +322,31 @@ def bn_fold(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, dev
     if bn.num_features != C:
         raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
     return BnFoldDesc(bn, C, slab, nrows, count_mult, device)
+
+
+# Per-channel in-kernel folds (ffc::bn_fold_channels): consumers whose workgroups / waves need only
+# one or a few channels (the staged Fourier unit's r2c / c2r, the fused FU's split pass 1) merge just
+# those channels' slab rows -- cheap at any channel count, so the limit is the rows a lane merges.
+# FFC_BN_CHFOLD=0 restores the separate finalize launches (A/B); FFC_BN_CHFOLD_LOADS: max slab rows
+# per lane.
+BN_CHFOLD = __import__("os").environ.get("FFC_BN_CHFOLD", "1") != "0"
+BN_CHFOLD_LOADS = int(__import__("os").environ.get("FFC_BN_CHFOLD_LOADS", "16"))
+
+
+def bn_fold_channels(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, lanes: int = 64):
+    """a BnFoldDesc for a per-channel in-kernel fold (``lanes`` lanes merge one channel's rows), or
+    None: batch statistics on one rank only, momentum not None (the per-channel leaders cannot read
+    num_batches_tracked while another bumps it), at most BN_CHFOLD_LOADS rows per lane"""
+    use_batch, _ = bn_mode(bn)
+    if not (BN_FOLD and BN_CHFOLD and use_batch and slab is not None and _sync_group() is None):
+        return None
+    if bn.momentum is None or -(-nrows // lanes) > BN_CHFOLD_LOADS:
+        return None
+    if bn.num_features != C:
+        raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
+    d = BnFoldDesc(bn, C, slab, nrows, count_mult, device)
+    d.channel_only = True
+    return d
 
 
 def act_code(mod: nn.Module):
@@ -559,7 +585,7 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS)
+            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS)
 
 
 def algorithmic_flops(plan) -> float:

@@ -113,4 +113,73 @@ __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool l
     if (leader && f.update_running && tid == 0) *f.num_batches_tracked += 1;
 }
 
+// Groups of L lanes (L a power of two <= 64) finalize one channel each -- channel o, given per lane --
+// from that channel's partial rows only: for the consumers whose workgroups need one or a few
+// channels (the staged Fourier unit's per-plane r2c / c2r: L = 64; the fused FU's per-wave pass 1:
+// 64 / (2 x its channels)).  Rows (lane % L), + L, ... are merged per lane in that order (four loads
+// in flight), then an xor tree over the group whose every level adds commutative pairs: the L lanes
+// end with bit-identical totals, and so does every workgroup that folds channel o with the same L.
+// Same finalize arithmetic as bn_fold_block.  leader: the running-statistics update and scale_out /
+// shift_out of channel o (exactly one workgroup per channel leads); num_batches_tracked is bumped by
+// the caller (one lane of the workgroup leading channel 0).  Needs momentum >= 0 (no read of
+// num_batches_tracked: with per-channel leaders that read would race with the bump).
+template <int L>
+__device__ inline void bn_fold_channels(const ffc_bn_fold& f, int o, bool leader, float& scale, float& shift) {
+    static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "lanes per channel");
+    const int gl = threadIdx.x & (L - 1);
+    const float4* slab = reinterpret_cast<const float4*>(f.slab) + o;
+    double n = 0.0, s = 0.0, q = 0.0;
+    int r = gl;
+    for (; r + 3 * L < f.nrows; r += 4 * L) {
+        float4 e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = slab[(size_t)(r + L * u) * f.C];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double en = e[u].x, em = e[u].y;
+            n += en;
+            s += en * em;
+            q += (double)e[u].z + en * em * em;
+        }
+    }
+    for (; r < f.nrows; r += L) {
+        const float4 e = slab[(size_t)r * f.C];
+        const double en = e.x, em = e.y;
+        n += en;
+        s += en * em;
+        q += (double)e.z + en * em * em;
+    }
+#pragma unroll
+    for (int m = 1; m < L; m <<= 1) {
+        n += shfl_xor_f64(n, m);
+        s += shfl_xor_f64(s, m);
+        q += shfl_xor_f64(q, m);
+    }
+    const double mu = s / n;
+    double v = q / n - mu * mu;
+    if (v < 0.0) v = 0.0;
+    const float mean = (float)mu, var = (float)v;
+    const float inv = 1.0f / sqrtf(var + f.eps);
+    const float g = f.gamma ? f.gamma[o] : 1.0f;
+    const float b = f.beta ? f.beta[o] : 0.0f;
+    scale = g * inv;
+    shift = fmaf(-mean, scale, b);
+    if (leader && gl == 0) {
+        if (f.update_running) {
+            const float fm = f.momentum;
+            const double nfull = n * (double)f.count_mult;
+            const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
+            f.running_mean[o] = fmaf(fm, mean, (1.0f - fm) * f.running_mean[o]);
+            f.running_var[o] = fmaf(fm, (float)unb, (1.0f - fm) * f.running_var[o]);
+        }
+        if (f.scale_out) f.scale_out[o] = scale;
+        if (f.shift_out) f.shift_out[o] = shift;
+    }
+}
+
+// one whole wave per channel
+__device__ inline void bn_fold_channel(const ffc_bn_fold& f, int o, bool leader, float& scale, float& shift) {
+    bn_fold_channels<64>(f, o, leader, scale, shift);
+}
+
 }  // namespace ffc

@@ -32,6 +32,7 @@
 #include <set>
 
 #include "fft_common.h"
+#include "bn_common.h"
 
 namespace {
 
@@ -166,6 +167,8 @@ struct R2cArgs {
     float* T;
     int C, in_relu;
     float oscale, iscale;   // PLANAR: every bin x oscale, bins with a Hermitian mirror x iscale too
+    int has_fold;           // the input BN (SpectralTransform.bn1) finalized here, per plane channel
+    ffc_bn_fold fold;       // (in_scale / in_shift unused; the channel leaders write scale_out / shift_out)
 };
 
 // ---------------------------------------------------------------- stage 1: R2C of the t planes
@@ -185,8 +188,8 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     const int plane = blockIdx.x;
     const int ch = plane % a.C;
     const int tid = threadIdx.x;
-    const float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
-    const float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
+    float sc = a.in_scale ? a.in_scale[ch] : 1.0f;
+    float sh = a.in_scale ? a.in_shift[ch] : 0.0f;
 
     // 1. t plane -> transform -> R
     const float4* src = reinterpret_cast<const float4*>(a.t + (size_t)plane * h * w);
@@ -196,6 +199,23 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     for (int j = 0; j < NV; ++j) {
         const int i = j * FU2_THREADS + tid;
         if (i < h * w / 4) v[j] = src[i];
+    }
+    if (!PLANAR && a.has_fold) {
+        // bn1 of this plane's channel from its slab rows, under the plane loads' latency; the
+        // workgroups of sample 0 lead (running statistics, scale_out / shift_out for the C2R)
+        __shared__ float fsc[2];
+        if (tid < 64) {
+            float fs, fh;
+            ffc::bn_fold_channel(a.fold, ch, plane < a.C, fs, fh);
+            if (tid == 0) {
+                fsc[0] = fs;
+                fsc[1] = fh;
+                if (plane == 0 && a.fold.update_running) *a.fold.num_batches_tracked += 1;
+            }
+        }
+        __syncthreads();
+        sc = fsc[0];
+        sh = fsc[1];
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -297,6 +317,8 @@ struct C2rArgs {
     const float* bn_scale;   // optional [2C]: Y is the raw mix output, relu(Y*bn_scale + bn_shift) on load
     const float* bn_shift;
     float iscale;            // PLANAR: bins 0 < kw < W/2 x iscale (0.5: the adjoint of rfftn)
+    int has_bn_fold;         // the FU's BN finalized here (channels 2c, 2c+1 of this plane) instead of
+    ffc_bn_fold bn_fold;     // bn_scale / bn_shift; sample 0's workgroups lead
 };
 
 // PLANAR (the training path's ffc_irfft2_planes): Y in the interleaved channel-plane layout (Re of
@@ -330,9 +352,10 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
     constexpr bool RPRE = !PLANAR && UP == 2;
     float2 res[RPRE ? RROUNDS : 1][RPRE ? RITER : 1];
     {
-        const bool bn = a.bn_scale != nullptr;
-        const float bsr = bn ? a.bn_scale[2 * ch] : 1.0f, bhr = bn ? a.bn_shift[2 * ch] : 0.0f;
-        const float bsi = bn ? a.bn_scale[2 * ch + 1] : 1.0f, bhi = bn ? a.bn_shift[2 * ch + 1] : 0.0f;
+        const bool bn = a.bn_scale != nullptr || a.has_bn_fold;
+        float bsr = bn && !a.has_bn_fold ? a.bn_scale[2 * ch] : 1.0f, bhr = bn && !a.has_bn_fold ? a.bn_shift[2 * ch] : 0.0f;
+        float bsi = bn && !a.has_bn_fold ? a.bn_scale[2 * ch + 1] : 1.0f;
+        float bhi = bn && !a.has_bn_fold ? a.bn_shift[2 * ch + 1] : 0.0f;
         if constexpr (!PLANAR) {
             constexpr int N4 = H * WP / 2;                         // H even: whole float4 pairs
             constexpr int NL = (N4 + FU2_THREADS - 1) / FU2_THREADS;
@@ -342,6 +365,26 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
             for (int u = 0; u < NL; ++u) {
                 const int i = u * FU2_THREADS + tid;
                 v[u] = src4[i < N4 ? i : 0];
+            }
+            if (a.has_bn_fold) {
+                // the FU's BN of this plane's two spectral channels (Re 2c, Im 2c+1) from pass 0's slab
+                // rows, waves 0 and 1 in parallel, under the Y loads' latency
+                __shared__ float fbn[4];
+                const int wv = tid >> 6;
+                if (wv < 2) {
+                    float fs, fh;
+                    ffc::bn_fold_channel(a.bn_fold, 2 * ch + wv, plane < a.C, fs, fh);
+                    if ((tid & 63) == 0) {
+                        fbn[2 * wv] = fs;
+                        fbn[2 * wv + 1] = fh;
+                        if (plane == 0 && wv == 0 && a.bn_fold.update_running) *a.bn_fold.num_batches_tracked += 1;
+                    }
+                }
+                __syncthreads();
+                bsr = fbn[0];
+                bhr = fbn[1];
+                bsi = fbn[2];
+                bhi = fbn[3];
             }
             if constexpr (RPRE) {
                 if (a.residual) {
@@ -1181,9 +1224,24 @@ extern "C" int ffc_fu2d_slab_rows(int B, int C, int H, int W) {
 
 extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const float* in_scale,
                             const float* in_shift, int in_relu, float* T, void* stream) {
+    return ffc_fu2d_r2c_ex(t, B, C, h, w, in_scale, in_shift, in_relu, nullptr, T, stream);
+}
+
+// a per-channel fold (ffc::bn_fold_channel): momentum >= 0 (no num_batches_tracked read), C channels
+static bool channel_fold_ok(const ffc_bn_fold* f, int C) {
+    return f->slab && f->nrows > 0 && f->C == C && (!f->update_running ||
+           (f->running_mean && f->running_var && f->num_batches_tracked && f->momentum >= 0.0f));
+}
+
+extern "C" int ffc_fu2d_r2c_ex(const float* t, int B, int C, int h, int w, const float* in_scale,
+                               const float* in_shift, int in_relu, const ffc_bn_fold* in_fold, float* T,
+                               void* stream) {
     FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_r2c: B and C must be positive");
     FFC_CHECK_ARG(t && T, "ffc_fu2d_r2c: null pointer");
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_r2c: in_scale/in_shift pairing");
+    FFC_CHECK_ARG(!in_fold || (!in_scale && channel_fold_ok(in_fold, C) && in_fold->scale_out && in_fold->shift_out),
+                  "ffc_fu2d_r2c: in_fold replaces in_scale / in_shift, needs C channels, momentum >= 0 and "
+                  "scale_out / shift_out");
     R2cKernel k = pick_r2c(h, w);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_r2c: unsupported plane (square, power of two in [8, 128])");
     const size_t lds = r2c_lds(h, w);
@@ -1191,6 +1249,8 @@ extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const fl
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c");
     if (rc) return rc;
     R2cArgs a{t, in_scale, in_shift, T, C, in_relu, 1.0f, 1.0f};
+    a.has_fold = in_fold != nullptr;
+    if (in_fold) a.fold = *in_fold;
     hipLaunchKernelGGL(k, dim3(B * C), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_r2c");
 }
@@ -1272,7 +1332,8 @@ extern "C" int ffc_fu2d_mix_f16(const float* T, int B, int C, int H, int W, int 
 
 static int fu2d_c2r_launch(const float* Y, int B, int C, int H, int W, const float* t, int up,
                            const float* in_scale, const float* in_shift, int in_relu, int residual,
-                           const float* bn_scale, const float* bn_shift, float* out, void* stream) {
+                           const float* bn_scale, const float* bn_shift, float* out, void* stream,
+                           const ffc_bn_fold* bn_fold = nullptr) {
     FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_c2r: B and C must be positive");
     FFC_CHECK_ARG((bn_scale == nullptr) == (bn_shift == nullptr), "ffc_fu2d_c2r: bn_scale/bn_shift pairing");
     FFC_CHECK_ARG(Y && out, "ffc_fu2d_c2r: null pointer");
@@ -1281,6 +1342,8 @@ static int fu2d_c2r_launch(const float* Y, int B, int C, int H, int W, const flo
     FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_c2r: in_scale/in_shift pairing");
     C2rArgs a{Y, t, in_scale, in_shift, out, C, in_relu, residual, (float)(1.0 / std::sqrt((double)H * (double)W)),
               bn_scale, bn_shift, 1.0f};
+    a.has_bn_fold = bn_fold != nullptr;
+    if (bn_fold) a.bn_fold = *bn_fold;
     C2rKernel k = pick_c2r(H, W, up);
     FFC_CHECK_ARG(k != nullptr, "ffc_fu2d_c2r: unsupported plane (square, power of two in [16, 128])");
     const size_t lds = c2r_lds(H, W);
@@ -1303,6 +1366,15 @@ extern "C" int ffc_fu2d_c2r_bn(const float* Y, int B, int C, int H, int W, const
     FFC_CHECK_ARG(bn_scale && bn_shift, "ffc_fu2d_c2r_bn: bn_scale and bn_shift required");
     return fu2d_c2r_launch(Y, B, C, H, W, t, up, in_scale, in_shift, in_relu, residual, bn_scale, bn_shift, out,
                            stream);
+}
+
+extern "C" int ffc_fu2d_c2r_fold(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                                 const float* in_scale, const float* in_shift, int in_relu, int residual,
+                                 const ffc_bn_fold* bn_fold, float* out, void* stream) {
+    FFC_CHECK_ARG(bn_fold && channel_fold_ok(bn_fold, 2 * C),
+                  "ffc_fu2d_c2r_fold: bn_fold needs 2C channels and momentum >= 0");
+    return fu2d_c2r_launch(Y, B, C, H, W, t, up, in_scale, in_shift, in_relu, residual, nullptr, nullptr, out,
+                           stream, bn_fold);
 }
 
 extern "C" int ffc_fu2d_cols_supported(int C, int H, int W, int up, int f16) {

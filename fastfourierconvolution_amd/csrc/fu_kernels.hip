@@ -381,12 +381,31 @@ __global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
     const int tid = threadIdx.x;
     float* Yre = smem;
     float* Yim = Yre + CPG * NB;
+    __shared__ float fbn[2][2 * CPG];
+    const float* bsc = a.bn_scale + 2 * c0;
+    const float* bsh = a.bn_shift + 2 * c0;
+    if (a.has_mix_fold) {
+        // the FU's BN of this wave's 2 CPG spectral channels, folded here: 64 / (2 CPG) lanes per
+        // channel (ffc::bn_fold_channels), sample 0's waves lead
+        constexpr int LPC = 64 / (2 * CPG);
+        const int ol = tid / LPC;
+        float fs, fh;
+        ffc::bn_fold_channels<LPC>(a.mix_fold, 2 * c0 + ol, b == 0, fs, fh);
+        if ((tid & (LPC - 1)) == 0) {
+            fbn[0][ol] = fs;
+            fbn[1][ol] = fh;
+        }
+        if (blockIdx.x == 0 && tid == 0 && a.mix_fold.update_running) *a.mix_fold.num_batches_tracked += 1;
+        __syncthreads();
+        bsc = fbn[0];
+        bsh = fbn[1];
+    }
     // Y rows 2 c0 .. 2 (c0 + CPG) of this sample -> BN + ReLU -> the Y planes
     const float4* ys = reinterpret_cast<const float4*>(a.yspill + ((size_t)b * C2 + 2 * c0) * NB);
     for (int i = tid; i < 2 * CPG * NB / 4; i += 64) {
-        const int ol = (4 * i) / NB, n = 4 * i - ol * NB, o = 2 * c0 + ol;
+        const int ol = (4 * i) / NB, n = 4 * i - ol * NB;
         const float4 v = ys[i];
-        const float sc = a.bn_scale[o], sh = a.bn_shift[o];
+        const float sc = bsc[ol], sh = bsh[ol];
         float* dst = ((ol & 1) ? Yim : Yre) + (ol >> 1) * NB + n;
         *reinterpret_cast<float4*>(dst) = make_float4(fmaxf(fmaf(v.x, sc, sh), 0.0f), fmaxf(fmaf(v.y, sc, sh), 0.0f),
                                                       fmaxf(fmaf(v.z, sc, sh), 0.0f), fmaxf(fmaf(v.w, sc, sh), 0.0f));
@@ -609,8 +628,11 @@ extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int
             raised.insert(reinterpret_cast<const void*>(k));
         }
     }
-    // pass 1 from the spill with the BN scale / shift given: one wave per (sample, 64 / H channels)
-    if (pass == 1 && yspill && !mix_fold && fu_split_on() && H * W <= 64 * 64 && H <= 64 && C % (64 / H) == 0) {
+    // pass 1 from the spill with the BN scale / shift given, or a mix fold the waves can take channel by
+    // channel (momentum >= 0: ffc::bn_fold_channels): one wave per (sample, 64 / H channels)
+    const bool chan_fold = mix_fold && mix_fold->momentum >= 0.0f && (2 * 64 / H) <= 64;
+    if (pass == 1 && yspill && (!mix_fold || chan_fold) && fu_split_on() && H * W <= 64 * 64 && H <= 64 &&
+        C % (64 / H) == 0) {
         FuKernel ks = pick_split(H, W, up);
         if (ks) {
             const size_t slds = (size_t)2 * (64 / H) * H * (W / 2 + 1) * sizeof(float);

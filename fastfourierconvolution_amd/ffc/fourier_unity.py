@@ -68,14 +68,12 @@ class FourierUnitSN(nn.Module):
             fused = False
         if fused and staged_ok and (rt.FU_PATH == "staged" or (rt.FU_PATH == "auto" and B < rt.FU_FUSED_MIN_BATCH)):
             fused = False
-        if in_fold is not None and fused and not self._fold_ok(C, H, W):
+        if in_fold is not None and fused and (in_fold.channel_only or not self._fold_ok(C, H, W)):
             in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
             in_fold = None
         if not fused:
             if L.ffc_fu2d_supported(C, H, W, up):
-                if in_fold is not None:
-                    in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
-                return self._run2d(t, up, in_scale, in_shift, in_relu, residual)
+                return self._run2d(t, up, in_scale, in_shift, in_relu, residual, in_fold)
             raise NotImplementedError(f"Fourier unit supports H,W in {{4,8,16,32}} with 16*C*H*(W/2+1) <= 160 KiB "
                                       f"(fused) or square H=W in {{16,32,64,128}} with 2C <= 128 (staged); "
                                       f"got C={C}, {H}x{W}")
@@ -101,7 +99,12 @@ class FourierUnitSN(nn.Module):
                                           None, ptr(yspill), stream), "ffc_fu_forward(pass 0)")
             if in_fold is not None:          # pass 0's workgroup 0 wrote the folded bn1 affine
                 in_scale, in_shift = in_fold.scale, in_fold.shift
-            mix_fold = rt.bn_fold(self.bn, 2 * C, slab, B, 1.0, dev) if self._fold_ok(C, H, W) else None
+            mix_fold = None
+            if yspill is not None and H == W and H in (8, 16, 32) and C % (64 // H) == 0:
+                # the split pass 1 (one wave per 64 / H channels) folds its 2 * 64 / H channels itself
+                mix_fold = rt.bn_fold_channels(self.bn, 2 * C, slab, B, 1.0, dev, lanes=64 // (2 * 64 // H))
+            if mix_fold is None and self._fold_ok(C, H, W):
+                mix_fold = rt.bn_fold(self.bn, 2 * C, slab, B, 1.0, dev)
             if mix_fold is None:
                 sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, B, 1.0, dev, stream)
         else:
@@ -127,9 +130,19 @@ class FourierUnitSN(nn.Module):
             return mix16
         return self._packs.get("mix16", [w], build)
 
-    def _run2d(self, t, up, in_scale, in_shift, in_relu, residual):
-        """large-plane FU: r2c -> mix (pass 0 stats, pass 1 BN/ReLU) -> c2r (include/ffc_amd.h ffc_fu2d_*)"""
+    def _run2d(self, t, up, in_scale, in_shift, in_relu, residual, in_fold=None):
+        """large-plane FU: r2c -> mix (pass 0 stats, pass 1 BN/ReLU) -> c2r (include/ffc_amd.h ffc_fu2d_*).
+        in_fold: the input BN as an rt.BnFoldDesc -- finalized inside the r2c, one channel per plane
+        workgroup, when that fold applies (rt.bn_fold_channels), else by its own launch"""
         B, C, h, w = t.shape
+        if in_fold is not None:
+            chf = rt.bn_fold_channels(in_fold.bn, C, in_fold.slab, in_fold.struct.nrows, in_fold.struct.count_mult,
+                                      t.device)
+            if chf is None:
+                in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
+                in_fold = None
+            else:
+                in_fold = chf
         H, W = h * up, w * up
         L = rt.lib()
         dev = t.device
@@ -148,8 +161,11 @@ class FourierUnitSN(nn.Module):
         # bytes never transferred
         mvr = 4.0 * t.numel() + 8.0 * nT
         with rt.observe("fu2d_r2c", bytes=min(4.0 * n_r + 8.0 * n_c, mvr), moved=mvr):
-            check(L.ffc_fu2d_r2c(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(T), stream),
+            check(L.ffc_fu2d_r2c_ex(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu),
+                                    ctypes.byref(in_fold.struct) if in_fold else None, ptr(T), stream),
                   "ffc_fu2d_r2c")
+        if in_fold is not None:   # the r2c's sample-0 workgroups wrote the folded bn1 affine
+            in_scale, in_shift = in_fold.scale, in_fold.shift
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         c2r_moved = 8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)
         c2r_bytes = min(8.0 * n_c + 4.0 * n_r, c2r_moved)                   # SURVEY.md §8d C2R pass
@@ -162,6 +178,13 @@ class FourierUnitSN(nn.Module):
             with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT + (8.0 * nY if Y is not None else 0.0)):
                 check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, ptr(Y), stream),
                       "ffc_fu2d_mix(pass 0)")
+            cfold = rt.bn_fold_channels(self.bn, 2 * C, slab, rows, 1.0, dev) if Y is not None else None
+            if cfold is not None:   # the FU's BN finalized inside the C2R (two channels per plane)
+                with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):
+                    check(L.ffc_fu2d_c2r_fold(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
+                                              int(in_relu), int(residual), ctypes.byref(cfold.struct), ptr(out),
+                                              stream), "ffc_fu2d_c2r_fold")
+                return out
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
             if Y is not None:
                 with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):

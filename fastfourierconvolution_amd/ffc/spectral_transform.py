@@ -164,6 +164,8 @@ class SpectralTransform(nn.Module):
             slab = torch.empty((nrows, c, 4), device=dev, dtype=torch.float32) if use_batch else None
             lp.launch([ex.job([(x, gate)], t, stats=slab)], stream, flops=ex.flops)
         fold = rt.bn_fold(self.bn1, c, slab, nrows, float(up * up), dev) if use_batch else None
+        if fold is None and use_batch:   # the staged FU's r2c can still fold it channel by channel
+            fold = rt.bn_fold_channels(self.bn1, c, slab, nrows, float(up * up), dev)
         if fold is not None:   # bn1 finalized inside the FU's first kernel
             return self.fu._run(t, up=up, in_relu=True, residual=True, in_fold=fold)
         sc1, sh1 = rt.bn_scale_shift(self.bn1, c, slab, nrows if use_batch else 0, float(up * up), dev, stream)

@@ -468,6 +468,17 @@ int ffc_fu2d_c2r(const float* Y, int B, int C, int H, int W, const float* t, int
 int ffc_fu2d_c2r_bn(const float* Y, int B, int C, int H, int W, const float* t, int up,
                     const float* in_scale, const float* in_shift, int in_relu, int residual,
                     const float* bn_scale, const float* bn_shift, float* out, void* stream);
+/* The same two stages with their BatchNorm finalized in-kernel, one channel per consumer (replaces
+ * the ffc_bn_reduce_finalize launch before each; SpectralTransform.bn1, spectral_transform.py:57,89,
+ * and FourierUnitSN.bn, fourier_unity.py:46): every (sample, channel) workgroup merges its channel's
+ * slab rows itself (ffc_bn_fold over C = the r2c's C, or 2C for the c2r's two spectral channels;
+ * momentum >= 0); the workgroups of sample 0 update the running statistics and write scale_out /
+ * shift_out (required for in_fold: the C2R's residual takes them as in_scale / in_shift). */
+int ffc_fu2d_r2c_ex(const float* t, int B, int C, int h, int w, const float* in_scale,
+                    const float* in_shift, int in_relu, const ffc_bn_fold* in_fold, float* T, void* stream);
+int ffc_fu2d_c2r_fold(const float* Y, int B, int C, int H, int W, const float* t, int up,
+                      const float* in_scale, const float* in_shift, int in_relu, int residual,
+                      const ffc_bn_fold* bn_fold, float* out, void* stream);
 
 /* ------------------------------------------------------------------ fgan128 caller ops
  * NoiseInjection.forward(x, noise) (layers/noise_injection.py:25-32): out = x + weight[c]*noise[b]

@@ -106,3 +106,62 @@ def test_st_prologue_split_matches_one_workgroup_per_sample(cin, cout, hw, B):
             assert int(sd[k]) == int(v), k
         elif k.endswith("running_mean") or k.endswith("running_var"):
             torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=k)
+
+
+# --------------------------------------------------------------------------- round 5: per-channel folds
+def _run_chfold(st, xs, chfold, path):
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.BN_CHFOLD, rt.FU_PATH, rt.FU_SPILL
+    rt.BN_CHFOLD, rt.FU_PATH, rt.FU_SPILL = chfold, path, True
+    try:
+        with torch.no_grad():
+            outs = [st(x).clone() for x in xs]
+        torch.cuda.synchronize()
+    finally:
+        rt.BN_CHFOLD, rt.FU_PATH, rt.FU_SPILL = old
+    return outs, {k: v.detach().clone() for k, v in st.state_dict().items()}
+
+
+@pytest.mark.parametrize("momentum", [0.1, None])
+@pytest.mark.parametrize("path,cin,cout,hw,B", [("staged", 32, 64, 8, 6), ("staged", 64, 32, 16, 3),
+                                                ("fused", 64, 128, 4, 7), ("fused", 32, 64, 8, 5),
+                                                ("fused", 16, 32, 16, 4)])
+def test_channel_folds_match_separate_launches(momentum, path, cin, cout, hw, B):
+    """bn1 folded into the staged r2c (one channel per plane workgroup), the FU's BN into the staged
+    c2r (two channels per plane) and into the fused FU's split pass 1 (2 x 64/H channels per wave),
+    ffc::bn_fold_channels, against the separate finalize launches (FFC_BN_CHFOLD=0): outputs within
+    1e-6 normwise, running statistics within 1e-6, num_batches_tracked exact, over three steps.
+    momentum None takes the separate launches (the per-channel leaders cannot read
+    num_batches_tracked), and must still agree."""
+    from fastfourierconvolution_amd import _runtime as rt
+    base = _st(cin, cout, momentum, seed=cin + hw + 1)
+    g = torch.Generator().manual_seed(hw + 1)
+    xs = [torch.randn((B, cin, hw, hw), generator=g).cuda() for _ in range(3)]
+    ref_out, ref_sd = _run_chfold(copy.deepcopy(base), xs, False, path)
+    L = rt.lib()
+    calls = {"r2c": 0, "c2r": 0}
+    o_r2c, o_c2r = L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold
+
+    def r2c(*a):
+        calls["r2c"] += a[8] is not None
+        return o_r2c(*a)
+
+    def c2r(*a):
+        calls["c2r"] += 1
+        return o_c2r(*a)
+    L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold = r2c, c2r
+    try:
+        out, sd = _run_chfold(copy.deepcopy(base), xs, True, path)
+    finally:
+        L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold = o_r2c, o_c2r
+    if path == "staged" and momentum is not None:
+        assert calls["r2c"] == 3 and calls["c2r"] == 3, calls
+    for a, b in zip(out, ref_out):
+        assert normwise_err(a.double().cpu(), b.double().cpu()) <= 1e-6
+    for k, v in ref_sd.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(v) == 3, k
+        elif k.endswith("running_mean") or k.endswith("running_var"):
+            torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=k)
+    again, _ = _run_chfold(copy.deepcopy(base), xs, True, path)
+    assert all(torch.equal(a, b) for a, b in zip(out, again))   # deterministic
