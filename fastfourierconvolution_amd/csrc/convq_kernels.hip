@@ -276,8 +276,9 @@ __device__ __forceinline__ void convq_epilogue(const ffc_convp_job& J, int wave,
 // One output tile (one row of the tile table) of one workgroup; returns when the tile is done (the
 // staging waves after their last barrier of the tile, the compute waves after the epilogue).  Every
 // wave of the workgroup runs the same tiles, so the barrier counts match tile by tile.
-template <int MT, int NTW>
+template <int MT, int NTW, int SL = QSLOTS>
 __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix, char* lds) {
+    static_assert(SL >= 2 && SL <= 6, "convq staging slots");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave_id = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stager = wave_id >= 4;
@@ -440,7 +441,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
     const int slo = min(lo, nstaged), nst = min(hi, nstaged) - slo;
     const int dlo = max(lo, nstaged) - nstaged, dhi = max(hi, nstaged) - nstaged;
 
-    const int npad = (nst + QSLOTS - 1) / QSLOTS * QSLOTS;   // barrier periods after the first (>= nst)
+    const int npad = (nst + SL - 1) / SL * SL;   // barrier periods after the first (>= nst)
     if (nst > 0) {
         int ss = 0;
         while (J.seg[ss].direct) ++ss;
@@ -461,8 +462,8 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0, qi = 0;
             QSTAMP(q0);
 #endif
-            floatx4 sv[QSLOTS][8];
-            int wbs[QSLOTS];
+            floatx4 sv[SL][8];
+            int wbs[SL];
             stage_setup(ss);
             // the chunk at the load cursor (ss, sch); past the last chunk the loads still issue (the
             // previous addresses, no store): every period then has the same load / wait pattern, so
@@ -509,33 +510,33 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
                 qw += qb - qa;
 #endif
             };
-            // QSLOTS register slots (chunk k in slot k % QSLOTS; the loop is unrolled by QSLOTS so
-            // every slot index is a compile-time constant): the loads of chunks c + 2 .. c + QSLOTS are
+            // SL register slots (chunk k in slot k % SL; the loop is unrolled by SL so
+            // every slot index is a compile-time constant): the loads of chunks c + 2 .. c + SL are
             // in flight while chunk c + 1 is split and stored
 #pragma unroll
-            for (int u = 0; u < QSLOTS; ++u) issue(sv[u], wbs[u]);
+            for (int u = 0; u < SL; ++u) issue(sv[u], wbs[u]);
             store_timed(sv[0], wbs[0], lds);
-            issue(sv[0], wbs[0]);                                   // chunk QSLOTS
-            store_timed(sv[1 % QSLOTS], wbs[1 % QSLOTS], lds + ebuf);
+            issue(sv[0], wbs[0]);                                   // chunk SL
+            store_timed(sv[1 % SL], wbs[1 % SL], lds + ebuf);
             bar();   // B0
             int wbuf = 2;   // buffer of the chunk stored next (chunk c + 1 of period c)
-            // periods 1 .. npad (nst rounded up to whole QSLOTS-period rounds: no exit in the middle of the
+            // periods 1 .. npad (nst rounded up to whole SL-period rounds: no exit in the middle of the
             // unrolled body, so every path into the loop head has the same loads in flight); periods
             // past the last chunk issue nothing live, store nothing and only meet the compute waves'
             // barriers
-            for (int c0 = 1; c0 <= npad; c0 += QSLOTS) {
+            for (int c0 = 1; c0 <= npad; c0 += SL) {
 #pragma unroll
-                for (int u = 0; u < QSLOTS; ++u) {   // period c = c0 + u: c % QSLOTS == (1 + u) % QSLOTS
+                for (int u = 0; u < SL; ++u) {   // period c = c0 + u: c % SL == (1 + u) % SL
 #ifndef FFC_QPROBE_NOSTAGE
 #ifdef FFC_TRACE_Q
                     QSTAMP(qa);
 #endif
-                    issue(sv[(1 + u) % QSLOTS], wbs[(1 + u) % QSLOTS]);   // chunk c + QSLOTS
+                    issue(sv[(1 + u) % SL], wbs[(1 + u) % SL]);   // chunk c + SL
 #ifdef FFC_TRACE_Q
                     QSTAMP(qb);
                     qi += qb - qa;
 #endif
-                    store_timed(sv[(2 + u) % QSLOTS], wbs[(2 + u) % QSLOTS], lds + wbuf * ebuf);   // chunk c + 1
+                    store_timed(sv[(2 + u) % SL], wbs[(2 + u) % SL], lds + wbuf * ebuf);   // chunk c + 1
 #endif
                     wbuf = wbuf == 2 ? 0 : wbuf + 1;
                     bar();
@@ -752,7 +753,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
 // multiple of 8, so every tile of a workgroup comes from its XCD's range of the XCD-remapped table).
 // A tile's epilogue stores drain while the staging waves already load and split the next tile's
 // first chunk, and the next tile's MFMAs start without a fresh workgroup launch.
-template <int MT, int NTW>
+template <int MT, int NTW, int SL = QSLOTS>
 __global__ __launch_bounds__(QTHREADS) FFC_CONVQ_WPE void convq_kernel(ConvQArgs args_byval) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -760,7 +761,7 @@ __global__ __launch_bounds__(QTHREADS) FFC_CONVQ_WPE void convq_kernel(ConvQArgs
     const ConvQArgs& args = args_byval;
 #endif
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW>(args, tix, lds);
+    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW, SL>(args, tix, lds);
 }
 
 // K split, second pass: workgroup = one output tile (slot), wave w = phase w; adds the ksplit
@@ -844,9 +845,9 @@ int persistent_grid(const void* k, size_t lds, int ntiles) {
     return ntiles < slots ? ntiles : slots;
 }
 
-template <int MT, int NTW>
+template <int MT, int NTW, int SL = QSLOTS>
 int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const int4* slots, int nslots) {
-    auto k = convq_kernel<MT, NTW>;
+    auto k = convq_kernel<MT, NTW, SL>;
     if (lds > 64 * 1024) {
         static bool raised = false;   // per instantiation
         if (!raised) {
@@ -869,6 +870,15 @@ int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const in
         hipLaunchKernelGGL(r, dim3(nslots), dim3(256), 0, s, a, slots);
     }
     return ffc::launch_status("ffc_convq_forward_split");
+}
+
+int slots11() {
+    static const int v = [] {
+        const char* e = getenv("FFC_CONVQ_SLOTS11");
+        const int n = e ? atoi(e) : 0;
+        return (n == 3 || n == 4) ? n : QSLOTS;
+    }();
+    return v;
 }
 
 }  // namespace
@@ -1038,7 +1048,15 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
         case 0: rc = launch_q<1, 4>(a, ntiles, lds, s, sl, nslots); break;
         case 1: rc = launch_q<1, 2>(a, ntiles, lds, s, sl, nslots); break;
         case 2: rc = launch_q<2, 2>(a, ntiles, lds, s, sl, nslots); break;
-        case 3: rc = launch_q<1, 1>(a, ntiles, lds, s, sl, nslots); break;
+        case 3:
+            // the (1, 1) tile's chunk period is one MFMA tile (768 cycles): its staging loads get more
+            // register slots in flight (FFC_CONVQ_SLOTS11 = 2 | 3 | 4) to cover the memory latency
+            switch (slots11()) {
+                case 3: rc = launch_q<1, 1, 3>(a, ntiles, lds, s, sl, nslots); break;
+                case 4: rc = launch_q<1, 1, 4>(a, ntiles, lds, s, sl, nslots); break;
+                default: rc = launch_q<1, 1>(a, ntiles, lds, s, sl, nslots); break;
+            }
+            break;
         default: ffc::set_error("ffc_convq_forward: unknown cfg"); return FFC_E_INVALID;
     }
     if (rc != FFC_OK) return rc;
