@@ -123,38 +123,66 @@ __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool l
 // shift_out of channel o (exactly one workgroup per channel leads); num_batches_tracked is bumped by
 // the caller (one lane of the workgroup leading channel 0).  Needs momentum >= 0 (no read of
 // num_batches_tracked: with per-channel leaders that read would race with the bump).
+template <int CTRL>
+__device__ __forceinline__ double dpp_full_f64(double v) {
+    const long long iv = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)iv, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(iv >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// v + v of the lane 16 (SWAP16) or 32 lanes away, through v_permlane16_swap / v_permlane32_swap
+template <bool SWAP16>
+__device__ __forceinline__ double permlane_sum_f64(double v) {
+    const long long iv = __builtin_bit_cast(long long, v);
+    const int lo = (int)iv, hi = (int)(iv >> 32);
+    const auto sl = SWAP16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                           : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto sh = SWAP16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                           : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const double a = __builtin_bit_cast(double, ((long long)(int)sh[0] << 32) | (unsigned)(int)sl[0]);
+    const double b = __builtin_bit_cast(double, ((long long)(int)sh[1] << 32) | (unsigned)(int)sl[1]);
+    return a + b;
+}
+// sum over aligned groups of L lanes (L = 1 .. 64, a power of two) by symmetric DPP / permlane steps
+// (each v += partner(v) with an involutive partner): every lane of a group holds the bit-identical sum
+template <int L>
+__device__ __forceinline__ double group_sum_f64(double v) {
+    if constexpr (L >= 2) v += dpp_full_f64<0xB1>(v);     // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (L >= 4) v += dpp_full_f64<0x4E>(v);     // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (L >= 8) v += dpp_full_f64<0x141>(v);    // row_half_mirror: the other quad of the 8
+    if constexpr (L >= 16) v += dpp_full_f64<0x140>(v);   // row_mirror: the other 8 of the row
+    if constexpr (L >= 32) v = permlane_sum_f64<true>(v);
+    if constexpr (L >= 64) v = permlane_sum_f64<false>(v);
+    return v;
+}
+
 template <int L>
 __device__ inline void bn_fold_channels(const ffc_bn_fold& f, int o, bool leader, float& scale, float& shift) {
     static_assert(L >= 1 && L <= 64 && (L & (L - 1)) == 0, "lanes per channel");
     const int gl = threadIdx.x & (L - 1);
-    const float4* slab = reinterpret_cast<const float4*>(f.slab) + o;
+    // rows through a buffer descriptor: a row past the slab is a load at offset OOB that reads a
+    // zero-count entry (a predicated load would compile to a branch and a wait per row)
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(f.slab, (unsigned long long)f.nrows * f.C * 16);
     double n = 0.0, s = 0.0, q = 0.0;
-    int r = gl;
-    for (; r + 3 * L < f.nrows; r += 4 * L) {
-        float4 e[4];
+    // up to 8 rows per lane in flight per round: one memory round trip for <= 8 L rows (the usual case)
+    for (int r0 = gl; r0 < f.nrows; r0 += 8 * L) {
+        floatx4 e[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = slab[(size_t)(r + L * u) * f.C];
+        for (int u = 0; u < 8; ++u) {
+            const int r = r0 + L * u;
+            e[u] = buf_ld4(rs, r < f.nrows ? (unsigned)((r * f.C + o) * 16) : OOB);
+        }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double en = e[u].x, em = e[u].y;
+        for (int u = 0; u < 8; ++u) {
+            const double en = e[u][0], em = e[u][1];
             n += en;
             s += en * em;
-            q += (double)e[u].z + en * em * em;
+            q += (double)e[u][2] + en * em * em;
         }
     }
-    for (; r < f.nrows; r += L) {
-        const float4 e = slab[(size_t)r * f.C];
-        const double en = e.x, em = e.y;
-        n += en;
-        s += en * em;
-        q += (double)e.z + en * em * em;
-    }
-#pragma unroll
-    for (int m = 1; m < L; m <<= 1) {
-        n += shfl_xor_f64(n, m);
-        s += shfl_xor_f64(s, m);
-        q += shfl_xor_f64(q, m);
-    }
+    n = group_sum_f64<L>(n);
+    s = group_sum_f64<L>(s);
+    q = group_sum_f64<L>(q);
     const double mu = s / n;
     double v = q / n - mu * mu;
     if (v < 0.0) v = 0.0;

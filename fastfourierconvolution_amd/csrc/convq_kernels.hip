@@ -276,9 +276,35 @@ __device__ __forceinline__ void convq_epilogue(const ffc_convp_job& J, int wave,
 // One output tile (one row of the tile table) of one workgroup; returns when the tile is done (the
 // staging waves after their last barrier of the tile, the compute waves after the epilogue).  Every
 // wave of the workgroup runs the same tiles, so the barrier counts match tile by tile.
-template <int MT, int NTW, int SL = QSLOTS>
+// PX pixels per staging unit (4, 2 or 1): a unit = PX consecutive pixels x 8 channels, loaded as 8
+// PX-float buffer loads (one per channel), split and stored pixel by pixel.  Small tiles (a few
+// patch rows per chunk: the per-rank batches of strong scaling) have far fewer 4-pixel units than
+// staging threads, and one unit's loads + split + stores are the chunk's staging chain; PX = 1 runs
+// the same work on 4x the threads (host: the smallest PX whose units fit the 256 staging threads).
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+template <int PX>
+struct StageVec {
+    float v[PX];
+};
+template <int PX>
+__device__ __forceinline__ StageVec<PX> stage_ld(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    StageVec<PX> r;
+    if constexpr (PX == 4) {
+        const floatx4 q = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+        r.v[0] = q[0]; r.v[1] = q[1]; r.v[2] = q[2]; r.v[3] = q[3];
+    } else if constexpr (PX == 2) {
+        const floatx2 q = __builtin_bit_cast(floatx2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+        r.v[0] = q[0]; r.v[1] = q[1];
+    } else {
+        r.v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+    }
+    return r;
+}
+
+template <int MT, int NTW, int SL = QSLOTS, int PX = 4>
 __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix, char* lds) {
     static_assert(SL >= 2 && SL <= 6, "convq staging slots");
+    static_assert(PX == 1 || PX == 2 || PX == 4, "pixels per staging unit");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave_id = __builtin_amdgcn_readfirstlane(tid >> 6);
     const bool stager = wave_id >= 4;
@@ -363,7 +389,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
         st.Cpad = S.Cpad;
         st.cfull = (S.C & 15) == 0;
         st.cstride = (unsigned)IHW * 4u;
-        const int PR = S.PR, G = S.PC >> 2, QR = S.qrow, QS = S.qsample;
+        const int PR = S.PR, G = S.PC / PX, QR = S.qrow, QS = S.qsample;
         const int ngrp = NS * PR * G;
         const int nunits = 2 * ngrp;
         const int iy0 = r0 * S.mult_y + S.org_y;
@@ -373,28 +399,27 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
         const int q = n - hu * ngrp;
         const int g = q % G, q1 = q / G;
         const int pr = q1 % PR, ns = q1 / PR;
-        const int b = b0 + ns, iy = iy0 + pr, ix = xa + 4 * g;
+        const int b = b0 + ns, iy = iy0 + pr, ix = xa + PX * g;
         const bool ok = n < nunits && b < J.B && (unsigned)iy < (unsigned)S.IH && (unsigned)ix < (unsigned)S.IW;
         st.voff = ok ? (unsigned)(((b * S.C + 8 * hu) * IHW + iy * S.IW + ix) * 4) : ffc::OOB;
         st.hu8 = 8 * hu;
-        st.wb = n < nunits ? ((hu * NS + ns) * QS + pr * QR + 4 * g) * 48 : -1;
+        st.wb = n < nunits ? ((hu * NS + ns) * QS + pr * QR + PX * g) * 48 : -1;
     };
-    auto stage_load = [&](floatx4 (&sv)[8], int ch0) {
+    auto stage_load = [&](StageVec<PX> (&sv)[8], int ch0) {
         const unsigned sbase = (unsigned)ch0 * st.cstride;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const unsigned vo = (st.cfull || ch0 + st.hu8 + j < st.C) ? st.voff : ffc::OOB;
-            sv[j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     st.rs, (int)vo, (int)(sbase + (unsigned)j * st.cstride), 0));
+            sv[j] = stage_ld<PX>(st.rs, (int)vo, (int)(sbase + (unsigned)j * st.cstride));
         }
     };
-    auto stage_store = [&](const floatx4 (&sv)[8], int wb, char* buf) {
+    auto stage_store = [&](const StageVec<PX> (&sv)[8], int wb, char* buf) {
         if (wb >= 0) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < PX; ++e) {
                 float v8[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) v8[j] = sv[j][e];
+                for (int j = 0; j < 8; ++j) v8[j] = sv[j].v[e];
                 const Split3 sp = split3(v8);
                 u32x4* d = reinterpret_cast<u32x4*>(buf + wb + 48 * e);
                 d[0] = __builtin_bit_cast(u32x4, sp.hi);
@@ -462,7 +487,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             unsigned long long q0, qa, qb, ql = 0, qs = 0, qw = 0, qi = 0;
             QSTAMP(q0);
 #endif
-            floatx4 sv[SL][8];
+            StageVec<PX> sv[SL][8];
             int wbs[SL];
             stage_setup(ss);
             // the chunk at the load cursor (ss, sch); past the last chunk the loads still issue (the
@@ -470,7 +495,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
             // the compiler's wait counts stay exact (a conditional issue made it wait for every
             // outstanding load at the loop head, serialising the pipeline)
             int ic = 0;   // chunks issued (this workgroup's K range is chunks 0 .. nst - 1)
-            auto issue = [&](floatx4 (&dst)[8], int& wb) {
+            auto issue = [&](StageVec<PX> (&dst)[8], int& wb) {
                 const bool live = ss < nseg && ic < nst;
                 ++ic;
                 stage_load(dst, live ? sch : 0);
@@ -484,10 +509,10 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
                     }
                 }
             };
-            auto store_timed = [&](const floatx4 (&src)[8], int wb, char* buf) {
+            auto store_timed = [&](const StageVec<PX> (&src)[8], int wb, char* buf) {
 #ifdef FFC_TRACE_Q
                 QSTAMP(qa);
-                float chk = src[0][0] + src[7][3];
+                float chk = src[0].v[0] + src[7].v[PX - 1];
                 asm volatile("" ::"v"(chk));   // data arrived
                 QSTAMP(qb);
                 ql += qb - qa;
@@ -753,7 +778,7 @@ __device__ __forceinline__ void convq_tile(const ConvQArgs& args, const int tix,
 // multiple of 8, so every tile of a workgroup comes from its XCD's range of the XCD-remapped table).
 // A tile's epilogue stores drain while the staging waves already load and split the next tile's
 // first chunk, and the next tile's MFMAs start without a fresh workgroup launch.
-template <int MT, int NTW, int SL = QSLOTS>
+template <int MT, int NTW, int SL = QSLOTS, int PX = 4>
 __global__ __launch_bounds__(QTHREADS) FFC_CONVQ_WPE void convq_kernel(ConvQArgs args_byval) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const ConvQArgs& args = *(const ConvQArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -761,7 +786,7 @@ __global__ __launch_bounds__(QTHREADS) FFC_CONVQ_WPE void convq_kernel(ConvQArgs
     const ConvQArgs& args = args_byval;
 #endif
     extern __shared__ __attribute__((aligned(16))) char lds[];
-    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW, SL>(args, tix, lds);
+    for (int tix = blockIdx.x; tix < args.ntiles; tix += gridDim.x) convq_tile<MT, NTW, SL, PX>(args, tix, lds);
 }
 
 // K split, second pass: workgroup = one output tile (slot), wave w = phase w; adds the ksplit
@@ -845,9 +870,9 @@ int persistent_grid(const void* k, size_t lds, int ntiles) {
     return ntiles < slots ? ntiles : slots;
 }
 
-template <int MT, int NTW, int SL = QSLOTS>
+template <int MT, int NTW, int SL = QSLOTS, int PX = 4>
 int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const int4* slots, int nslots) {
-    auto k = convq_kernel<MT, NTW, SL>;
+    auto k = convq_kernel<MT, NTW, SL, PX>;
     if (lds > 64 * 1024) {
         static bool raised = false;   // per instantiation
         if (!raised) {
@@ -870,6 +895,15 @@ int launch_q(const ConvQArgs& a, int ntiles, size_t lds, hipStream_t s, const in
         hipLaunchKernelGGL(r, dim3(nslots), dim3(256), 0, s, a, slots);
     }
     return ffc::launch_status("ffc_convq_forward_split");
+}
+
+int stage_px(int units4) {
+    static const int force = [] {
+        const char* e = getenv("FFC_CONVQ_PX");
+        return e ? atoi(e) : 0;
+    }();
+    const int fit = 4 * units4 <= 256 ? 1 : (2 * units4 <= 256 ? 2 : 4);   // one unit per staging thread
+    return (force == 1 || force == 2 || force == 4) && force >= fit ? force : fit;
 }
 
 int slots11() {
@@ -981,7 +1015,7 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
                   "ffc_convq_forward: ksplit > 1 needs the partial buffer (16-byte aligned)");
     FFC_CHECK_ARG(ksplit == 1 || (slot_tiles && nslots > 0 && (long long)nslots * ksplit == ntiles),
                   "ffc_convq_forward: ksplit > 1 needs the slot table (ntiles = nslots * ksplit)");
-    int npix_max = 0;
+    int npix_max = 0, units4 = 0;
     for (int j = 0; j < njobs; ++j) {
         const ffc_convp_job& J = jobs[j];
         FFC_CHECK_ARG(J.A3 && J.out && J.B > 0 && J.M > 0, "ffc_convq_forward: incomplete job (needs the A3 planes)");
@@ -1016,6 +1050,7 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
                               "ffc_convq_forward: staged segments are read through 32-bit buffer offsets (< 2 GiB)");
                 FFC_CHECK_ARG(2 * J.NS * S.PR * (S.PC / 4) <= 256,
                               "ffc_convq_forward: patch too large for the staging waves (one unit per thread)");
+                if (2 * J.NS * S.PR * (S.PC / 4) > units4) units4 = 2 * J.NS * S.PR * (S.PC / 4);
                 const int npix = J.NS * S.qsample;   // LDS image pixels per channel half
                 if (npix > npix_max) npix_max = npix;
             }
@@ -1043,19 +1078,25 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
             Jc.act = FFC_ACT_IDENTITY;
         }
     }
+    // pixels per staging unit: the smallest of 1, 2, 4 whose units fit the 256 staging threads
+    // (FFC_CONVQ_PX = 4 keeps the 4-pixel units everywhere: A/B)
+    const int px = stage_px(units4);
     int rc = FFC_E_INVALID;
     switch (cfg) {
         case 0: rc = launch_q<1, 4>(a, ntiles, lds, s, sl, nslots); break;
-        case 1: rc = launch_q<1, 2>(a, ntiles, lds, s, sl, nslots); break;
+        case 1:
+            if (px <= 2) rc = launch_q<1, 2, QSLOTS, 2>(a, ntiles, lds, s, sl, nslots);
+            else rc = launch_q<1, 2>(a, ntiles, lds, s, sl, nslots);
+            break;
         case 2: rc = launch_q<2, 2>(a, ntiles, lds, s, sl, nslots); break;
         case 3:
-            // the (1, 1) tile's chunk period is one MFMA tile (768 cycles): its staging loads get more
-            // register slots in flight (FFC_CONVQ_SLOTS11 = 2 | 3 | 4) to cover the memory latency
-            switch (slots11()) {
-                case 3: rc = launch_q<1, 1, 3>(a, ntiles, lds, s, sl, nslots); break;
-                case 4: rc = launch_q<1, 1, 4>(a, ntiles, lds, s, sl, nslots); break;
-                default: rc = launch_q<1, 1>(a, ntiles, lds, s, sl, nslots); break;
-            }
+            // the (1, 1) tile: pixels per staging unit by the patch size (stage_px); FFC_CONVQ_SLOTS11 = 3 | 4
+            // keeps more chunks' loads in flight (measured slower: it halves the workgroups per CU, r05a)
+            if (slots11() == 3) rc = launch_q<1, 1, 3>(a, ntiles, lds, s, sl, nslots);
+            else if (slots11() == 4) rc = launch_q<1, 1, 4>(a, ntiles, lds, s, sl, nslots);
+            else if (px == 1) rc = launch_q<1, 1, QSLOTS, 1>(a, ntiles, lds, s, sl, nslots);
+            else if (px == 2) rc = launch_q<1, 1, QSLOTS, 2>(a, ntiles, lds, s, sl, nslots);
+            else rc = launch_q<1, 1>(a, ntiles, lds, s, sl, nslots);
             break;
         default: ffc::set_error("ffc_convq_forward: unknown cfg"); return FFC_E_INVALID;
     }

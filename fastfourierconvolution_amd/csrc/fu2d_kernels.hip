@@ -203,7 +203,8 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_kernel(R2cArgs a) {
     if (!PLANAR && a.has_fold) {
         // bn1 of this plane's channel from its slab rows, under the plane loads' latency; the
         // workgroups of sample 0 lead (running statistics, scale_out / shift_out for the C2R)
-        __shared__ float fsc[2];
+        float* fsc = smem + h * RS + 2 * h * ZS;   // 16 B behind the planes (r2c_lds; no static LDS:
+                                                   // it would cap the dynamic size below 160 KiB)
         if (tid < 64) {
             float fs, fh;
             ffc::bn_fold_channel(a.fold, ch, plane < a.C, fs, fh);
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_c2r_kernel(C2rArgs a) {
             if (a.has_bn_fold) {
                 // the FU's BN of this plane's two spectral channels (Re 2c, Im 2c+1) from pass 0's slab
                 // rows, waves 0 and 1 in parallel, under the Y loads' latency
-                __shared__ float fbn[4];
+                float* fbn = reinterpret_cast<float*>(Z + H * ZS);   // 16 B behind the plane (c2r_lds)
                 const int wv = tid >> 6;
                 if (wv < 2) {
                     float fs, fh;
@@ -1174,8 +1175,9 @@ C2rKernel pick_rows(int H, int W, int up) {
     return nullptr;
 }
 
-size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * zstride(w / 2 + 1) * 8; }
-size_t c2r_lds(int H, int W) { return (size_t)H * zstride(W / 2 + 1) * 8; }
+// + 16 B: the in-kernel BN fold's scale / shift behind the planes
+size_t r2c_lds(int h, int w) { return (size_t)h * (w + 4) * 4 + (size_t)h * zstride(w / 2 + 1) * 8 + 16; }
+size_t c2r_lds(int H, int W) { return (size_t)H * zstride(W / 2 + 1) * 8 + 16; }
 size_t mix_wm_floats(int C) { return (size_t)(2 * C) * ((2 * C + 31) / 32 * 32); }
 size_t mix_lds(int C, int pass, bool f16 = false) {
     const size_t wm = f16 ? 0 : (mix_wm_floats(C) + 255) / 256 * 256;   // <= 64 KiB for 2C <= 128

@@ -175,6 +175,7 @@ def test_backward_channels_last_input(op):
     gradients equal those of the same values in NCHW (the backward read the saved raw x)"""
     x0 = torch.randn(4, 32, 8, 8, device=DEV)
     dy = torch.randn(4, 32, 8, 8, device=DEV)
+    w_se = (0.3 * torch.randn(2, 32, device=DEV), 0.3 * torch.randn(32, 2, device=DEV))
     res = []
     for x in (x0.clone(), x0.clone().to(memory_format=torch.channels_last)):
         x.requires_grad_()
@@ -184,8 +185,7 @@ def test_backward_channels_last_input(op):
             y = torch.ops.ffc.bn_act(x, gm, bt, None, None, True, 1e-5, 2, 0.1)[0]
             params = (gm, bt)
         else:
-            gm = (0.3 * torch.randn(2, 32, device=DEV)).requires_grad_()
-            bt = (0.3 * torch.randn(32, 2, device=DEV)).requires_grad_()
+            gm, bt = (w.clone().requires_grad_() for w in w_se)
             y = torch.ops.ffc.se_scale(x, gm, bt)
             params = (gm, bt)
         (y * dy).sum().backward()
@@ -222,14 +222,27 @@ def test_threaded_replicas_bitwise_equal_serial():
     for g, sd in zip(reps, init):
         g.load_state_dict(sd)
     torch.cuda.synchronize()
-    held = {}
-    orig_take = ops._TemplatePool._take
+    from fastfourierconvolution_amd import _runtime as rt
+    held, used, clash = set(), {}, []
+    lock = threading.Lock()
+    orig_take, orig_give = rt.StreamPool.take, rt.StreamPool.give
 
     def spy_take(self):
-        inst = orig_take(self)
-        held.setdefault(threading.get_ident(), set()).add(id(inst))
-        return inst
-    ops._TemplatePool._take = spy_take
+        obj = orig_take(self)
+        if isinstance(obj, ops._Template):
+            with lock:
+                if id(obj) in held:
+                    clash.append(id(obj))   # checked out twice at once
+                held.add(id(obj))
+                used.setdefault(threading.get_ident(), set()).add(id(obj))
+        return obj
+
+    def spy_give(self, obj):
+        if isinstance(obj, ops._Template):
+            with lock:
+                held.discard(id(obj))
+        orig_give(self, obj)
+    rt.StreamPool.take, rt.StreamPool.give = spy_take, spy_give
     outs = [[None] * n_iter for _ in reps]
     errors = []
     bar = threading.Barrier(2)
@@ -251,7 +264,7 @@ def test_threaded_replicas_bitwise_equal_serial():
         for t in ths:
             t.join(timeout=120)
     finally:
-        ops._TemplatePool._take = orig_take
+        rt.StreamPool.take, rt.StreamPool.give = orig_take, orig_give
     torch.cuda.synchronize()
     assert not errors, errors
     for k in range(2):
@@ -259,5 +272,7 @@ def test_threaded_replicas_bitwise_equal_serial():
             assert torch.equal(outs[k][i], serial[k][i]), (k, i)
         for key, v in reps[k].state_dict().items():
             assert torch.equal(v, after_serial[k][key]), key
-    ids = list(held.values())
-    assert len(ids) == 2 and not (ids[0] & ids[1]), "the two threads shared a template instance"
+    assert not clash, "a template instance was held by two callers at once"
+    assert len(used) == 2, used.keys()
+    insts = {ops.template(ops.layer_spec(m)).instances for m in reps[0].modules() if hasattr(m, "_ffc_ctor")}
+    print(f"template instances per spec after the threaded run: {sorted(insts)}")
