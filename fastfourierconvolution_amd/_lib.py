@@ -144,6 +144,10 @@ SIGNATURES = [
     ("ffc_st_prologue_split", c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     ("ffc_st_prologue_ex", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                    c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("ffc_st_pack_a3_elems", c_size_t, [c_int, c_int]),
+    ("ffc_st_pack_a3", c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    ("ffc_st_prologue_ex3", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("ffc_fu2d_supported", c_int, [c_int, c_int, c_int, c_int]),
     ("ffc_fu2d_slab_rows", c_int, [c_int, c_int, c_int, c_int]),
     ("ffc_fu2d_r2c", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

@@ -281,6 +281,8 @@ def _pow2_floor(v: int) -> int:
 
 
 ST_SPLIT_MAX = _pow2_floor(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "8"))   # cap, rounded to 2^k
+# ST prologue conv1 on the split-bf16 MFMA products (FFC_ST_MFMA=f32: the exact f32-input MFMA, A/B)
+ST_SPLIT_MFMA = __import__("os").environ.get("FFC_ST_MFMA", "split") != "f32"
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
 FU_SPILL = __import__("os").environ.get("FFC_FU_SPILL", "1") != "0"
 
@@ -585,7 +587,7 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS)
+            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, ST_SPLIT_MFMA)
 
 
 def algorithmic_flops(plan) -> float:

@@ -71,6 +71,7 @@ struct FuArgs {
     ffc_bn_fold in_fold, mix_fold;   // BNs finalized in-kernel (has_*: in use)
     int has_in_fold, has_mix_fold;
     float* yspill;                   // (B, 2C, NB) mix output: written by pass 0, read by pass 1
+    int mix3;                        // mix on split-bf16 MFMA products (C % 8 == 0), else f32-input MFMA
 };
 
 constexpr int FU_THREADS = 512;
@@ -238,7 +239,23 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
         const float* zp = (h ? Zim : Zre) + nt * 32 + col;
         const int wstep = 2 * a.Mpad;
-        if (a.wm_lds) {
+        if (a.mix3) {
+            // fp32-accurate split-bf16 products (ffc_internal.h split3 / mfma_split3): k-block q, lane
+            // half h element j is k = 2 (8q + j) + h -- channel 8q + j, Re (h = 0) or Im (h = 1) --
+            // in both operands; six bf16 MFMAs per 16 k instead of eight f32 MFMAs at twice the cycles
+            const float* wsrc = a.wm_lds ? Wm : a.wmixT;
+            const float* wq = wsrc + h * a.Mpad + mt * 32 + col;
+#pragma unroll 2
+            for (int q = 0; q < C / 8; ++q) {
+                float av[8], zv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    av[j] = wq[(size_t)(8 * q + j) * wstep];
+                    zv[j] = zp[(8 * q + j) * NB];
+                }
+                acc = mfma_split3(split3(av), split3(zv), acc);
+            }
+        } else if (a.wm_lds) {
             const float* wp = Wm + h * a.Mpad + mt * 32 + col;
 #pragma unroll 8
             for (int s = 0; s < C; ++s)
@@ -505,6 +522,16 @@ FuKernel pick_split(int H, int W, int up) {
     }
     return nullptr;
 }
+// FFC_FU_MFMA=split: the fused mix on the split-bf16 products instead of the exact f32-input MFMA.
+// Off by default: measured neutral (gen64 B = 256 fu_pass0 51 vs 52 us per step, B = 32 the same,
+// r05f) -- the fused mix waits on its LDS operand reads and the per-tile statistics, not the MFMA
+bool fu_mix3_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("FFC_FU_MFMA");
+        return e && e[0] == 's';
+    }();
+    return on;
+}
 // FFC_FU_SPLIT=0: pass 1 as one workgroup per sample (fu_kernel) for A/B runs
 bool fu_split_on() {
     static const bool on = [] {
@@ -613,6 +640,7 @@ extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int
     }
     if (mix_fold) a.mix_fold = *mix_fold;
     a.yspill = yspill;
+    a.mix3 = fu_mix3_on() && C % 8 == 0;
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;

@@ -25,6 +25,8 @@ struct StArgs {
     float* slab;         // [B][c] float4
     float* gate_out;     // optional (B, Cin) copy of the gate (tests / debugging), may be null
     int Cin, H, W, pool, hid, c;
+    const uint16_t* wc3; // optional: conv1 weight as split-bf16 MFMA fragments (ffc_st_pack_a3); else the
+                         // exact f32-input MFMA on wcT
     int x_dma;           // sample copied by LDS-DMA (no pooling, 16-byte aligned rows)
     int split;           // workgroups per sample: each takes 1/split of conv1's output tiles
     // LDS layout (float offsets; -1: not staged, read from global)
@@ -191,6 +193,35 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         }
         return acc;
     };
+    // split-bf16 products (ffc_internal.h split3 / mfma_split3: fp32-accurate, six bf16 MFMAs per 16 k
+    // instead of eight f32 MFMAs at twice their cycles): k-block q of 16 channels, lane half h2 holds
+    // channels 16q + 8 h2 + j; A from the pre-split fragments (three coalesced 16-byte loads), B = the
+    // gated sample split in registers
+    const int KQ = Cin >> 4;
+    auto mfma_range3 = [&](int mt, int nt, int q0, int q1) {
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        const int p = nt * 32 + col;
+        const int pc = p < hw ? p : hw - 1;
+        const float* xp = xs + pc;
+        const uint16_t* af = a.wc3 + (size_t)mt * KQ * 1536 + lane * 8;
+#pragma unroll 2
+        for (int q = q0; q < q1; ++q) {
+            const uint16_t* f = af + (size_t)q * 1536;
+            Split3 A;
+            A.hi = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(f));
+            A.mid = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(f + 512));
+            A.lo = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(f + 1024));
+            float xb[8];
+            const int k0 = 16 * q + 8 * h2;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xb[j] = xp[(k0 + j) * hw] * gate[k0 + j];
+            acc = mfma_split3(A, split3(xb), acc);
+        }
+        return acc;
+    };
+    const bool use3 = a.wc3 != nullptr;
     auto finish = [&](int mt, int nt, const floatx16& acc) {
         const int p = nt * 32 + col;
         const bool valid = p < hw;
@@ -213,14 +244,19 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     if (nsplit == 1) {
         for (int tl = wave; tl < tiles; tl += ST_THREADS / 64) {
             const int tile = t0 + tl, mt = tile % MT, nt = tile / MT;
-            finish(mt, nt, mfma_range(mt, nt, 0, KS, true));
+            finish(mt, nt, use3 ? mfma_range3(mt, nt, 0, KQ) : mfma_range(mt, nt, 0, KS, true));
         }
     } else {
         const int tl = wave / nsplit, part = wave % nsplit, tile = t0 + tl;
         const int mt = tile % MT, nt = tile / MT;
-        const int per = (KS + nsplit - 1) / nsplit;
         floatx16 acc;
-        if (tl < tiles) acc = mfma_range(mt, nt, min(KS, part * per), min(KS, (part + 1) * per), part == 0);
+        if (use3) {
+            const int per = (KQ + nsplit - 1) / nsplit;
+            if (tl < tiles) acc = mfma_range3(mt, nt, min(KQ, part * per), min(KQ, (part + 1) * per));
+        } else {
+            const int per = (KS + nsplit - 1) / nsplit;
+            if (tl < tiles) acc = mfma_range(mt, nt, min(KS, part * per), min(KS, (part + 1) * per), part == 0);
+        }
         if (tl < tiles && part > 0) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
@@ -310,7 +346,40 @@ StLayout st_layout(int Cin, int H, int W, int pool, int hid, int c) {
     return L;
 }
 
+// conv1 weight (c, Cin) row-major -> split-bf16 MFMA fragments: element
+// ((mt * Cin/16 + q) * 3 + piece) * 512 + lane * 8 + j holds piece `piece` of
+// W[m = 32 mt + (lane & 31)][k = 16 q + 8 (lane >> 5) + j] (zero for m >= c)
+__global__ void st_pack_a3_kernel(const float* __restrict__ w, int c, int cin, uint16_t* __restrict__ out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int lane = i & 63, fr = i >> 6;
+    const int KQ = cin >> 4;
+    const int mt = fr / KQ, q = fr - mt * KQ;
+    const int m = 32 * mt + (lane & 31), k0 = 16 * q + 8 * (lane >> 5);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = m < c ? w[(size_t)m * cin + k0 + j] : 0.0f;
+    const Split3 sp = split3(v);
+    uint16_t* dst = out + (size_t)fr * 1536 + lane * 8;
+    *reinterpret_cast<u32x4*>(dst) = __builtin_bit_cast(u32x4, sp.hi);
+    *reinterpret_cast<u32x4*>(dst + 512) = __builtin_bit_cast(u32x4, sp.mid);
+    *reinterpret_cast<u32x4*>(dst + 1024) = __builtin_bit_cast(u32x4, sp.lo);
+}
+
 }  // namespace
+
+extern "C" size_t ffc_st_pack_a3_elems(int c, int cin) {
+    if (c <= 0 || cin <= 0 || cin % 16 || c > 65536 || cin > 65536) return 0;
+    return (size_t)((c + 31) / 32) * (cin / 16) * 1536;
+}
+
+extern "C" int ffc_st_pack_a3(const float* w, int c, int cin, uint16_t* out, void* stream) {
+    FFC_CHECK_ARG(w && out && ffc_st_pack_a3_elems(c, cin) > 0, "ffc_st_pack_a3: bad args (Cin % 16 == 0)");
+    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(out) & 15) == 0, "ffc_st_pack_a3: out must be 16-byte aligned");
+    const int n = (c + 31) / 32 * (cin / 16) * 64;
+    hipLaunchKernelGGL(st_pack_a3_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, c, cin, out, n);
+    return ffc::launch_status("ffc_st_pack_a3");
+}
 
 #ifdef FFC_TRACE
 extern "C" int ffc_debug_st_trace_read(void* dst, size_t bytes) {
@@ -346,7 +415,16 @@ extern "C" int ffc_st_prologue(const float* x, int B, int Cin, int H, int W, int
 extern "C" int ffc_st_prologue_ex(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
                                   const float* w2, int hidden, const float* wconv1T, int c, int split, float* t,
                                   float* slab, float* gate_out, void* stream) {
+    return ffc_st_prologue_ex3(x, B, Cin, H, W, pool, w1, w2, hidden, wconv1T, nullptr, c, split, t, slab, gate_out,
+                               stream);
+}
+
+extern "C" int ffc_st_prologue_ex3(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
+                                   const float* w2, int hidden, const float* wconv1T, const uint16_t* wc3, int c,
+                                   int split, float* t, float* slab, float* gate_out, void* stream) {
     FFC_CHECK_ARG(x && wconv1T && t && slab && B > 0, "ffc_st_prologue: bad args");
+    FFC_CHECK_ARG(!wc3 || (Cin % 16 == 0 && (reinterpret_cast<uintptr_t>(wc3) & 15) == 0),
+                  "ffc_st_prologue: split-bf16 conv1 fragments need Cin % 16 == 0 and 16-byte alignment");
     {
         const long long hw = (long long)(pool ? H / 2 : H) * (pool ? W / 2 : W);
         const long long T = (long long)((c + 31) / 32) * ((hw + 31) / 32);
@@ -391,6 +469,7 @@ extern "C" int ffc_st_prologue_ex(const float* x, int B, int Cin, int H, int W, 
     a.w1_off = L.w1_off;
     a.w2_off = L.w2_off;
     a.split = split;
+    a.wc3 = wc3;
     a.x_dma = !pool && ((size_t)Cin * H * W) % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     if (L.w1_off >= 0 && ((reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w2)) & 15)) {
         a.w1_off = a.w2_off = -1;   // unaligned SE weights: read from global

@@ -99,6 +99,21 @@ class SpectralTransform(nn.Module):
             return c1T
         return self.__dict__.setdefault("_packs", rt.PackCache()).get("conv1T", [w], build)
 
+    def _conv1_3(self, stream):
+        """conv1 weight as split-bf16 MFMA fragments for ffc_st_prologue_ex3 (None: Cin % 16 != 0 or
+        FFC_ST_MFMA=f32)"""
+        w = rt.require(self.conv1.weight.detach(), "conv1.weight")
+        c, cin = w.shape[0], w.shape[1]
+        n = rt.lib().ffc_st_pack_a3_elems(c, cin)
+        if not n or not rt.ST_SPLIT_MFMA:
+            return None
+
+        def build():
+            wc3 = torch.empty(n, device=w.device, dtype=torch.int16)
+            check(rt.lib().ffc_st_pack_a3(ptr(w), c, cin, ptr(wc3), stream), "ffc_st_pack_a3")
+            return wc3
+        return self.__dict__.setdefault("_packs", rt.PackCache()).get("conv1_3", [w], build)
+
     def _mode(self):
         if self.stride == 2 and self.upsample:
             return 1, 2  # pool, up
@@ -136,9 +151,10 @@ class SpectralTransform(nn.Module):
             split = min(L.ffc_st_prologue_split(B, Cin, H, W, int(pool), c), rt.ST_SPLIT_MAX) if rt.ST_SPLIT else 1
             nrows = B * split
             slab = torch.empty((nrows, c, 4), device=dev, dtype=torch.float32)
+            wc3 = self._conv1_3(stream)
             with rt.observe("st_prologue", flops=2.0 * B * c * Cin * h2 * w2):
-                check(L.ffc_st_prologue_ex(ptr(x), B, Cin, H, W, int(pool), ptr(se1), ptr(se2), hid, ptr(wc), c, split,
-                                           ptr(t), ptr(slab), None, stream), "ffc_st_prologue")
+                check(L.ffc_st_prologue_ex3(ptr(x), B, Cin, H, W, int(pool), ptr(se1), ptr(se2), hid, ptr(wc),
+                                            ptr(wc3), c, split, ptr(t), ptr(slab), None, stream), "ffc_st_prologue")
         elif not pool and L.ffc_pw_gate_lds_bytes(Cin, c) > 0:
             # large planes: SE gate (plane means + FCs), then conv1 with the gate folded into the
             # per-sample weights and the bn1 partials in the epilogue (csrc/st_pw.hip)

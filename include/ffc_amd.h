@@ -320,6 +320,15 @@ int ffc_st_prologue_split(int B, int Cin, int H, int W, int pool, int c);
 int ffc_st_prologue_ex(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
                        const float* w2, int hidden, const float* wconv1T, int c, int split, float* t,
                        float* slab, float* gate_out, void* stream);
+/* ffc_st_prologue_ex with conv1 on fp32-accurate split-bf16 MFMA products (three exact bf16
+ * pieces per operand, six products: as the local convolutions) instead of the f32-input MFMA:
+ * wc3 = ffc_st_pack_a3(conv1.weight (c, Cin)), ffc_st_pack_a3_elems(c, Cin) uint16 elements,
+ * 16-byte aligned; Cin % 16 == 0 (0 elements: unsupported).  wc3 = NULL is ffc_st_prologue_ex. */
+size_t ffc_st_pack_a3_elems(int c, int cin);
+int ffc_st_pack_a3(const float* w, int c, int cin, uint16_t* wc3, void* stream);
+int ffc_st_prologue_ex3(const float* x, int B, int Cin, int H, int W, int pool, const float* w1,
+                        const float* w2, int hidden, const float* wconv1T, const uint16_t* wc3, int c, int split,
+                        float* t, float* slab, float* gate_out, void* stream);
 /* SpectralTransform conv1 with the SE gate for planes the fused prologue cannot hold
  * (spectral_transform.py:87-89): t[b,o,p] = sum_c w[o,c] * gate[b,c] * x[b,c,p], p < HW, plus
  * bn1 partials slab [B * ffc_pw_gate_blocks(HW)][M] float4 {n, mean, M2} (slab may be NULL).

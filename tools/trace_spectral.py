@@ -44,7 +44,7 @@ def main():
     for f in (rfu, rst):
         f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     recs = []
-    ofu, ost = L.ffc_fu_forward_ex, L.ffc_st_prologue_ex
+    ofu, ost = L.ffc_fu_forward_ex, L.ffc_st_prologue_ex3
 
     def fu(*a):
         rc = ofu(*a)
@@ -58,16 +58,16 @@ def main():
     def st(*a):
         rc = ost(*a)
         torch.cuda.synchronize()
-        B = a[1] * a[11]   # workgroups: samples x split
+        B = a[1] * a[12]   # workgroups: samples x split
         buf = np.zeros((B, 8), dtype=np.uint64)
         assert rst(buf.ctypes.data, buf.nbytes) == 0
-        recs.append(("st", f"Cin={a[2]} {a[3]}x{a[4]} c={a[10]} split={a[11]}", buf))
+        recs.append(("st", f"Cin={a[2]} {a[3]}x{a[4]} c={a[11]} split={a[12]}", buf))
         return rc
 
-    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex = fu, st
+    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex3 = fu, st
     with torch.no_grad():
         G(z)
-    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex = ofu, ost
+    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex3 = ofu, ost
     for kind, desc, buf in recs:
         rt0, rt1 = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64)
         dur = (rt1 - rt0) / 100.0
