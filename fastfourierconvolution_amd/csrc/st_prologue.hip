@@ -301,7 +301,9 @@ struct StLayout {
     int gate_off, hv_off, st_off, red_off, scr_off, wt_off, w1_off, w2_off;
 };
 size_t pad256(size_t n) { return (n + 255) / 256 * 256; }
-StLayout st_layout(int Cin, int H, int W, int pool, int hid, int c) {
+// stage_wt = false: conv1 runs on the pre-split fragments (ffc_st_pack_a3) read from L2, so its f32
+// weight is not staged (at gen64 ffc1 that copy was 64 KB of LDS-DMA per workgroup, unused)
+StLayout st_layout(int Cin, int H, int W, int pool, int hid, int c, bool stage_wt = true) {
     const int h = pool ? H / 2 : H, w = pool ? W / 2 : W;
     const size_t hw = (size_t)h * w;
     const size_t nt = (hw + 31) / 32;
@@ -323,7 +325,7 @@ StLayout st_layout(int Cin, int H, int W, int pool, int hid, int c) {
     for (int opt = 0; opt < 3; ++opt) {   // 0: conv1 + SE weights staged, 1: conv1 only, 2: neither
         size_t q = base;
         int wt = -1, w1 = -1, w2 = -1;
-        if (opt < 2) {
+        if (opt < 2 && stage_wt) {
             wt = (int)q;
             q += pad256((size_t)Cin * Mpad);
         }
@@ -431,8 +433,10 @@ extern "C" int ffc_st_prologue_ex3(const float* x, int B, int Cin, int H, int W,
         FFC_CHECK_ARG(split >= 1 && T % split == 0, "ffc_st_prologue: split must divide conv1's output tiles");
     }
     FFC_CHECK_ARG(hidden == 0 || (w1 && w2), "ffc_st_prologue: null SE weights");
-    const size_t lds = ffc_st_prologue_lds_bytes(Cin, H, W, pool, hidden, c);
-    FFC_CHECK_ARG(lds > 0, "ffc_st_prologue: sample does not fit in LDS (use se_gate + conv)");
+    FFC_CHECK_ARG(ffc_st_prologue_lds_bytes(Cin, H, W, pool, hidden, c) > 0,
+                  "ffc_st_prologue: sample does not fit in LDS (use se_gate + conv)");
+    const StLayout L = st_layout(Cin, H, W, pool, hidden, c, wc3 == nullptr);
+    const size_t lds = L.bytes;
     if (lds > 64 * 1024) {
         static std::once_flag once;
         static hipError_t err = hipSuccess;
@@ -459,7 +463,6 @@ extern "C" int ffc_st_prologue_ex3(const float* x, int B, int Cin, int H, int W,
     a.pool = pool;
     a.hid = hidden;
     a.c = c;
-    const StLayout L = st_layout(Cin, H, W, pool, hidden, c);
     a.gate_off = L.gate_off;
     a.hv_off = L.hv_off;
     a.st_off = L.st_off;
