@@ -160,7 +160,7 @@ def parse():
 # kernel-name prefixes behind each observed launch label (for the PMC traffic lookup)
 LABEL_KERNELS = {"conv_gemm": ("convq_kernel", "convq_reduce_kernel", "convp_kernel", "conv_gemm_kernel"), "fu_pass0": ("fu_kernel",),
                  "fu_pass1": ("fu_kernel",), "st_prologue": ("st_prologue_kernel",),
-                 "convt_smallm": ("convt_smallm_kernel",), "fu2d_r2c": ("fu2d_r2c_kernel",),
+                 "convt_smallm": ("convt_smallm_kernel",), "fu2d_r2c": ("fu2d_r2c_kernel", "fu2d_r2c_mix_kernel"),
                  "fu2d_mix0": ("fu2d_mix_kernel",), "fu2d_mix1": ("fu2d_mix_cols_kernel", "fu2d_mix_kernel"),
                  "fu2d_c2r": ("fu2d_c2r",), "conv3_smallm": ("conv3x3_smallm_kernel",),
                  "dense": ("dense_kernel",)}

@@ -169,6 +169,9 @@ SIGNATURES = [
                                 ctypes.POINTER(BnFold), c_void_p, c_void_p]),
     ("ffc_fu2d_c2r_fold", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                   c_int, ctypes.POINTER(BnFold), c_void_p, c_void_p]),
+    ("ffc_fu2d_r2c_mix_supported", c_int, [c_int, c_int, c_int, c_int]),
+    ("ffc_fu2d_r2c_mix", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                 ctypes.POINTER(BnFold), c_void_p, c_void_p, c_void_p, c_void_p]),
     ("ffc_noise_inject", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     ("ffc_noise_wgrad", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("ffc_quantize_u8", c_int, [c_void_p, c_void_p, c_longlong, c_void_p]),

@@ -587,7 +587,7 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, ST_SPLIT_MFMA)
+            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, ST_SPLIT_MFMA, FU2D_R2CMIX)
 
 
 def algorithmic_flops(plan) -> float:
@@ -651,6 +651,9 @@ FU_COLS = True      # staged FU: inverse column FFT fused into mix pass 1, rows-
 # staged FU, batch-statistics BN: pass 0 spills the raw Y and the whole-plane C2R applies BN + ReLU on
 # load (no second mix); FFC_FU2D_SPILL=0 keeps the two-pass mix
 FU2D_SPILL = __import__("os").environ.get("FFC_FU2D_SPILL", "1") != "0"
+# staged FU with the spill on small t planes (h in {8, 16}, C in {16, 32}): the R2C inside mix pass 0
+# (ffc_fu2d_r2c_mix: one launch instead of two); FFC_FU2D_R2CMIX=0 keeps the separate R2C
+FU2D_R2CMIX = __import__("os").environ.get("FFC_FU2D_R2CMIX", "1") != "0"
 # Run SpectralTransform's kernels on a side stream beside the local-branch GEMM of the same FFC
 # layer ("gemm-first" / "spectral-first": which is issued first).  Off by default: measured on
 # MI355X (B=256 generator) 10-18 % slower than one launch pairing the local and global GEMMs,

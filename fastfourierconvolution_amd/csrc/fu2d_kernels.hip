@@ -892,6 +892,181 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- r2c + mix pass 0 in one launch
+// Small t planes (HT = 8 or 16, the gen64 generator's ffc2 / ffc3 Fourier units at the per-rank
+// batches of strong scaling): every mix workgroup recomputes its sample's T -- bn1 (+ ReLU) of the
+// C planes, row FFTs (one row per thread), column FFTs (one column line per thread), all in LDS --
+// instead of reading it from a separate r2c launch.  The sample is 8-16 KB and its FFTs are a few
+// hundred VALU per thread, so the repeat per bin-range workgroup costs less than a kernel boundary
+// plus the r2c's own latency chain (B x C workgroups of one small plane each).  bn1 is finalized
+// here from its whole slab (ffc::bn_fold_block; workgroup 0 leads); T stays in LDS.  Then exactly
+// mix pass 0 with the spilled raw Y (the C2R applies the FU's BN on load).
+struct R2cMixArgs {
+    MixArgs m;
+    const float* t;          // (B, C, HT, HT)
+    const float* in_scale;   // bn1 affine (or has_fold)
+    const float* in_shift;
+    int in_relu, has_fold;
+    ffc_bn_fold fold;
+};
+
+template <int HT, int CC>
+struct R2cMixLds {
+    static constexpr int WPt = HT / 2 + 1, PT = HT * WPt;
+    static constexpr int MPAD = (2 * CC + 31) / 32 * 32;
+    static constexpr int WM = (2 * CC * MPAD + 255) / 256 * 256;       // mix weight (DMA groups)
+    static constexpr int SCR = (FU2_THREADS / 64) * ffc::TILE_SCRATCH;  // tile stats / merge
+    static constexpr int TL = 2 * CC * PT;                             // T (float2)
+    static constexpr int R = CC * HT * HT;                             // transformed real planes
+    static constexpr int FLOATS = WM + SCR + TL + R + 2 * CC;
+};
+
+template <int MT, int CC, int HT>
+__global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra) {
+    using LY = R2cMixLds<HT, CC>;
+    constexpr int C = CC, C2 = 2 * CC, WPt = LY::WPt, PT = LY::PT;
+    static_assert((CC & (CC - 1)) == 0 && CC <= FU2_THREADS / 4 && (C * HT * HT) % (4 * FU2_THREADS) == 0,
+                  "whole float4 rounds of the sample");
+    const MixArgs& a = ra.m;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hh = lane >> 5, col = lane & 31;
+    const int b = blockIdx.x % a.B;
+    const int split = blockIdx.x / a.B;
+    const int t_lo = (int)((long long)split * a.ntiles / a.nsplit);
+    const int t_hi = (int)((long long)(split + 1) * a.ntiles / a.nsplit);
+    float* Wm = smem;
+    float* scr = smem + LY::WM;
+    float2* Tl = reinterpret_cast<float2*>(scr + LY::SCR);
+    float* R = scr + LY::SCR + LY::TL;
+    float* fss = R + LY::R;   // bn1 scale [C] | shift [C]
+
+    // 1. the sample's t planes (registers) and the mix weight (LDS-DMA), all in flight
+    constexpr int NV = C * HT * HT / 4 / FU2_THREADS;
+    const float4* src = reinterpret_cast<const float4*>(ra.t + (size_t)b * C * HT * HT);
+    float4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = src[j * FU2_THREADS + tid];
+    ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
+    // 2. bn1 (under the loads' latency): the whole-slab fold, scratch in the (not yet used) tile-stats
+    //    area.  The per-channel fold (ffc::bn_fold_channels, as in the staged r2c) was measured
+    //    non-deterministic here -- T of two channels wrong in a few workgroups per launch (r05i,
+    //    tools/experiments/r2cmix_*.py) -- and bn_fold_block is not.
+    if (ra.has_fold) {
+        ffc::bn_fold_block<FU2_THREADS>(ra.fold, fss, fss + C, blockIdx.x == 0, reinterpret_cast<double*>(scr));
+    } else if (tid < C) {
+        fss[tid] = ra.in_scale ? ra.in_scale[tid] : 1.0f;
+        fss[C + tid] = ra.in_scale ? ra.in_shift[tid] : 0.0f;
+    }
+    __syncthreads();
+    // 3. s0 = relu(t * scale + shift) -> R
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = j * FU2_THREADS + tid;
+        const int ch = (4 * i) / (HT * HT);
+        const float sc = fss[ch], sh = fss[C + ch];
+        float4 q = v[j];
+        q.x = in_tf(q.x, sc, sh, ra.in_relu);
+        q.y = in_tf(q.y, sc, sh, ra.in_relu);
+        q.z = in_tf(q.z, sc, sh, ra.in_relu);
+        q.w = in_tf(q.w, sc, sh, ra.in_relu);
+        reinterpret_cast<float4*>(R)[i] = q;
+    }
+    __syncthreads();
+    // 4. row FFTs (row r = channel * HT + y), bins 0..HT/2 -> Tl[r * WPt + k]
+    for (int r = tid; r < C * HT; r += FU2_THREADS) {
+        float re[HT], im[HT];
+#pragma unroll
+        for (int x4 = 0; x4 < HT / 4; ++x4) {
+            const float4 q = reinterpret_cast<const float4*>(R + r * HT)[x4];
+            re[4 * x4] = q.x;
+            re[4 * x4 + 1] = q.y;
+            re[4 * x4 + 2] = q.z;
+            re[4 * x4 + 3] = q.w;
+        }
+#pragma unroll
+        for (int x = 0; x < HT; ++x) im[x] = 0.0f;
+        fft_reg<HT, false>(re, im);
+#pragma unroll
+        for (int k = 0; k < WPt; ++k) Tl[r * WPt + k] = make_float2(re[k], im[k]);
+    }
+    __syncthreads();
+    // 5. column FFTs (line l = channel * WPt + k)
+    for (int l = tid; l < C * WPt; l += FU2_THREADS) {
+        const int ch = l / WPt, k = l - ch * WPt;
+        float2* cp = Tl + ch * PT + k;
+        float re[HT], im[HT];
+#pragma unroll
+        for (int y = 0; y < HT; ++y) {
+            const float2 z = cp[y * WPt];
+            re[y] = z.x;
+            im[y] = z.y;
+        }
+        fft_reg<HT, false>(re, im);
+#pragma unroll
+        for (int y = 0; y < HT; ++y) cp[y * WPt] = make_float2(re[y], im[y]);
+    }
+    __syncthreads();
+
+    // 6. mix pass 0 on T in LDS: raw Y spill + BN partials (as fu2d_mix_kernel<MT, 0, CC>)
+    MixA<MT, CC, false> A;
+    A.load(Wm, a.wmixT, a.Mpad, C2, hh, col);
+    MixGeom g = mix_geom(a, b, C);
+    g.Tb = Tl;
+    const int NB = g.NB;
+    float st_n[MT], st_mean[MT], st_m2[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) st_n[mt] = st_mean[mt] = st_m2[mt] = 0.0f;
+    for (int tile = t_lo + wave; tile < t_hi; tile += FU2_THREADS / 64) {
+        const int n = tile * 32 + col;
+        const bool valid = n < NB;
+        floatx16 acc[MT];
+        mix_tile<MT, CC, false>(acc, g, A, n, C, hh, col);
+        float2* Yb = reinterpret_cast<float2*>(a.Y) + (size_t)b * C * NB;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+                const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // even: Re, o+1: Im
+                if (valid && o < C2) Yb[(size_t)(o >> 1) * NB + n] = make_float2(acc[mt][r], acc[mt][r + 1]);
+            }
+        const int nv = min(32, NB - tile * 32);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            float mean, m2;
+            ffc::tile_row_stats(acc[mt], nv, scr + wave * ffc::TILE_SCRATCH, mean, m2);
+            const float cn = (float)nv;
+            const float tot = st_n[mt] + cn;
+            const float delta = mean - st_mean[mt];
+            st_mean[mt] += delta * (cn / tot);
+            st_m2[mt] += m2 + delta * delta * (st_n[mt] * cn / tot);
+            st_n[mt] = tot;
+        }
+    }
+    __syncthreads();
+    float4* mg = reinterpret_cast<float4*>(scr);   // [wave][MT*32]
+    if ((lane & 1) == 0) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+            mg[wave * MT * 32 + mt * 32 + (lane >> 1)] = make_float4(st_n[mt], st_mean[mt], st_m2[mt], 0.0f);
+    }
+    __syncthreads();
+    for (int o = tid; o < C2; o += FU2_THREADS) {
+        float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+        for (int wv = 0; wv < FU2_THREADS / 64; ++wv) {
+            const float4 e = mg[wv * MT * 32 + o];
+            if (e.x > 0.0f) {
+                const float tot = nn + e.x;
+                const float delta = e.y - mean;
+                mean += delta * (e.x / tot);
+                m2 += e.z + delta * delta * (nn * e.x / tot);
+                nn = tot;
+            }
+        }
+        reinterpret_cast<float4*>(a.slab)[(size_t)blockIdx.x * C2 + o] = make_float4(nn, mean, m2, 0.0f);
+    }
+}
+
 // ---------------------------------------------------------------- pass 1 + inverse column FFT
 // Mix pass 1 for HC = H in {32, 64, 128} with the C2R's inverse column FFT fused in: a workgroup
 // owns whole spectral columns (CPW = 128 / HC columns, TPC = HC / 32 bin tiles each, one tile per
@@ -1202,9 +1377,17 @@ int raise_lds(const void* k, size_t lds, const char* what) {
 
 // workgroups per sample: ~MIX_TILES_PER_WG bin tiles each (2 per wave), but enough workgroups
 // (>= ~1024) to fill the chip when the batch is small, down to one tile per workgroup
+int mix_fill_target() {   // FFC_MIX_FILL: workgroups the split aims for at small batches (A/B)
+    static const int v = [] {
+        const char* e = std::getenv("FFC_MIX_FILL");
+        const int n = e ? std::atoi(e) : 0;
+        return n > 0 ? n : 512;
+    }();
+    return v;
+}
 int mix_nsplit(int B, int H, int W) {
     const int ntiles = (H * (W / 2 + 1) + 31) / 32;
-    const int fill = (512 + B - 1) / B;
+    const int fill = (mix_fill_target() + B - 1) / B;
     return std::max(1, std::min(ntiles, std::max(ntiles / MIX_TILES_PER_WG, fill)));
 }
 
@@ -1289,6 +1472,63 @@ extern "C" int ffc_fu2d_mix(const float* T, int B, int C, int H, int W, int up, 
     if (rc) return rc;
     hipLaunchKernelGGL(k, dim3(B * a.nsplit), dim3(FU2_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu2d_mix");
+}
+
+namespace {
+typedef void (*R2cMixKernel)(R2cMixArgs);
+R2cMixKernel pick_r2c_mix(int C, int h, size_t& lds) {
+    if (C == 16 && h == 8) return lds = 4 * R2cMixLds<8, 16>::FLOATS, fu2d_r2c_mix_kernel<1, 16, 8>;
+    if (C == 16 && h == 16) return lds = 4 * R2cMixLds<16, 16>::FLOATS, fu2d_r2c_mix_kernel<1, 16, 16>;
+    if (C == 32 && h == 8) return lds = 4 * R2cMixLds<8, 32>::FLOATS, fu2d_r2c_mix_kernel<2, 32, 8>;
+    if (C == 32 && h == 16) return lds = 4 * R2cMixLds<16, 32>::FLOATS, fu2d_r2c_mix_kernel<2, 32, 16>;
+    return nullptr;
+}
+}  // namespace
+
+extern "C" int ffc_fu2d_r2c_mix_supported(int C, int H, int W, int up) {
+    size_t lds = 0;
+    return ffc_fu2d_supported(C, H, W, up) && pick_r2c_mix(C, H / up, lds) != nullptr && lds <= 160 * 1024;
+}
+
+extern "C" int ffc_fu2d_r2c_mix(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                                const float* in_shift, int in_relu, const ffc_bn_fold* in_fold, const float* wmixT,
+                                float* stats_slab, float* Y, void* stream) {
+    FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu2d_r2c_mix: B and C must be positive");
+    FFC_CHECK_ARG(ffc_fu2d_r2c_mix_supported(C, H, W, up), "ffc_fu2d_r2c_mix: unsupported (C, H, W, up)");
+    FFC_CHECK_ARG(t && wmixT && stats_slab && Y, "ffc_fu2d_r2c_mix: null pointer");
+    FFC_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "ffc_fu2d_r2c_mix: in_scale/in_shift pairing");
+    FFC_CHECK_ARG(!in_fold || (!in_scale && channel_fold_ok(in_fold, C) && in_fold->scale_out && in_fold->shift_out),
+                  "ffc_fu2d_r2c_mix: in_fold replaces in_scale / in_shift, needs C channels, momentum >= 0 and "
+                  "scale_out / shift_out");
+    size_t lds = 0;
+    R2cMixKernel k = pick_r2c_mix(C, H / up, lds);
+    int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c_mix");
+    if (rc) return rc;
+    R2cMixArgs ra;
+    MixArgs& a = ra.m;
+    a.T = nullptr;
+    a.wmixT = wmixT;
+    a.slab = stats_slab;
+    a.bn_scale = nullptr;
+    a.bn_shift = nullptr;
+    a.Y = Y;
+    a.B = B;
+    a.C = C;
+    a.H = H;
+    a.W = W;
+    a.up = up;
+    a.ntiles = (H * (W / 2 + 1) + 31) / 32;
+    a.nsplit = mix_nsplit(B, H, W);   // the slab rows of ffc_fu2d_slab_rows
+    a.Mpad = (2 * C + 31) / 32 * 32;
+    a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
+    ra.t = t;
+    ra.in_scale = in_scale;
+    ra.in_shift = in_shift;
+    ra.in_relu = in_relu;
+    ra.has_fold = in_fold != nullptr;
+    if (in_fold) ra.fold = *in_fold;
+    hipLaunchKernelGGL(k, dim3(B * a.nsplit), dim3(FU2_THREADS), lds, (hipStream_t)stream, ra);
+    return ffc::launch_status("ffc_fu2d_r2c_mix");
 }
 
 extern "C" int ffc_fu_pack_mix_f16(const float* w, int C2, void* w16, void* stream) {

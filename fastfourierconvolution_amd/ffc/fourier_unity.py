@@ -154,30 +154,43 @@ class FourierUnitSN(nn.Module):
         nT = B * C * h * (w // 2 + 1)           # complex bins of T
         nY = B * C * H * (W // 2 + 1)           # complex bins of Y
         mix_flops = 2.0 * (2 * C) ** 2 * (B * H * (W // 2 + 1))   # (2C x 2C) GEMM over every bin
-        T = torch.empty((B, C, h, w // 2 + 1, 2), device=dev, dtype=torch.float32)
         n_r, n_c = float(B * C * H * W), float(B * C * H * (W // 2 + 1))   # SURVEY.md §8d, full resolution
         # SURVEY.md §8d's R2C bytes, capped at what the kernel moves: with the upsample folded in it
         # reads t (N_r / 4) and writes T (N_c / 4), and counting the full-resolution bytes would credit
         # bytes never transferred
         mvr = 4.0 * t.numel() + 8.0 * nT
-        with rt.observe("fu2d_r2c", bytes=min(4.0 * n_r + 8.0 * n_c, mvr), moved=mvr):
-            check(L.ffc_fu2d_r2c_ex(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu),
-                                    ctypes.byref(in_fold.struct) if in_fold else None, ptr(T), stream),
-                  "ffc_fu2d_r2c")
-        if in_fold is not None:   # the r2c's sample-0 workgroups wrote the folded bn1 affine
-            in_scale, in_shift = in_fold.scale, in_fold.shift
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         c2r_moved = 8.0 * nY + 4.0 * out.numel() + (4.0 * t.numel() if residual else 0.0)
         c2r_bytes = min(8.0 * n_c + 4.0 * n_r, c2r_moved)                   # SURVEY.md §8d C2R pass
+        fused_r2c = (use_batch and rt.FU2D_SPILL and rt.FU2D_R2CMIX and not f16 and
+                     L.ffc_fu2d_r2c_mix_supported(C, H, W, up))
+        T = None
+        if not fused_r2c:
+            T = torch.empty((B, C, h, w // 2 + 1, 2), device=dev, dtype=torch.float32)
+            with rt.observe("fu2d_r2c", bytes=min(4.0 * n_r + 8.0 * n_c, mvr), moved=mvr):
+                check(L.ffc_fu2d_r2c_ex(ptr(t), B, C, h, w, ptr(in_scale), ptr(in_shift), int(in_relu),
+                                        ctypes.byref(in_fold.struct) if in_fold else None, ptr(T), stream),
+                      "ffc_fu2d_r2c")
         if use_batch:
             rows = L.ffc_fu2d_slab_rows(B, C, H, W)
             slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
             # spill: pass 0 stores the raw Y and the C2R applies BN + ReLU on load (one mix instead of
             # two, and the statistics are taken from exactly the values they normalise)
             Y = torch.empty((B, C, H, W // 2 + 1, 2), device=dev, dtype=torch.float32) if rt.FU2D_SPILL else None
-            with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT + (8.0 * nY if Y is not None else 0.0)):
-                check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, ptr(Y), stream),
-                      "ffc_fu2d_mix(pass 0)")
+            if fused_r2c:
+                # the R2C inside mix pass 0 (small t planes: every bin-range workgroup recomputes its
+                # sample's T in LDS); labelled as the R2C stage, bytes = t in + the spilled Y out
+                mv = 4.0 * t.numel() + 8.0 * nY
+                with rt.observe("fu2d_r2c", flops=mix_flops, bytes=min(4.0 * n_r + 8.0 * n_c, mv), moved=mv):
+                    check(L.ffc_fu2d_r2c_mix(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu),
+                                             ctypes.byref(in_fold.struct) if in_fold else None, ptr(mixT),
+                                             ptr(slab), ptr(Y), stream), "ffc_fu2d_r2c_mix")
+            else:
+                with rt.observe("fu2d_mix0", flops=mix_flops, bytes=8.0 * nT + (8.0 * nY if Y is not None else 0.0)):
+                    check(mixfn(ptr(T), B, C, H, W, up, ptr(mixT), 0, ptr(slab), None, None, ptr(Y), stream),
+                          "ffc_fu2d_mix(pass 0)")
+            if in_fold is not None:   # the r2c's (or r2c_mix's) leader workgroups wrote the folded bn1 affine
+                in_scale, in_shift = in_fold.scale, in_fold.shift
             cfold = rt.bn_fold_channels(self.bn, 2 * C, slab, rows, 1.0, dev) if Y is not None else None
             if cfold is not None:   # the FU's BN finalized inside the C2R (two channels per plane)
                 with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):
@@ -194,6 +207,8 @@ class FourierUnitSN(nn.Module):
                 return out
         else:
             sc, sh = rt.bn_scale_shift(self.bn, 2 * C, None, 0, 1.0, dev, stream)
+        if in_fold is not None and not use_batch:
+            in_scale, in_shift = in_fold.scale, in_fold.shift
         if rt.FU_COLS and L.ffc_fu2d_cols_supported(C, H, W, up, int(f16)):
             # pass 1 with the inverse column FFT fused in (column-major Yc), then rows-only C2R
             Yc = torch.empty((B, C, W // 2 + 1, H, 2), device=dev, dtype=torch.float32)

@@ -488,6 +488,16 @@ int ffc_fu2d_r2c_ex(const float* t, int B, int C, int h, int w, const float* in_
 int ffc_fu2d_c2r_fold(const float* Y, int B, int C, int H, int W, const float* t, int up,
                       const float* in_scale, const float* in_shift, int in_relu, int residual,
                       const ffc_bn_fold* bn_fold, float* out, void* stream);
+/* ffc_fu2d_r2c_ex + ffc_fu2d_mix pass 0 with the raw-Y spill, in one launch, for small t planes
+ * (h = H/up in {8, 16}, C in {16, 32}; ffc_fu2d_r2c_mix_supported): every mix workgroup recomputes
+ * its sample's T in LDS (bn1 + ReLU, row and column FFTs) instead of reading it from the R2C's
+ * output; bn1 folded from its whole slab when in_fold is given (workgroup 0 leads: running statistics,
+ * scale_out / shift_out).  stats_slab has ffc_fu2d_slab_rows() rows, as for ffc_fu2d_mix; T is not
+ * materialized.  Same results as the two launches up to fp32 rounding of the FFT order. */
+int ffc_fu2d_r2c_mix_supported(int C, int H, int W, int up);
+int ffc_fu2d_r2c_mix(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                     const float* in_shift, int in_relu, const ffc_bn_fold* in_fold, const float* wmixT,
+                     float* stats_slab, float* Y, void* stream);
 
 /* ------------------------------------------------------------------ fgan128 caller ops
  * NoiseInjection.forward(x, noise) (layers/noise_injection.py:25-32): out = x + weight[c]*noise[b]

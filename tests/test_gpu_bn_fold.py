@@ -140,20 +140,24 @@ def test_channel_folds_match_separate_launches(momentum, path, cin, cout, hw, B)
     ref_out, ref_sd = _run_chfold(copy.deepcopy(base), xs, False, path)
     L = rt.lib()
     calls = {"r2c": 0, "c2r": 0}
-    o_r2c, o_c2r = L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold
+    o_r2c, o_c2r, o_r2cm = L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold, L.ffc_fu2d_r2c_mix
 
     def r2c(*a):
         calls["r2c"] += a[8] is not None
         return o_r2c(*a)
 
+    def r2cm(*a):   # the R2C inside mix pass 0 (small t planes), fold argument 9
+        calls["r2c"] += a[9] is not None
+        return o_r2cm(*a)
+
     def c2r(*a):
         calls["c2r"] += 1
         return o_c2r(*a)
-    L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold = r2c, c2r
+    L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold, L.ffc_fu2d_r2c_mix = r2c, c2r, r2cm
     try:
         out, sd = _run_chfold(copy.deepcopy(base), xs, True, path)
     finally:
-        L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold = o_r2c, o_c2r
+        L.ffc_fu2d_r2c_ex, L.ffc_fu2d_c2r_fold, L.ffc_fu2d_r2c_mix = o_r2c, o_c2r, o_r2cm
     if path == "staged" and momentum is not None:
         assert calls["r2c"] == 3 and calls["c2r"] == 3, calls
     for a, b in zip(out, ref_out):
@@ -165,3 +169,62 @@ def test_channel_folds_match_separate_launches(momentum, path, cin, cout, hw, B)
             torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=k)
     again, _ = _run_chfold(copy.deepcopy(base), xs, True, path)
     assert all(torch.equal(a, b) for a, b in zip(out, again))   # deterministic
+
+
+# --------------------------------------------------------------------------- round 5: R2C inside mix pass 0
+@pytest.mark.parametrize("chfold", [True, False])
+@pytest.mark.parametrize("cin,cout,hw,B", [(32, 64, 8, 6), (64, 64, 16, 3), (32, 32, 8, 5), (16, 32, 16, 4)])
+def test_r2c_mix_matches_separate_launches(chfold, cin, cout, hw, B):
+    """ffc_fu2d_r2c_mix (bn1 + ReLU + R2C of the sample recomputed in every mix pass-0 workgroup, T
+    in LDS) against the separate r2c + mix launches (FFC_FU2D_R2CMIX=0), staged FU, train-mode BN,
+    bn1 folded per channel (chfold) or finalized by its own launch: outputs within 1e-6 normwise
+    (the FFT order differs), running statistics within 1e-6, num_batches_tracked exact, three steps"""
+    from fastfourierconvolution_amd import _runtime as rt
+    L = rt.lib()
+    C, up = cout // 2, 2
+    assert L.ffc_fu2d_r2c_mix_supported(C, hw * up, hw * up, up)
+    base = _st(cin, cout, 0.1, seed=cin + hw + B + 7)
+    g = torch.Generator().manual_seed(hw + B)
+    xs = [torch.randn((B, cin, hw, hw), generator=g).cuda() for _ in range(3)]
+    old = rt.FU2D_R2CMIX, rt.BN_CHFOLD
+    n = {"fused": 0}
+    o = L.ffc_fu2d_r2c_mix
+
+    def spy(*a):
+        n["fused"] += 1
+        return o(*a)
+    try:
+        rt.BN_CHFOLD = chfold
+        rt.FU2D_R2CMIX = False
+        ref_out, ref_sd = _run_chfold(copy.deepcopy(base), xs, chfold, "staged")
+        rt.FU2D_R2CMIX = True
+        L.ffc_fu2d_r2c_mix = spy
+        out, sd = _run_chfold(copy.deepcopy(base), xs, chfold, "staged")
+    finally:
+        rt.FU2D_R2CMIX, rt.BN_CHFOLD = old
+        L.ffc_fu2d_r2c_mix = o
+    assert n["fused"] == 3
+    for a, b in zip(out, ref_out):
+        assert normwise_err(a.double().cpu(), b.double().cpu()) <= 1e-6
+    for k, v in ref_sd.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(v) == 3, k
+        elif k.endswith("running_mean") or k.endswith("running_var"):
+            torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=k)
+
+
+@pytest.mark.parametrize("cin,cout,hw,B", [(64, 32, 16, 64), (64, 32, 16, 86), (128, 64, 8, 86)])
+def test_staged_fu_repeat_bitwise(cin, cout, hw, B):
+    """the staged Fourier unit at the strong-scaling shard sizes, twelve fresh train forwards of one
+    SpectralTransform on one input: bitwise equal outputs (r05i: a per-channel bn1 fold inside
+    ffc_fu2d_r2c_mix corrupted T of two channels in a few workgroups of some launches; one-run parity
+    checks passed it)"""
+    torch.manual_seed(cin + hw + B)
+    base = _st(cin, cout, 0.1, seed=cin + B)
+    x = torch.randn((B, cin, hw, hw), generator=torch.Generator().manual_seed(B)).cuda()
+    outs = []
+    for _ in range(12):
+        out, _sd = _run_chfold(copy.deepcopy(base), [x], True, "staged")
+        outs.append(out[0])
+    bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
+    assert not bad, f"runs {bad} differ from run 0"
