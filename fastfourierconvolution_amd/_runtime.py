@@ -333,16 +333,20 @@ def bn_fold(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, dev
 # per lane.
 BN_CHFOLD = __import__("os").environ.get("FFC_BN_CHFOLD", "1") != "0"
 BN_CHFOLD_LOADS = int(__import__("os").environ.get("FFC_BN_CHFOLD_LOADS", "16"))
+BN_CHFOLD_READS = int(__import__("os").environ.get("FFC_BN_CHFOLD_READS", "16384"))
 
 
-def bn_fold_channels(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, lanes: int = 64):
+def bn_fold_channels(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, lanes: int = 64,
+                     consumers: int = 1):
     """a BnFoldDesc for a per-channel in-kernel fold (``lanes`` lanes merge one channel's rows), or
     None: batch statistics on one rank only, momentum not None (the per-channel leaders cannot read
-    num_batches_tracked while another bumps it), at most BN_CHFOLD_LOADS rows per lane"""
+    num_batches_tracked while another bumps it), at most BN_CHFOLD_LOADS rows per lane, and at most
+    BN_CHFOLD_READS slab rows read per channel over its ``consumers`` workgroups (at fgan128's
+    B = 512 every 64^2 C2R plane workgroup re-read 1024 rows: C2R 798 -> 1046 us per step, r05l)"""
     use_batch, _ = bn_mode(bn)
     if not (BN_FOLD and BN_CHFOLD and use_batch and slab is not None and _sync_group() is None):
         return None
-    if bn.momentum is None or -(-nrows // lanes) > BN_CHFOLD_LOADS:
+    if bn.momentum is None or -(-nrows // lanes) > BN_CHFOLD_LOADS or nrows * max(1, consumers) > BN_CHFOLD_READS:
         return None
     if bn.num_features != C:
         raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
@@ -587,7 +591,7 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, ST_SPLIT_MFMA, FU2D_R2CMIX)
+            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, BN_CHFOLD_READS, ST_SPLIT_MFMA, FU2D_R2CMIX)
 
 
 def algorithmic_flops(plan) -> float:

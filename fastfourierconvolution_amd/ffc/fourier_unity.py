@@ -137,7 +137,7 @@ class FourierUnitSN(nn.Module):
         B, C, h, w = t.shape
         if in_fold is not None:
             chf = rt.bn_fold_channels(in_fold.bn, C, in_fold.slab, in_fold.struct.nrows, in_fold.struct.count_mult,
-                                      t.device)
+                                      t.device, consumers=B)
             if chf is None:
                 in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
                 in_fold = None
@@ -191,7 +191,7 @@ class FourierUnitSN(nn.Module):
                           "ffc_fu2d_mix(pass 0)")
             if in_fold is not None:   # the r2c's (or r2c_mix's) leader workgroups wrote the folded bn1 affine
                 in_scale, in_shift = in_fold.scale, in_fold.shift
-            cfold = rt.bn_fold_channels(self.bn, 2 * C, slab, rows, 1.0, dev) if Y is not None else None
+            cfold = rt.bn_fold_channels(self.bn, 2 * C, slab, rows, 1.0, dev, consumers=B) if Y is not None else None
             if cfold is not None:   # the FU's BN finalized inside the C2R (two channels per plane)
                 with rt.observe("fu2d_c2r", bytes=c2r_bytes, moved=c2r_moved):
                     check(L.ffc_fu2d_c2r_fold(ptr(Y), B, C, H, W, ptr(t), up, ptr(in_scale), ptr(in_shift),
