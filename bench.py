@@ -154,6 +154,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", type=int, default=3)
+    p.add_argument("--syncbn-rehearsal", action="store_true",
+                   help="N = 1 only: run the SyncBN path of N > 1 (moments reduce -> all_reduce over a one-rank "
+                        "RCCL group -> finalize, no in-kernel BN folds) to time a rank's kernels as they run at "
+                        "N > 1, without the xGMI latency (DESIGN.md section 5)")
     return p.parse_args()
 
 
@@ -730,6 +734,14 @@ def main():
         D.broadcast_module(G)           # weights + BN buffers from rank 0, once
         if args.bn_mode == "train":
             D.enable_sync_bn()          # the only data-path exchange: BN moments all-reduce
+    elif args.syncbn_rehearsal and args.bn_mode == "train":
+        import datetime
+        from fastfourierconvolution_amd import distributed as D
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{29500 + os.getpid() % 2000}", rank=0,
+                                world_size=1, device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=300))
+        D.enable_sync_bn(even_world1=True)
     # one global z from one seed (weak or strong), this rank's slice: at N = 1 both modes time the
     # same batch, and at N > 1 the gathered output can be checked against the global-batch forward
     gen = torch.Generator(device="cpu").manual_seed(100)
@@ -877,14 +889,15 @@ def main():
                        "global_batch": global_batch, "per_gpu_batch": args.batch, "bn_mode": args.bn_mode,
                        "spectral_mix": args.mix,
                        "hipgraph": use_graph, "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and
-                                                                          args.bn_mode == "train" else "")},
+                                                                          args.bn_mode == "train" else "")
+                       + ("+syncbn-rehearsal(1-rank RCCL group)" if world == 1 and args.syncbn_rehearsal else "")},
             "roofline": roof, "fft_roofline": fft_roof, "cpu_baseline": cpu, "parity": parity,
             "kernels": kernels,
         }
         if weak is not None:
             line["weak_scaling"] = weak
         print(json.dumps(line))
-    if world > 1:
+    if world > 1 or (args.syncbn_rehearsal and dist.is_initialized()):
         dist.destroy_process_group()
 
 
