@@ -106,21 +106,40 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
     // means over 16x16 planes: 16), ~5 us of the ST prologue at every batch size (r04 probe:
     // st_prologue with the SE gate skipped, profiles/r04/w)
     const int row = tid >> 4, rl = tid & 15;
-#pragma unroll 4
-    for (int ch = row; ch < Cin; ch += ST_THREADS / 16) {
-        const float* xc = xs + ch * hw;
-        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-        int i = rl;
-        for (; i + 48 < hw; i += 64) {
-            s0 += xc[i];
-            s1 += xc[i + 16];
-            s2 += xc[i + 32];
-            s3 += xc[i + 48];
+    const int n4 = hw >> 2;
+    if ((hw & 3) == 0 && n4 <= 16 && (n4 & (n4 - 1)) == 0) {
+        // small planes (gen64's 4x4 and 8x8): one thread per channel, the plane as float4 LDS reads
+        // in a per-thread rotated order (threads hw floats apart would otherwise share one bank
+        // group) -- no DPP reduction chain, one round for Cin <= 512
+        for (int ch = tid; ch < Cin; ch += ST_THREADS) {
+            const float4* xc = reinterpret_cast<const float4*>(xs + ch * hw);
+            float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            for (int i = 0; i < n4; ++i) {
+                const float4 v = xc[(i + ch) & (n4 - 1)];
+                acc.x += v.x;
+                acc.y += v.y;
+                acc.z += v.z;
+                acc.w += v.w;
+            }
+            gate[ch] = ((acc.x + acc.y) + (acc.z + acc.w)) / (float)hw;   // channel mean (gate below)
         }
-        for (; i < hw; i += 16) s0 += xc[i];
-        float s = (s0 + s1) + (s2 + s3);
-        s = ffc::row16_sum(s);
-        if (rl == 15) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
+    } else {
+#pragma unroll 4
+        for (int ch = row; ch < Cin; ch += ST_THREADS / 16) {
+            const float* xc = xs + ch * hw;
+            float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+            int i = rl;
+            for (; i + 48 < hw; i += 64) {
+                s0 += xc[i];
+                s1 += xc[i + 16];
+                s2 += xc[i + 32];
+                s3 += xc[i + 48];
+            }
+            for (; i < hw; i += 16) s0 += xc[i];
+            float s = (s0 + s1) + (s2 + s3);
+            s = ffc::row16_sum(s);
+            if (rl == 15) gate[ch] = s / (float)hw;  // channel mean (overwritten by the gate below)
+        }
     }
     __syncthreads();
     // fc1: one wave per hidden unit (64 lanes over the inputs)
@@ -142,21 +161,44 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
         if (lane == 0) hv[j] = fmaxf(s, 0.0f);
     }
     __syncthreads();
-    // fc2 + sigmoid: one 16-lane row per input channel k (lanes over the hidden units)
-#pragma unroll 4
-    for (int k = row; k < Cin; k += ST_THREADS / 16) {
-        float s = 0.0f;
-        if (a.w2_off >= 0) {
-            const float* w2 = sm + a.w2_off + k * hid;
-            for (int j = rl; j < hid; j += 16) s = fmaf(w2[j], hv[j], s);
-        } else {
-            for (int j = rl; j < hid; j += 16) s = fmaf(a.w2[(size_t)k * hid + j], hv[j], s);
-        }
-        s = ffc::row16_sum(s);
-        if (rl == 15) {
-            const float gk = 1.0f / (1.0f + expf(-s));   // hidden = 0: sigmoid(0) = 0.5
+    // fc2 + sigmoid
+    const int h4 = hid >> 2;
+    if (a.w2_off >= 0 && hid > 0 && (hid & 3) == 0 && h4 <= 16 && (h4 & (h4 - 1)) == 0) {
+        // few hidden units (gen64: Cin / 16 = 4 .. 16): one thread per input channel k, its w2 row as
+        // float4 LDS reads in a rotated order (rows hid floats apart), hv broadcast
+        const float4* hv4 = reinterpret_cast<const float4*>(hv);
+        for (int k = tid; k < Cin; k += ST_THREADS) {
+            const float4* w2 = reinterpret_cast<const float4*>(sm + a.w2_off + k * hid);
+            float s = 0.0f;
+            for (int i = 0; i < h4; ++i) {
+                const int q = (i + k) & (h4 - 1);
+                const float4 w = w2[q], hh = hv4[q];
+                s = fmaf(w.x, hh.x, s);
+                s = fmaf(w.y, hh.y, s);
+                s = fmaf(w.z, hh.z, s);
+                s = fmaf(w.w, hh.w, s);
+            }
+            const float gk = 1.0f / (1.0f + expf(-s));
             gate[k] = gk;
             if (a.gate_out && sp == 0) a.gate_out[(size_t)b * Cin + k] = gk;
+        }
+    } else {
+        // one 16-lane row per input channel k (lanes over the hidden units)
+#pragma unroll 4
+        for (int k = row; k < Cin; k += ST_THREADS / 16) {
+            float s = 0.0f;
+            if (a.w2_off >= 0) {
+                const float* w2 = sm + a.w2_off + k * hid;
+                for (int j = rl; j < hid; j += 16) s = fmaf(w2[j], hv[j], s);
+            } else {
+                for (int j = rl; j < hid; j += 16) s = fmaf(a.w2[(size_t)k * hid + j], hv[j], s);
+            }
+            s = ffc::row16_sum(s);
+            if (rl == 15) {
+                const float gk = 1.0f / (1.0f + expf(-s));   // hidden = 0: sigmoid(0) = 0.5
+                gate[k] = gk;
+                if (a.gate_out && sp == 0) a.gate_out[(size_t)b * Cin + k] = gk;
+            }
         }
     }
     __syncthreads();
