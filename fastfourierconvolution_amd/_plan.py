@@ -444,6 +444,9 @@ def plan_convq_job(B: int, M: int, segs, cfg: int):
     PHm = max(ph.PH for ph in base.phases)
     PWm = max(ph.PW for ph in base.phases)
     TC = min(PWm, npix)
+    tc_max = int(os.environ.get("FFC_CONVQ_TCMAX", "0"))   # A/B: squarer pixel blocks (less halo)
+    if tc_max >= 4 and TC > tc_max:
+        TC = tc_max
     TR = min(PHm, max(1, npix // TC))
     NS = max(1, min(B, npix // (TR * TC)))
     nrb, ncb = -(-PHm // TR), -(-PWm // TC)

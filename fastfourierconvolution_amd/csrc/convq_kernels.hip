@@ -1079,16 +1079,23 @@ extern "C" int ffc_convq_forward_split(const ffc_convp_job* jobs, int njobs, con
         }
     }
     // pixels per staging unit: the smallest of 1, 2, 4 whose units fit the 256 staging threads
-    // (FFC_CONVQ_PX = 4 keeps the 4-pixel units everywhere: A/B)
+    // (FFC_CONVQ_PX = 4 keeps the 4-pixel units everywhere: A/B; the (1, 4) and (2, 2) tiles with
+    // 2-pixel units measured neutral on gen64 and 0.3-1 % faster on fgan128's conv, r05y / r05aa)
     const int px = stage_px(units4);
     int rc = FFC_E_INVALID;
     switch (cfg) {
-        case 0: rc = launch_q<1, 4>(a, ntiles, lds, s, sl, nslots); break;
+        case 0:
+            if (px <= 2) rc = launch_q<1, 4, QSLOTS, 2>(a, ntiles, lds, s, sl, nslots);
+            else rc = launch_q<1, 4>(a, ntiles, lds, s, sl, nslots);
+            break;
         case 1:
             if (px <= 2) rc = launch_q<1, 2, QSLOTS, 2>(a, ntiles, lds, s, sl, nslots);
             else rc = launch_q<1, 2>(a, ntiles, lds, s, sl, nslots);
             break;
-        case 2: rc = launch_q<2, 2>(a, ntiles, lds, s, sl, nslots); break;
+        case 2:
+            if (px <= 2) rc = launch_q<2, 2, QSLOTS, 2>(a, ntiles, lds, s, sl, nslots);
+            else rc = launch_q<2, 2>(a, ntiles, lds, s, sl, nslots);
+            break;
         case 3:
             // the (1, 1) tile: pixels per staging unit by the patch size (stage_px); FFC_CONVQ_SLOTS11 = 3 | 4
             // keeps more chunks' loads in flight (measured slower: it halves the workgroups per CU, r05a)
