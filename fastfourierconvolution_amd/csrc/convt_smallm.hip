@@ -23,6 +23,7 @@
 // FMAs, written to the other LDS buffer after them).
 #include "ffc_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -75,6 +76,7 @@ struct SmallMArgs {
     float* out;
     int B, IH, IW, M;
     int nty, ntx;
+    int comb;            // convt_smallm_kernel quarter combine: 0 serial, 1 all quarters at once (8 x 1 wave), 2 one barrier into quarter 0
     int act;
     float act_param;
     ffc_in_tf tf[2];     // conv3x3_smallm_kernel<MM, true>: deferred BN + act (+ noise) of segment s
@@ -87,6 +89,9 @@ constexpr int CT_TT = 32;                    // input tile columns; a thread own
 #endif
 #ifndef FFC_CT_CPQ
 #define FFC_CT_CPQ 2
+#endif
+#ifndef FFC_CT_ONECOMB
+#define FFC_CT_ONECOMB 1   // 0: the serial quarter combine everywhere (A/B)
 #endif
 constexpr int CT_TR = FFC_CT_TR;             // input tile rows
 constexpr int CT_QT = (CT_TT / 2) * (CT_TR / 2);   // threads per channel quarter
@@ -255,30 +260,99 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
         if (more) put(buf(k + 1), r);
         __syncthreads();
     }
-    // fixed-order combine of the quarters' partial sums: ((q0 + q1) + q2) + q3
-    float* part = lds;   // QT threads x 16 MM floats
-    for (int rq = 1; rq < CT_NQ; ++rq) {
-        if (q == rq) {
-#pragma unroll
-            for (int o = 0; o < 16; ++o)
-#pragma unroll
-                for (int m = 0; m < MM; ++m) part[(o * MM + m) * CT_QT + tid] = get(o, m);
-        }
-        __syncthreads();
-        if (q == 0) {
-#pragma unroll
-            for (int o = 0; o < 16; ++o)
-#pragma unroll
-                for (int m = 0; m < MM; ++m) add(o, m, part[(o * MM + m) * CT_QT + tid]);
-        }
-        __syncthreads();
-    }
-    if (q != 0) return;
     const int OH = 2 * a.IH, OW = 2 * a.IW;
     const int oy0 = 2 * (y0 + qy), ox0 = 2 * (x0 + qx);
     const bool xin = x0 + qx + 1 < a.IW;   // both input columns in range
     // argument fields read before the stores (after a store the compiler reloads them: ISA r04)
     float* const out = a.out;
+    const float ap = a.act_param;
+    // the activation as a template argument of the store loops (one switch outside them)
+    auto with_act = [&](auto&& body) {
+        switch (a.act) {
+            case FFC_ACT_RELU: body([](float v) { return fmaxf(v, 0.0f); }); break;
+            case FFC_ACT_LEAKY_RELU: body([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
+            case FFC_ACT_TANH: body([](float v) { return tanhf(v); }); break;
+            case FFC_ACT_SIGMOID: body([](float v) { return 1.0f / (1.0f + expf(-v)); }); break;
+            case FFC_ACT_GELU: body([](float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }); break;
+            default: body([](float v) { return v; }); break;
+        }
+    };
+    if (FFC_CT_ONECOMB && MM <= 3 && CT_NQ == 8 && CT_QT == 64 && a.comb == 1) {
+        // 8 quarters of one wave each (the small-batch tiles): every quarter stores its partial sums
+        // at once (the patch buffers are free after the last barrier), then wave w adds the output
+        // rows (m, i) = w, w + 8, ... over the quarters in the serial combine's order
+        // (((q0 + q1) + q2) + ...: the same rounding) and stores them -- one barrier instead of 14
+        float* part = lds;   // [q][o * MM + m][QT]   (host: the dynamic LDS covers 8 * 16 * MM * 64 floats)
+#pragma unroll
+        for (int o = 0; o < 16; ++o)
+#pragma unroll
+            for (int m = 0; m < MM; ++m) part[((q * 16 + o) * MM + m) * CT_QT + tid] = get(o, m);
+        __syncthreads();
+        with_act([&](auto actf) {
+            for (int u = q; u < 4 * MM; u += CT_NQ) {
+                const int m = u >> 2, i = u & 3;
+                const int oy = oy0 + i;
+                const float bv = a.bias ? a.bias[m] : 0.0f;
+                float v4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int o = i * 4 + j;
+                    float sacc = part[(o * MM + m) * CT_QT + tid];
+#pragma unroll
+                    for (int rq = 1; rq < CT_NQ; ++rq) sacc += part[((rq * 16 + o) * MM + m) * CT_QT + tid];
+                    v4[j] = actf(sacc + bv);
+                }
+                if (oy >= OH) continue;
+                float* row = out + (((size_t)b * M + m) * OH + oy) * OW + ox0;
+                if (xin) {
+                    *reinterpret_cast<float4*>(row) = make_float4(v4[0], v4[1], v4[2], v4[3]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (ox0 + j < OW) row[j] = v4[j];
+                }
+            }
+        });
+        return;
+    }
+    float* part = lds;
+    if (FFC_CT_ONECOMB && MM <= 3 && CT_NQ != 8 && a.comb == 2) {
+        // quarters 1 .. NQ-1 store their partial sums at once, quarter 0 adds them in quarter order
+        // (the serial combine's rounding) after one barrier (host: LDS for (NQ - 1) * 16 * MM * QT floats)
+        if (q != 0) {
+#pragma unroll
+            for (int o = 0; o < 16; ++o)
+#pragma unroll
+                for (int m = 0; m < MM; ++m) part[(((q - 1) * 16 + o) * MM + m) * CT_QT + tid] = get(o, m);
+        }
+        __syncthreads();
+        if (q != 0) return;
+        for (int rq = 1; rq < CT_NQ; ++rq) {
+#pragma unroll
+            for (int o = 0; o < 16; ++o)
+#pragma unroll
+                for (int m = 0; m < MM; ++m) add(o, m, part[(((rq - 1) * 16 + o) * MM + m) * CT_QT + tid]);
+        }
+    } else {
+        // fixed-order combine of the quarters' partial sums: ((q0 + q1) + q2) + q3
+        for (int rq = 1; rq < CT_NQ; ++rq) {
+            if (q == rq) {
+#pragma unroll
+                for (int o = 0; o < 16; ++o)
+#pragma unroll
+                    for (int m = 0; m < MM; ++m) part[(o * MM + m) * CT_QT + tid] = get(o, m);
+            }
+            __syncthreads();
+            if (q == 0) {
+#pragma unroll
+                for (int o = 0; o < 16; ++o)
+#pragma unroll
+                    for (int m = 0; m < MM; ++m) add(o, m, part[(o * MM + m) * CT_QT + tid]);
+            }
+            __syncthreads();
+        }
+        if (q != 0) return;
+    }
     float bvs[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) bvs[m] = a.bias ? a.bias[m] : 0.0f;
@@ -302,7 +376,6 @@ __global__ __launch_bounds__((CT_TT / 2) * (TR_ / 2) * NQ_) __attribute__((amdgp
             }
         }
     };
-    const float ap = a.act_param;
     switch (a.act) {
         case FFC_ACT_RELU: store([](float v) { return fmaxf(v, 0.0f); }); break;
         case FFC_ACT_LEAKY_RELU: store([ap](float v) { return v > 0.0f ? v : v * ap; }); break;
@@ -647,7 +720,22 @@ extern "C" int ffc_convt_k4s2_smallm(const float* x0, int C0, const float* x1, i
     a.act = act;
     a.act_param = act_param;
 
-    const size_t lds = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PS * sizeof(float);   // patch double buffer
+    size_t lds = (size_t)2 * nq * CT_CPQ * (tr + 2) * CT_PS * sizeof(float);   // patch double buffer
+    // quarter combine (convt_smallm_kernel): all 8 one-wave quarters at once when the grid is one
+    // workgroup per CU or less (its LDS allows one per CU); else one barrier into quarter 0 while that
+    // keeps two workgroups per CU (<= 80 KB); else the serial combine
+    const size_t qt = (size_t)(CT_TT / 2) * (tr / 2);
+    const size_t comb_all = (size_t)nq * 16 * M * qt * sizeof(float);
+    const size_t comb_q0 = (size_t)(nq - 1) * 16 * M * qt * sizeof(float);
+    a.comb = 0;   // M = 4: the serial combine (the one-barrier forms spill registers there)
+    if (M > 3) {
+    } else if (nq == 8 && qt == 64 && (long long)B * a.nty * a.ntx <= 256 && comb_all <= 160 * 1024) {
+        a.comb = 1;
+        lds = std::max(lds, comb_all);
+    } else if (nq != 8 && comb_q0 <= 80 * 1024) {
+        a.comb = 2;
+        lds = std::max(lds, comb_q0);
+    }
     const unsigned grid = (unsigned)B * a.nty * a.ntx;
     // M is a template parameter: no runtime m < M branches in the FMA body
     typedef void (*CtKernel)(SmallMArgs);

@@ -220,7 +220,7 @@ def test_golden_generic_conv_kernel(case):
 
 
 @pytest.mark.parametrize("M,H,W,bias", [(1, 5, 7, True), (2, 32, 32, False), (4, 3, 40, True), (3, 64, 16, False)])
-def test_smallm_convt_vs_oracle(M, H, W, bias):
+def test_smallm_convt_odd_sizes_vs_oracle(M, H, W, bias):
     """direct VALU ConvT k4 s2 p1 path (M <= 4): odd sizes, tiles wider than 32, bias"""
     import fastfourierconvolution_amd as F
     from oracle.ffc_oracle import ffc_bn_act
