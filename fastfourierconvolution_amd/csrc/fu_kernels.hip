@@ -72,6 +72,8 @@ struct FuArgs {
     int has_in_fold, has_mix_fold;
     float* yspill;                   // (B, 2C, NB) mix output: written by pass 0, read by pass 1
     int mix3;                        // mix on split-bf16 MFMA products (C % 8 == 0), else f32-input MFMA
+    const uint16_t* wmix3;           // mix weight pre-split in fragment order (ffc_fu_pack_mix3), or null
+    int w3_lds;                      // wmix3 staged in the LDS weight region instead of wmixT
 };
 
 constexpr int FU_THREADS = 512;
@@ -145,11 +147,13 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     if (a.wm_lds && !from_spill) {
         typedef __attribute__((address_space(1))) void* gptr_t;
         typedef __attribute__((address_space(3))) void* lptr_t;
-        const int n4 = (C2 * a.Mpad) >> 2;   // Mpad is a multiple of 32
+        // the f32 weight (2C x Mpad floats) or its split pieces (Mpad / 32 x C / 8 fragments of 3 KB)
+        const float* wsrc = a.w3_lds ? reinterpret_cast<const float*>(a.wmix3) : a.wmixT;
+        const int n4 = a.w3_lds ? (a.Mpad >> 5) * (C >> 3) * 192 : (C2 * a.Mpad) >> 2;   // 16-byte groups
         for (int i0 = 0; i0 < n4; i0 += FU_THREADS) {
             if (i0 + (tid & ~63) < n4) {   // whole wave-instructions; the region is padded to 64 groups
                 const int i = min(i0 + tid, n4 - 1);
-                __builtin_amdgcn_global_load_lds((gptr_t)(a.wmixT + 4 * (size_t)i),
+                __builtin_amdgcn_global_load_lds((gptr_t)(wsrc + 4 * (size_t)i),
                                                  (lptr_t)(Wm + 4 * (i0 + (tid & ~63))), 16, 0, 0);
             }
         }
@@ -239,7 +243,24 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
         const float* zp = (h ? Zim : Zre) + nt * 32 + col;
         const int wstep = 2 * a.Mpad;
-        if (a.mix3) {
+        if (a.mix3 && a.wmix3) {
+            // the weight's pieces come pre-split (ffc_fu_pack_mix3: one 16-byte read per piece and
+            // k-block); only Z is split here
+            const int QN = C >> 3;
+            const uint16_t* w3 = (a.w3_lds ? reinterpret_cast<const uint16_t*>(Wm) : a.wmix3) +
+                                 (size_t)mt * QN * 1536 + lane * 8;
+#pragma unroll 2
+            for (int q = 0; q < QN; ++q) {
+                Split3 av;
+                av.hi = *reinterpret_cast<const bf16x8*>(w3 + q * 1536);
+                av.mid = *reinterpret_cast<const bf16x8*>(w3 + q * 1536 + 512);
+                av.lo = *reinterpret_cast<const bf16x8*>(w3 + q * 1536 + 1024);
+                float zv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) zv[j] = zp[(8 * q + j) * NB];
+                acc = mfma_split3(av, split3(zv), acc);
+            }
+        } else if (a.mix3) {
             // fp32-accurate split-bf16 products (ffc_internal.h split3 / mfma_split3): k-block q, lane
             // half h element j is k = 2 (8q + j) + h -- channel 8q + j, Re (h = 0) or Im (h = 1) --
             // in both operands; six bf16 MFMAs per 16 k instead of eight f32 MFMAs at twice the cycles
@@ -532,6 +553,15 @@ bool fu_mix3_on() {
     }();
     return on;
 }
+// with pre-split weights (ffc_fu_forward_ex3) the split mix is the default; FFC_FU_MFMA=f32 keeps the
+// exact f32-input MFMA (A/B)
+bool fu_mix_f32_forced() {
+    static const bool on = [] {
+        const char* e = std::getenv("FFC_FU_MFMA");
+        return e && e[0] == 'f';
+    }();
+    return on;
+}
 // FFC_FU_SPLIT=0: pass 1 as one workgroup per sample (fu_kernel) for A/B runs
 bool fu_split_on() {
     static const bool on = [] {
@@ -547,11 +577,16 @@ struct FuLayout {
     size_t bytes;
     int wm_lds, scr_off, bn_off;
 };
-FuLayout fu_layout(int C, int H, int W) {
+// floats of the LDS weight region holding the split pieces: (Mpad / 32) x (C / 8) fragments of 3 KB
+__host__ inline size_t fu_wm3_floats(int C) {
+    const size_t Mpad = (size_t)(2 * C + 31) / 32 * 32;
+    return ((Mpad / 32) * (size_t)(C / 8) * 768 + 255) / 256 * 256;
+}
+FuLayout fu_layout(int C, int H, int W, bool packed = false) {
     const size_t plane = (size_t)C * H * (W / 2 + 1);
     const bool in_y = plane >= (size_t)FU_SCRATCH;
     for (int wm = 1; wm >= 0; --wm) {
-        const size_t wfl = wm ? fu_wm_floats(C) : 0;
+        const size_t wfl = wm ? (packed ? fu_wm3_floats(C) : fu_wm_floats(C)) : 0;
         const size_t scr = in_y ? 0 : FU_SCRATCH;
         const size_t floats = 4 * plane + wfl + scr + 6 * (size_t)C;
         if (4 * floats <= 160 * 1024)
@@ -583,15 +618,75 @@ extern "C" int ffc_fu_forward(const float* t, int B, int C, int H, int W, int up
                              bn_shift, residual, out, nullptr, nullptr, nullptr, stream);
 }
 
+namespace {
+__global__ void fu_pack_mix3_kernel(const float* __restrict__ wmixT, int C, int Mpad, uint16_t* __restrict__ out) {
+    const int QN = C / 8, n = (Mpad / 32) * QN * 64;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int lane = i & 63, fr = i >> 6;   // fragment fr = M-tile * QN + k-block
+        const int mt = fr / QN, q = fr - mt * QN;
+        const int h = lane >> 5, col = lane & 31;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = wmixT[(size_t)(2 * (8 * q + j) + h) * Mpad + mt * 32 + col];
+        const Split3 sp = split3(v);
+        uint16_t* d = out + (size_t)fr * 1536 + lane * 8;
+        *reinterpret_cast<u32x4*>(d) = __builtin_bit_cast(u32x4, sp.hi);
+        *reinterpret_cast<u32x4*>(d + 512) = __builtin_bit_cast(u32x4, sp.mid);
+        *reinterpret_cast<u32x4*>(d + 1024) = __builtin_bit_cast(u32x4, sp.lo);
+    }
+}
+}  // namespace
+
+extern "C" size_t ffc_fu_mix3_elems(int C) {
+    if (C <= 0 || C % 8 != 0) return 0;
+    return (size_t)((2 * C + 31) / 32) * (C / 8) * 1536;
+}
+
+extern "C" int ffc_fu_pack_mix3(const float* wmixT, int C, uint16_t* wmix3, void* stream) {
+    FFC_CHECK_ARG(wmixT && wmix3 && C > 0 && C % 8 == 0, "ffc_fu_pack_mix3: bad args (C % 8 == 0)");
+    FFC_CHECK_ARG((reinterpret_cast<uintptr_t>(wmix3) & 15) == 0, "ffc_fu_pack_mix3: wmix3 must be 16-byte aligned");
+    const int Mpad = (2 * C + 31) / 32 * 32;
+    const int n = (Mpad / 32) * (C / 8) * 64;
+    hipLaunchKernelGGL(fu_pack_mix3_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, wmixT, C, Mpad,
+                       wmix3);
+    return ffc::launch_status("ffc_fu_pack_mix3");
+}
+
+static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                           const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
+                           float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
+                           const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream);
+
 extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
                                  const float* in_shift, int in_relu, const float* wmixT, int pass, float* stats_slab,
                                  const float* bn_scale, const float* bn_shift, int residual, float* out,
                                  const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill,
                                  void* stream) {
+    return fu_forward_impl(t, B, C, H, W, up, in_scale, in_shift, in_relu, wmixT, nullptr, pass, stats_slab, bn_scale,
+                           bn_shift, residual, out, in_fold, mix_fold, yspill, stream);
+}
+
+extern "C" int ffc_fu_forward_ex3(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                                  const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3,
+                                  int pass, float* stats_slab, const float* bn_scale, const float* bn_shift,
+                                  int residual, float* out, const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold,
+                                  float* yspill, void* stream) {
+    FFC_CHECK_ARG(!wmix3 || (C % 8 == 0 && (reinterpret_cast<uintptr_t>(wmix3) & 15) == 0),
+                  "ffc_fu_forward_ex3: wmix3 needs C % 8 == 0 and 16-byte alignment");
+    return fu_forward_impl(t, B, C, H, W, up, in_scale, in_shift, in_relu, wmixT, wmix3, pass, stats_slab, bn_scale,
+                           bn_shift, residual, out, in_fold, mix_fold, yspill, stream);
+}
+
+static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                           const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
+                           float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
+                           const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream) {
     FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu_forward: B and C must be positive");
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu_forward: up must be 1 or 2");
     FFC_CHECK_ARG(pass == 0 || pass == 1, "ffc_fu_forward: pass must be 0 or 1");
-    const size_t lds = ffc_fu_lds_bytes(C, H, W);
+    if (fu_mix_f32_forced() || C % 8 != 0) wmix3 = nullptr;
+    const bool packed = wmix3 != nullptr;
+    const size_t lds = ffc_fu_lds_bytes(C, H, W) > 0 ? fu_layout(C, H, W, packed).bytes : 0;
     FFC_CHECK_ARG(lds > 0, "ffc_fu_forward: unsupported (C,H,W): H,W must be powers of two in [4,32] "
                            "and 16*C*H*(W/2+1) <= 160 KiB");
     FFC_CHECK_ARG(t && wmixT, "ffc_fu_forward: null input");
@@ -628,8 +723,10 @@ extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int
     a.Mpad = (2 * C + 31) / 32 * 32;
     a.residual = residual;
     a.norm = (float)(1.0 / std::sqrt((double)H * (double)W));
-    const FuLayout lay = fu_layout(C, H, W);
+    const FuLayout lay = fu_layout(C, H, W, packed);
     a.wm_lds = lay.wm_lds;
+    a.wmix3 = wmix3;
+    a.w3_lds = packed && lay.wm_lds;
     a.scr_off = lay.scr_off;
     a.bn_off = lay.bn_off;
     a.has_in_fold = in_fold != nullptr;
@@ -640,7 +737,7 @@ extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int
     }
     if (mix_fold) a.mix_fold = *mix_fold;
     a.yspill = yspill;
-    a.mix3 = fu_mix3_on() && C % 8 == 0;
+    a.mix3 = (packed || fu_mix3_on()) && !fu_mix_f32_forced() && C % 8 == 0;
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;

@@ -48,6 +48,21 @@ class FourierUnitSN(nn.Module):
             return mixT
         return self._packs.get("mix", [w], build)
 
+    def _packed_mix3(self, mixT, device, stream):
+        """the mix weight's split bf16 pieces in MFMA fragment order (ffc_fu_pack_mix3), or None when
+        C % 8 != 0 (the fused kernel then splits wmixT itself)"""
+        w = self.conv_layer.weight
+        C = w.shape[0] // 2
+        n = rt.lib().ffc_fu_mix3_elems(C)
+        if n == 0:
+            return None
+
+        def build():
+            w3 = torch.empty(int(n), device=device, dtype=torch.int16)
+            check(rt.lib().ffc_fu_pack_mix3(ptr(mixT), C, ptr(w3), stream), "ffc_fu_pack_mix3")
+            return w3
+        return self._packs.get("mix3", [rt.require(w.detach(), "conv_layer.weight")], build)
+
     @staticmethod
     def _fold_ok(C, H, W):
         """the fused kernel's planes hold the in-kernel BN fold's scratch (csrc/bn_common.h)"""
@@ -80,6 +95,7 @@ class FourierUnitSN(nn.Module):
         dev = t.device
         stream = rt.stream_of(t)
         mixT = self._packed_mix(dev, stream)
+        mix3 = self._packed_mix3(mixT, dev, stream)
         use_batch, _ = rt.bn_mode(self.bn)
         n_r = float(B * C * H * W)              # fused FU moves 4*N_r per read/write
         n_y = float(B * 2 * C * H * (W // 2 + 1))
@@ -93,10 +109,11 @@ class FourierUnitSN(nn.Module):
             # moved: what this kernel pair actually streams (including the Y spill written and read back)
             mv0 = 4.0 * t.numel() + (4.0 * n_y if rt.FU_SPILL else 0.0)
             with rt.observe("fu_pass0", bytes=min(4.0 * n_r, mv0), moved=mv0):
-                check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
-                                          None if in_fold else ptr(in_shift), int(in_relu), ptr(mixT), 0, ptr(slab),
-                                          None, None, 0, None, ctypes.byref(in_fold.struct) if in_fold else None,
-                                          None, ptr(yspill), stream), "ffc_fu_forward(pass 0)")
+                check(L.ffc_fu_forward_ex3(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
+                                           None if in_fold else ptr(in_shift), int(in_relu), ptr(mixT), ptr(mix3), 0,
+                                           ptr(slab), None, None, 0, None,
+                                           ctypes.byref(in_fold.struct) if in_fold else None, None, ptr(yspill),
+                                           stream), "ffc_fu_forward(pass 0)")
             if in_fold is not None:          # pass 0's workgroup 0 wrote the folded bn1 affine
                 in_scale, in_shift = in_fold.scale, in_fold.shift
             mix_fold = None
@@ -114,9 +131,9 @@ class FourierUnitSN(nn.Module):
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         mv1 = (4.0 * n_y if yspill is not None else 4.0 * t.numel()) + 4.0 * t.numel() * bool(residual) + 4.0 * n_r
         with rt.observe("fu_pass1", bytes=min(8.0 * n_r, mv1), moved=mv1):
-            check(L.ffc_fu_forward_ex(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT), 1,
-                                      None, ptr(sc), ptr(sh), int(residual), ptr(out), None,
-                                      ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), stream),
+            check(L.ffc_fu_forward_ex3(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
+                                       ptr(mix3), 1, None, ptr(sc), ptr(sh), int(residual), ptr(out), None,
+                                       ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), stream),
                   "ffc_fu_forward(pass 1)")
         return out
 

@@ -431,6 +431,18 @@ int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int up, const 
                       const float* in_shift, int in_relu, const float* wmixT, int pass, float* stats_slab,
                       const float* bn_scale, const float* bn_shift, int residual, float* out,
                       const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream);
+/* ffc_fu_forward_ex with the mix weight also given pre-split (wmix3 from ffc_fu_pack_mix3, C % 8 == 0):
+ * the spectral mix then runs on split-bf16 MFMA products (six bf16 MFMAs per 16-deep k-block, each
+ * product within 2^-21 of the fp32 product) and reads each weight piece as one 16-byte fragment
+ * instead of splitting wmixT in every tile.  wmix3 = NULL (or FFC_FU_MFMA=f32) is ffc_fu_forward_ex. */
+int ffc_fu_forward_ex3(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                       const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
+                       float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
+                       const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream);
+/* wmixT (ffc_fu_pack_mix) -> its split bf16 pieces in MFMA fragment order: ffc_fu_mix3_elems(C) uint16
+ * (16-byte aligned); 0 when C % 8 != 0 */
+size_t ffc_fu_mix3_elems(int C);
+int ffc_fu_pack_mix3(const float* wmixT, int C, uint16_t* wmix3, void* stream);
 
 /* Large-plane Fourier unit (FourierUnitSN.forward, fourier_unity.py:32-56, for planes whose
  * per-sample spectrum does not fit one workgroup's LDS: the fgan128 generator's 64x64 and
