@@ -647,10 +647,11 @@ FORCE_FU2D = False  # large-plane FU stages even where the fused per-sample FU a
 # (st_prologue.hip), else SE gate + gated 1x1 GEMM (st_pw.hip); "pw" forces the latter (A/B runs)
 ST_PATH = __import__("os").environ.get("FFC_ST_PATH", "auto")
 # Fourier-unit path where both apply: the fused one-workgroup-per-sample kernel fills the chip only
-# with B >= ~CUs/2 samples; smaller batches (fgan128's 64-sample shards) run the staged kernels,
-# which spread every sample over many workgroups.  "auto" | "fused" | "staged"
+# with B >= ~CUs/4 samples; smaller batches run the staged kernels, which spread every sample over
+# many workgroups.  "auto" | "fused" | "staged".  The threshold was 128 until the fused mix ran on
+# pre-split weights (r05ad); gen64 B = 64 then measured 0.2161 -> 0.2147 ms fused (r05af)
 FU_PATH = __import__("os").environ.get("FFC_FU_PATH", "auto")
-FU_FUSED_MIN_BATCH = 128
+FU_FUSED_MIN_BATCH = 64
 FU_COLS = True      # staged FU: inverse column FFT fused into mix pass 1, rows-only C2R (H in 32..128)
 # staged FU, batch-statistics BN: pass 0 spills the raw Y and the whole-plane C2R applies BN + ReLU on
 # load (no second mix); FFC_FU2D_SPILL=0 keeps the two-pass mix

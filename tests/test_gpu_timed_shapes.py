@@ -1,6 +1,6 @@
 """Parity at the shapes bench.py times (VERDICT r1 "parity at the timed shapes").
 
-Kernel choice depends on the batch: the fused per-sample Fourier unit needs B >= 128
+Kernel choice depends on the batch: the fused per-sample Fourier unit needs B >= 64
 (_runtime.FU_FUSED_MIN_BATCH), the patch-conv tile configuration (_plan.pick_patch_cfg), the
 1x1 GEMM tiles (_runtime.pick_pw_cfg) and the weight-gradient split (_autograd.wgrad_splits)
 depend on B too.  So every per-GPU batch a bench line runs is checked here against the oracle:
