@@ -74,6 +74,7 @@ struct FuArgs {
     int mix3;                        // mix on split-bf16 MFMA products (C % 8 == 0), else f32-input MFMA
     const uint16_t* wmix3;           // mix weight pre-split in fragment order (ffc_fu_pack_mix3), or null
     int w3_lds;                      // wmix3 staged in the LDS weight region instead of wmixT
+    int mgroups;                     // pass 0: workgroups per sample, each mixing MT / mgroups M-tiles
 };
 
 constexpr int FU_THREADS = 512;
@@ -136,7 +137,10 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int C = a.C;
     const int C2 = 2 * C;
-    const int b = blockIdx.x;
+    // pass 0 over mgroups workgroups per sample (small batches: more CUs): each repeats the sample's
+    // FFTs and mixes / spills / reduces the statistics of its own M-tiles only
+    const int G = PASS == 0 ? a.mgroups : 1;
+    const int b = blockIdx.x / G, grp = blockIdx.x - b * G;
     const int tid = threadIdx.x;
     float* Zre = smem;
     float* Zim = Zre + C * NB;
@@ -164,6 +168,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     FU_STAMP(0);
     const int lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
     const int MT = (C2 + 31) >> 5, NTL = (NB + 31) >> 5;
+    const int MTG = MT / G;   // this workgroup's M-tiles (pass 0): grp * MTG .. grp * MTG + MTG - 1
     float* bnss = smem + a.bn_off;    // pass 1: BN scale [2C] | shift [2C]
     float* insc = bnss + 2 * C2;      // folded input affine: scale [C] | shift [C]
     // fold scratch: the Z/Y planes, all free until the row R2C / spill load below
@@ -236,8 +241,8 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
 
     // 3. spectral mix on MFMA: Y[o][n] = sum_i Wmix[o][i] Z[i][n], Z[2c+h] = (h ? Im : Re)(channel c)
     //    k-step s feeds k-slot h = lane>>5 with channel s, component h.
-    for (int tile = wave; tile < MT * NTL; tile += FU_THREADS / 64) {
-        const int mt = tile % MT, nt = tile / MT;
+    for (int tile = wave; tile < MTG * NTL; tile += FU_THREADS / 64) {
+        const int mt = grp * MTG + tile % MTG, nt = tile / MTG;
         floatx16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
@@ -326,7 +331,8 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     if constexpr (PASS == 0) {
         FU_STAMP(4);
         // merge the per-tile partials of each channel (Chan et al.) -> one slab row per sample
-        for (int o = tid; o < C2; o += FU_THREADS) {
+        const int o_hi = min(C2, (grp + 1) * MTG * 32);
+        for (int o = grp * MTG * 32 + tid; o < o_hi; o += FU_THREADS) {
             float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
             for (int nt = 0; nt < NTL; ++nt) {
                 const float* st = Yre + (nt * C2 + o) * 3;
@@ -738,6 +744,28 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
     if (mix_fold) a.mix_fold = *mix_fold;
     a.yspill = yspill;
     a.mix3 = (packed || fu_mix3_on()) && !fu_mix_f32_forced() && C % 8 == 0;
+    // pass 0 of small batches over several workgroups per sample (M-tile groups) while the grid
+    // stays within one workgroup per CU; FFC_FU_MGROUPS = 1 keeps one per sample (A/B)
+    a.mgroups = 1;
+    if (pass == 0) {
+        static const int force = [] {
+            const char* e = std::getenv("FFC_FU_MGROUPS");
+            return e ? std::atoi(e) : 0;
+        }();
+        const int MT = (2 * C + 31) / 32;
+        int cus = 256, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        for (int g : {4, 2}) {
+            if (force > 0 ? g == force : (long long)B * g <= cus) {
+                if (MT % g == 0) {
+                    a.mgroups = g;
+                    break;
+                }
+            }
+        }
+    }
     if (lds > 64 * 1024) {
         // opt each instance into the full 160 KiB once (not a stream op; safe under capture)
         static std::mutex mu;
@@ -765,7 +793,7 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
             return ffc::launch_status("ffc_fu_forward");
         }
     }
-    hipLaunchKernelGGL(k, dim3(B), dim3(FU_THREADS), lds, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)B * a.mgroups), dim3(FU_THREADS), lds, (hipStream_t)stream, a);
     return ffc::launch_status("ffc_fu_forward");
 }
 
