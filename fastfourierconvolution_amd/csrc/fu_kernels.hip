@@ -744,8 +744,8 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
     if (mix_fold) a.mix_fold = *mix_fold;
     a.yspill = yspill;
     a.mix3 = (packed || fu_mix3_on()) && !fu_mix_f32_forced() && C % 8 == 0;
-    // pass 0 of small batches over several workgroups per sample (M-tile groups) while the grid
-    // stays within one workgroup per CU; FFC_FU_MGROUPS = 1 keeps one per sample (A/B)
+    // pass 0 of small batches over two workgroups per sample (M-tile groups) while the grid stays
+    // within one workgroup per CU; FFC_FU_MGROUPS = 1 keeps one per sample, = 4 four (A/B)
     a.mgroups = 1;
     if (pass == 0) {
         static const int force = [] {
@@ -757,7 +757,8 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             cus = 256;
-        for (int g : {4, 2}) {
+        for (int g : {4, 2}) {   // 2 unless forced: 4 groups repeat the FFTs once too often (B = 32: r05an)
+            if (force <= 0 && g == 4) continue;
             if (force > 0 ? g == force : (long long)B * g <= cus) {
                 if (MT % g == 0) {
                     a.mgroups = g;
