@@ -60,16 +60,18 @@ def test_rccl_moments_all_reduce_in_graph(rccl_world1):
     assert torch.equal(m, ref * 4)
 
 
-def test_syncbn_generator_graph_over_rccl(rccl_world1):
+@pytest.mark.parametrize("B", [32, 64, 128])
+def test_syncbn_generator_graph_over_rccl(rccl_world1, B):
     """train-mode generator forward with every BN's moments all-reduced over RCCL: eager and
-    hipGraph-replayed outputs equal the forward without SyncBN, running statistics included"""
+    hipGraph-replayed outputs equal the forward without SyncBN, running statistics included
+    (B = 32: staged 16² / 32² FUs; 64 / 128: the fused FU over two workgroups per sample)"""
     import fastfourierconvolution_amd as F
     from fastfourierconvolution_amd import distributed as D
     from fastfourierconvolution_amd import _runtime as rt
     torch.manual_seed(0)
     with contextlib.redirect_stdout(io.StringIO()):
         G = F.FFCGenerator(100, 3, 64).cuda().train()
-    z = torch.randn(32, 100, 1, 1, device="cuda")
+    z = torch.randn(B, 100, 1, 1, device="cuda")
     state = {k: v.clone() for k, v in G.state_dict().items()}
     with torch.no_grad():
         ref = G(z).clone()
