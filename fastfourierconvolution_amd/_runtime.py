@@ -280,9 +280,10 @@ def _pow2_floor(v: int) -> int:
     return 1 << (v.bit_length() - 1)
 
 
-# cap, rounded to 2^k: 4 since the SE gate went thread-per-channel (B = 32: 0.1755 -> 0.1731 ms with 4
-# instead of 8, profiles/r05/an; r04 had measured them level)
-ST_SPLIT_MAX = _pow2_floor(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "4"))
+# cap, rounded to 2^k: 2 since the SE gate went thread-per-channel (B = 32: 0.1755 -> 0.1731 ms with 4
+# instead of 8, profiles/r05/an; B = 64 0.2105 -> 0.2092 ms with 2 instead of 4, r05/av; r04 had
+# measured them level)
+ST_SPLIT_MAX = _pow2_floor(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "2"))
 # ST prologue conv1 on the split-bf16 MFMA products (FFC_ST_MFMA=f32: the exact f32-input MFMA, A/B)
 ST_SPLIT_MFMA = __import__("os").environ.get("FFC_ST_MFMA", "split") != "f32"
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)
