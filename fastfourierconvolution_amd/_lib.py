@@ -138,6 +138,11 @@ SIGNATURES = [
     ("ffc_fu_forward_ex3", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                                    c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                    ctypes.POINTER(BnFold), ctypes.POINTER(BnFold), c_void_p, c_void_p]),
+    ("ffc_fu_forward_ex4", c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                   c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                   ctypes.POINTER(BnFold), ctypes.POINTER(BnFold), c_void_p, c_int, c_void_p]),
+    ("ffc_fu_kgroups", c_int, [c_int, c_int, c_int, c_int]),
+    ("ffc_fu_slab_rows", c_int, [c_int, c_int, c_int, c_int, c_int]),
     ("ffc_fu_mix3_elems", c_size_t, [c_int]),
     ("ffc_fu_pack_mix3", c_int, [c_void_p, c_int, c_void_p, c_void_p]),
     ("ffc_fu_pack_mix", c_int, [c_void_p, c_int, c_void_p, c_void_p]),

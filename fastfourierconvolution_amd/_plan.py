@@ -18,6 +18,9 @@ import os
 
 import numpy as np
 
+# FFC_CONVQ_TCMAX: convq pixel-block width cap (A/B), read once; part of _runtime.plan_knobs()
+CONVQ_TCMAX = int(os.environ.get("FFC_CONVQ_TCMAX", "0"))
+
 BK = 16
 MPAD = 128
 TILE_CFGS = {0: (128, 128, 2), 1: (64, 128, 2), 2: (32, 256, 4)}  # cfg -> (BM, BN, slab rows per tile)
@@ -444,9 +447,8 @@ def plan_convq_job(B: int, M: int, segs, cfg: int):
     PHm = max(ph.PH for ph in base.phases)
     PWm = max(ph.PW for ph in base.phases)
     TC = min(PWm, npix)
-    tc_max = int(os.environ.get("FFC_CONVQ_TCMAX", "0"))   # A/B: squarer pixel blocks (less halo)
-    if tc_max >= 4 and TC > tc_max:
-        TC = tc_max
+    if CONVQ_TCMAX >= 4 and TC > CONVQ_TCMAX:   # A/B: squarer pixel blocks (less halo)
+        TC = CONVQ_TCMAX
     TR = min(PHm, max(1, npix // TC))
     NS = max(1, min(B, npix // (TR * TC)))
     nrb, ncb = -(-PHm // TR), -(-PWm // TC)

@@ -337,6 +337,13 @@ def bn_fold(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, dev
 BN_CHFOLD = __import__("os").environ.get("FFC_BN_CHFOLD", "1") != "0"
 BN_CHFOLD_LOADS = int(__import__("os").environ.get("FFC_BN_CHFOLD_LOADS", "16"))
 BN_CHFOLD_READS = int(__import__("os").environ.get("FFC_BN_CHFOLD_READS", "16384"))
+# mirrors fu_kernels.hip fu_split_on(): FFC_FU_SPLIT=0 runs the fused FU's pass 1 as one workgroup per
+# sample, which folds a mix BN over its whole slab (bn_fold_block) -- a channel-only fold descriptor
+# (the split pass 1's) must not reach it
+FU_SPLIT = __import__("os").environ.get("FFC_FU_SPLIT", "1")[:1] != "0"
+# fused FU pass 0 over two bin groups per sample where the library takes them (ffc_fu_kgroups, round
+# 6); FFC_FU_KGROUPS=1 (read by the library too) or FU_KGROUPS = False keeps one workgroup per sample
+FU_KGROUPS = __import__("os").environ.get("FFC_FU_KGROUPS", "2")[:1] != "1"
 
 
 def bn_fold_channels(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, lanes: int = 64,
@@ -530,7 +537,15 @@ class StreamPool:
                 self._all.append(obj)
         last = self._last.get(id(obj))
         if last is not None and last[0] != me:
-            torch.cuda.current_stream().wait_stream(last[1])
+            cur = torch.cuda.current_stream()
+            if torch.cuda.is_current_stream_capturing():
+                # a wait on an event recorded outside the capture would invalidate it:
+                # drain the previous holder's stream from the host instead (legal under the
+                # thread-local capture mode graphs.capture_step uses)
+                if last[1] != cur:
+                    last[1].synchronize()
+            else:
+                cur.wait_stream(last[1])
         return obj
 
     def give(self, obj):
@@ -594,7 +609,8 @@ def plan_knobs():
     cache key, so a changed switch never meets a plan made under another setting"""
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
-            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, BN_CHFOLD_READS, ST_SPLIT_MFMA, FU2D_R2CMIX)
+            ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, BN_CHFOLD_READS, ST_SPLIT_MFMA, FU2D_R2CMIX,
+            FU_SPLIT, _plan.CONVQ_TCMAX, FU_KGROUPS)
 
 
 def algorithmic_flops(plan) -> float:

@@ -147,6 +147,10 @@ __device__ __forceinline__ double permlane_sum_f64(double v) {
 // (each v += partner(v) with an involutive partner): every lane of a group holds the bit-identical sum
 template <int L>
 __device__ __forceinline__ double group_sum_f64(double v) {
+#ifdef FFC_FOLD_SHFL
+    for (int m = 1; m < L; m <<= 1) v += shfl_xor_f64(v, m);
+    return v;
+#endif
     if constexpr (L >= 2) v += dpp_full_f64<0xB1>(v);     // quad_perm [1,0,3,2]: lane ^ 1
     if constexpr (L >= 4) v += dpp_full_f64<0x4E>(v);     // quad_perm [2,3,0,1]: lane ^ 2
     if constexpr (L >= 8) v += dpp_full_f64<0x141>(v);    // row_half_mirror: the other quad of the 8

@@ -78,4 +78,73 @@ __device__ __forceinline__ void fft_reg(float (&re)[N], float (&im)[N]) {
     }
 }
 
+// Real-input N-point DFT X[k] = sum_n x[n] exp(-2 pi i k n / N), k = 0 .. N/2, through ONE
+// N/2-point complex FFT of z[n] = x[2n] + i x[2n+1] (half the butterflies and registers of
+// fft_reg<N> on (x, 0)):  X[k] = E[k] + W^k O[k],  E = (Z[k] + conj Z[M-k]) / 2,
+// O = (Z[k] - conj Z[M-k]) / 2i,  W = exp(-2 pi i / N),  M = N/2 (Z[M] = Z[0]).
+template <int N>
+__device__ __forceinline__ void rfft_reg(const float (&x)[N], float (&Xr)[N / 2 + 1], float (&Xi)[N / 2 + 1]) {
+    constexpr int M = N / 2;
+    float zr[M], zi[M];
+#pragma unroll
+    for (int n = 0; n < M; ++n) {
+        zr[n] = x[2 * n];
+        zi[n] = x[2 * n + 1];
+    }
+    fft_reg<M, false>(zr, zi);
+    Xr[0] = zr[0] + zi[0];
+    Xi[0] = 0.0f;
+    Xr[M] = zr[0] - zi[0];
+    Xi[M] = 0.0f;
+#pragma unroll
+    for (int k = 1; k < M; ++k) {
+        const float ar = zr[k], ai = zi[k], br = zr[M - k], bi = zi[M - k];
+        const float er = 0.5f * (ar + br), ei = 0.5f * (ai - bi);
+        const float orr = 0.5f * (ai + bi), oi = 0.5f * (br - ar);
+        if (4 * k == N) {   // W^k = -i
+            Xr[k] = er + oi;
+            Xi[k] = ei - orr;
+        } else {
+            const float c = c_twc[k * (128 / N)], s = c_tws[k * (128 / N)];   // W^k = c - i s
+            Xr[k] = er + (orr * c + oi * s);
+            Xi[k] = ei + (oi * c - orr * s);
+        }
+    }
+}
+
+// Its inverse without normalisation, the C2R of irfftn: x[n] = sum_{k<N} F[k] exp(+2 pi i k n / N)
+// with F[k] = X[k] (k <= N/2, Im of X[0] and X[N/2] ignored) and F[N-k] = conj X[k], through ONE
+// N/2-point inverse FFT of Z[k] = (F[k] + F[k+M]) + i W^-k (F[k] - F[k+M]) (F[k+M] = conj X[M-k]):
+// z[n] = x[2n] + i x[2n+1].
+template <int N>
+__device__ __forceinline__ void irfft_reg(const float (&Xr)[N / 2 + 1], const float (&Xi)[N / 2 + 1], float (&x)[N]) {
+    constexpr int M = N / 2;
+    float zr[M], zi[M];
+    zr[0] = Xr[0] + Xr[M];
+    zi[0] = Xr[0] - Xr[M];
+#pragma unroll
+    for (int k = 1; k < M; ++k) {
+        const float ar = Xr[k], ai = Xi[k], br = Xr[M - k], bi = Xi[M - k];
+        const float sr = ar + br, si = ai - bi;   // F[k] + conj X[M-k]
+        const float dr = ar - br, di = ai + bi;   // F[k] - conj X[M-k]
+        float tr, ti;                             // T = W^-k D, W^-k = c + i s
+        if (4 * k == N) {
+            tr = -di;
+            ti = dr;
+        } else {
+            const float c = c_twc[k * (128 / N)], s = c_tws[k * (128 / N)];
+            tr = dr * c - di * s;
+            ti = dr * s + di * c;
+        }
+        zr[k] = sr - ti;   // Z = S + i T
+        zi[k] = si + tr;
+    }
+    fft_reg<M, true>(zr, zi);
+#pragma unroll
+    for (int n = 0; n < M; ++n) {
+        x[2 * n] = zr[n];
+        x[2 * n + 1] = zi[n];
+    }
+}
+
 }  // namespace

@@ -953,7 +953,30 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
     //    non-deterministic here -- T of two channels wrong in a few workgroups per launch (r05i,
     //    tools/experiments/r2cmix_*.py) -- and bn_fold_block is not.
     if (ra.has_fold) {
+#ifdef FFC_R2CMIX_CHFOLD
+#ifdef FFC_R2CMIX_DMA_WAIT
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#ifdef FFC_R2CMIX_PREBAR
+        __syncthreads();
+#endif
+        constexpr int L = FU2_THREADS / C;
+        float s_, h_;
+        const int o = tid / L;
+#ifdef FFC_R2CMIX_NOLEAD
+        constexpr bool lead = false;
+#else
+        const bool lead = blockIdx.x == 0;
+#endif
+        ffc::bn_fold_channels<L>(ra.fold, o, lead, s_, h_);
+        if ((tid & (L - 1)) == 0) {
+            fss[o] = s_;
+            fss[C + o] = h_;
+        }
+        if (lead && tid == 0 && ra.fold.update_running) *ra.fold.num_batches_tracked += 1;
+#else
         ffc::bn_fold_block<FU2_THREADS>(ra.fold, fss, fss + C, blockIdx.x == 0, reinterpret_cast<double*>(scr));
+#endif
     } else if (tid < C) {
         fss[tid] = ra.in_scale ? ra.in_scale[tid] : 1.0f;
         fss[C + tid] = ra.in_scale ? ra.in_shift[tid] : 0.0f;

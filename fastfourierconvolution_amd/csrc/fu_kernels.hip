@@ -75,6 +75,8 @@ struct FuArgs {
     const uint16_t* wmix3;           // mix weight pre-split in fragment order (ffc_fu_pack_mix3), or null
     int w3_lds;                      // wmix3 staged in the LDS weight region instead of wmixT
     int mgroups;                     // pass 0: workgroups per sample, each mixing MT / mgroups M-tiles
+    int B;
+    int kgroups;                     // bin groups of pass 0 (fu_pass0_kg_kernel): slab rows, spill layout
 };
 
 constexpr int FU_THREADS = 512;
@@ -127,6 +129,47 @@ __device__ __forceinline__ void load_s_row(const FuArgs& a, const float* insc, i
         v = fmaf(v, sc, sh);
         if (a.in_relu) v = fmaxf(v, 0.0f);
         s[x] = v;
+    }
+}
+
+// bin groups of the fused FU's pass 0 (fu_pass0_kg_kernel below): columns per group
+template <int W, int G>
+struct FuKg {
+    static constexpr int WP = W / 2 + 1;
+    static constexpr int KW0 = (WP + G - 1) / G;
+    static constexpr int KWL = WP - (G - 1) * KW0;   // the last group's columns
+    static_assert(KWL >= 1, "every bin group non-empty");
+};
+
+// spill offset (within a channel's NB floats) of bin (y, k) -> the natural bin index y WP + k:
+// the inverse map pass 1 applies to the bin-group layout
+template <int H, int W, int G>
+__device__ __forceinline__ int fu_spill_bin(int m) {
+    if constexpr (G == 1) {
+        return m;
+    } else {
+        using K = FuKg<W, G>;
+        constexpr int ZPL = H * K::KW0;
+        const int g = min(m / ZPL, G - 1);
+        const int rem = m - g * ZPL;
+        const int y = g < G - 1 ? rem / K::KW0 : rem / K::KWL;
+        const int kk = rem - y * (g < G - 1 ? K::KW0 : K::KWL);
+        return y * K::WP + g * K::KW0 + kk;
+    }
+}
+
+// BN + ReLU of spilled floats m .. m + 3 of one channel -> its Y plane (natural bin order)
+template <int H, int W, int G>
+__device__ __forceinline__ void spill_to_plane(float* dst, int m, float4 v, float sc, float sh) {
+    v = make_float4(fmaxf(fmaf(v.x, sc, sh), 0.0f), fmaxf(fmaf(v.y, sc, sh), 0.0f), fmaxf(fmaf(v.z, sc, sh), 0.0f),
+                    fmaxf(fmaf(v.w, sc, sh), 0.0f));
+    if constexpr (G == 1) {
+        *reinterpret_cast<float4*>(dst + m) = v;
+    } else {
+        dst[fu_spill_bin<H, W, G>(m)] = v.x;
+        dst[fu_spill_bin<H, W, G>(m + 1)] = v.y;
+        dst[fu_spill_bin<H, W, G>(m + 2)] = v.z;
+        dst[fu_spill_bin<H, W, G>(m + 3)] = v.w;
     }
 }
 
@@ -192,9 +235,11 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             const int o = (4 * i) / NB, n = 4 * i - o * NB;
             const float4 v = ys[i];
             const float sc = bnss[o], sh = bnss[C2 + o];
-            float* dst = ((o & 1) ? Yim : Yre) + (o >> 1) * NB + n;
-            *reinterpret_cast<float4*>(dst) = make_float4(fmaxf(fmaf(v.x, sc, sh), 0.0f), fmaxf(fmaf(v.y, sc, sh), 0.0f),
-                                                          fmaxf(fmaf(v.z, sc, sh), 0.0f), fmaxf(fmaf(v.w, sc, sh), 0.0f));
+            float* dst = ((o & 1) ? Yim : Yre) + (o >> 1) * NB;
+            if (a.kgroups == 2)
+                spill_to_plane<H, W, 2>(dst, n, v, sc, sh);
+            else
+                spill_to_plane<H, W, 1>(dst, n, v, sc, sh);
         }
         __syncthreads();
     } else {
@@ -408,12 +453,213 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- pass 0 over bin groups
+// fu_kernel's pass 0 holds a sample's whole spectrum (4 planes) in LDS: at ffc2 / ffc3 of the
+// generator that is 133-146 KB, one workgroup per CU, and at B = 256 the grid is exactly one round
+// of 256 workgroups whose load -> row R2C -> column FFT -> mix -> statistics phases run back to back
+// with nothing to overlap them (VERDICT r05 "occupancy-capped").  Pass 0 needs no Y planes, and a
+// column FFT needs only its own column: here G workgroups share a sample, workgroup g keeping only
+// the half-spectrum columns k in [g KW0, g KW0 + kw) (KW0 = ceil((W/2+1) / G)).  Each repeats the
+// row R2C (a few hundred VALU per row) but holds, transforms, mixes and spills only its columns:
+// LDS Z (2 C H KW0 floats) + tile statistics + a 16-row statistics scratch, 2-4 workgroups per CU.
+//   spill layout (per sample and channel o, still NB floats): [g][y][k - g KW0] -- workgroup g
+//   stores whole 32-bin runs; pass 1 decodes it (fu_spill_bin).
+//   slab rows: b G + g, each a partial over the workgroup's bins (the fold / reduce merge them).
+// Grid: blockIdx = g B + b, so a sample's groups share an XCD (B % 8 == 0) and its t planes' second
+// read comes from that XCD's L2.
+// tile_row_stats (ffc_internal.h) in two rounds of 16 rows through a 16 x 33 per-wave scratch (half
+// the LDS): lane quad 4 o' .. 4 o' + 3 reduces row 16 R + o' over 8 columns each (quad DPP sums,
+// bit-identical in the quad).  mean[R], m2[R]: row 16 R + (lane >> 2), valid in every lane.
+__device__ __forceinline__ void tile_row_stats16(const floatx16& acc, int nv, float* scratch, float (&mean)[2],
+                                                 float (&m2)[2]) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const int o = lane >> 2, c0 = (lane & 3) * 8;
+#pragma unroll
+    for (int R = 0; R < 2; ++R) {
+        wave_lds_sync();   // the previous round's (or tile's) reads of the scratch precede these writes
+#pragma unroll
+        for (int r = 8 * R; r < 8 * R + 8; ++r) scratch[((r & 3) + 8 * ((r >> 2) & 1) + 4 * h) * 33 + col] = acc[r];
+        wave_lds_sync();   // another lane's writes precede these reads (one wave: LDS in order)
+        float v[8];
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            v[j] = scratch[o * 33 + c0 + j];
+            if (c0 + j < nv) s += v[j];
+        }
+        s += ffc::dpp_full<0xB1>(s);
+        s += ffc::dpp_full<0x4E>(s);
+        const float mu = s / (float)nv;
+        float q = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float d = v[j] - mu;
+            if (c0 + j < nv) q = fmaf(d, d, q);
+        }
+        q += ffc::dpp_full<0xB1>(q);
+        q += ffc::dpp_full<0x4E>(q);
+        mean[R] = mu;
+        m2[R] = q;
+    }
+    wave_lds_sync();
+}
+
+constexpr int FU_KG_SCRATCH = (FU_THREADS / 64) * 16 * 33;
+
+// one bin group's body: group GI, columns K0 .. K0 + KW - 1 (compile-time strides and register
+// indices: the column lines' LDS offsets become immediates)
+template <int H, int W, int UP, int G, int GI>
+__device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
+    using K = FuKg<W, G>;
+    constexpr int WP = K::WP, NB = H * WP, KW0 = K::KW0;
+    constexpr int ZPL = H * KW0;                          // LDS bins of one channel (the widest group)
+    constexpr int K0 = GI * KW0, KW = GI < G - 1 ? KW0 : K::KWL;
+    constexpr int NBL = H * KW;                           // this group's bins per channel
+    constexpr int NTL = (NBL + 31) / 32;
+    const int C = a.C, C2 = 2 * C;
+    const int b = blockIdx.x % a.B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
+    float* Zre = smem;                                    // [C][H][KW] (channel stride NBL)
+    float* Zim = Zre + C * ZPL;
+    float* Wm = Zim + C * ZPL;                            // split mix weight (when staged: wm_lds)
+    float* st = smem + a.scr_off;                         // tile statistics [NTL][C2][3]
+    float* scr = st + ((ZPL + 31) / 32) * C2 * 3;         // per-wave 16 x 33 row scratch
+    const float* insc = smem + a.bn_off;                  // folded input affine: scale [C] | shift [C]
+
+    // 1. row R2C of every (channel, row) on a W/2-point complex FFT (rfft_reg); this group's columns
+    for (int r = tid; r < C * H; r += FU_THREADS) {
+        const int ch = r / H, y = r - ch * H;
+        float sv[W], re[WP], im[WP];
+        load_s_row<W, UP>(a, insc, b, ch, y, H, sv);
+        rfft_reg<W>(sv, re, im);
+        float* zr = Zre + ch * NBL + y * KW;
+        float* zi = Zim + ch * NBL + y * KW;
+#pragma unroll
+        for (int kk = 0; kk < KW; ++kk) {
+            zr[kk] = re[K0 + kk];
+            zi[kk] = im[K0 + kk];
+        }
+    }
+    // the mix weight's LDS-DMA (the kernel's first loads) is tracked by vmcnt only: this wave's
+    // copies landed before the barrier, so every wave may read Wm after it
+    if (a.wm_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // 2. column C2C over H of this group's columns, ortho scale
+    for (int q = tid; q < C * KW; q += FU_THREADS) {
+        const int ch = q / KW, kk = q - ch * KW;
+        float* zr = Zre + ch * NBL + kk;
+        float* zi = Zim + ch * NBL + kk;
+        float re[H], im[H];
+#pragma unroll
+        for (int y = 0; y < H; ++y) {
+            re[y] = zr[y * KW];
+            im[y] = zi[y * KW];
+        }
+        fft_reg<H, false>(re, im);
+#pragma unroll
+        for (int y = 0; y < H; ++y) {
+            zr[y * KW] = re[y] * a.norm;
+            zi[y * KW] = im[y] * a.norm;
+        }
+    }
+    __syncthreads();
+
+    // 3. mix (pre-split weight fragments, split-bf16 products) -> raw Y spill + tile statistics
+    const int MT = (C2 + 31) >> 5, QN = C >> 3;
+    float* ysb = a.yspill + (size_t)b * C2 * NB + GI * ZPL;
+    for (int tile = wave; tile < MT * NTL; tile += FU_THREADS / 64) {
+        const int mt = tile % MT, nt = tile / MT;
+        floatx16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+        const float* zp = (h ? Zim : Zre) + nt * 32 + col;
+        const uint16_t* w3 = (a.wm_lds ? reinterpret_cast<const uint16_t*>(Wm) : a.wmix3) +
+                             (size_t)mt * QN * 1536 + lane * 8;
+#pragma unroll 2
+        for (int q = 0; q < QN; ++q) {
+            Split3 av;
+            av.hi = *reinterpret_cast<const bf16x8*>(w3 + q * 1536);
+            av.mid = *reinterpret_cast<const bf16x8*>(w3 + q * 1536 + 512);
+            av.lo = *reinterpret_cast<const bf16x8*>(w3 + q * 1536 + 1024);
+            float zv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) zv[j] = zp[(8 * q + j) * NBL];
+            acc = mfma_split3(av, split3(zv), acc);
+        }
+        const int n = nt * 32 + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int o = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (n < NBL && o < C2) ysb[(size_t)o * NB + n] = acc[r];
+        }
+        const int nv = min(32, NBL - nt * 32);
+        float mean[2], m2[2];
+        tile_row_stats16(acc, nv, scr + wave * 16 * 33, mean, m2);
+        if ((lane & 3) == 0) {
+#pragma unroll
+            for (int R = 0; R < 2; ++R) {
+                const int o = mt * 32 + 16 * R + (lane >> 2);
+                if (o < C2) {
+                    float* s3 = st + (nt * C2 + o) * 3;
+                    s3[0] = (float)nv;
+                    s3[1] = mean[R];
+                    s3[2] = m2[R];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // 4. the tiles' partials of each channel (Chan et al., tile order) -> slab row GI B + b
+    for (int o = tid; o < C2; o += FU_THREADS) {
+        float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
+        for (int nt = 0; nt < NTL; ++nt) {
+            const float* s3 = st + (nt * C2 + o) * 3;
+            const float cn = s3[0], cm = s3[1], cq = s3[2];
+            const float tot = nn + cn;
+            const float delta = cm - mean;
+            mean += delta * (cn / tot);
+            m2 += cq + delta * delta * (nn * cn / tot);
+            nn = tot;
+        }
+        reinterpret_cast<float4*>(a.slab)[((size_t)GI * a.B + b) * C2 + o] = make_float4(nn, mean, m2, 0.0f);
+    }
+}
+
+template <int H, int W, int UP, int G>
+__global__ __launch_bounds__(FU_THREADS, 4) void fu_pass0_kg_kernel(FuArgs a) {   // 4 waves / SIMD: 2 WGs / CU
+    static_assert(G == 2, "two bin groups");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int C = a.C, tid = threadIdx.x;
+    const int g = blockIdx.x / a.B;
+    if (a.wm_lds) {
+        typedef __attribute__((address_space(1))) void* gptr_t;
+        typedef __attribute__((address_space(3))) void* lptr_t;
+        float* Wm = smem + 2 * C * (H * FuKg<W, G>::KW0);
+        const int n4 = (a.Mpad >> 5) * (C >> 3) * 192;   // 16-byte groups of the split pieces
+        for (int i0 = 0; i0 < n4; i0 += FU_THREADS) {
+            if (i0 + (tid & ~63) < n4) {
+                const int i = min(i0 + tid, n4 - 1);
+                __builtin_amdgcn_global_load_lds((gptr_t)(reinterpret_cast<const float*>(a.wmix3) + 4 * (size_t)i),
+                                                 (lptr_t)(Wm + 4 * (i0 + (tid & ~63))), 16, 0, 0);
+            }
+        }
+    }
+    if (a.has_in_fold)
+        ffc::bn_fold_block<FU_THREADS>(a.in_fold, smem + a.bn_off, smem + a.bn_off + C, blockIdx.x == 0,
+                                       reinterpret_cast<double*>(smem));
+    if (g == 0)
+        fu_kg_body<H, W, UP, G, 0>(a, smem);
+    else
+        fu_kg_body<H, W, UP, G, 1>(a, smem);
+}
+
 // Pass 1 from the spilled Y, split over channel groups: one wave per (sample, 64 / H channels).
 // fu_kernel's pass 1 runs a whole sample per 8-wave workgroup, one workgroup per CU at B = 256, so
 // its load / column-IFFT / row-C2R phases cannot overlap; pass 1 needs no cross-channel data (the
 // mix ran in pass 0), so here every wave takes 64 / H channels (64 rows, (64 / H) (W/2 + 1) column
 // lines) and many waves share a CU.  Same arithmetic per line as fu_kernel (bit-identical).
-template <int H, int W, int UP>
+template <int H, int W, int UP, int G>
 __global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
     constexpr int WP = W / 2 + 1;
     constexpr int NB = H * WP;
@@ -428,6 +674,15 @@ __global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
     __shared__ float fbn[2][2 * CPG];
     const float* bsc = a.bn_scale + 2 * c0;
     const float* bsh = a.bn_shift + 2 * c0;
+    // this lane's residual row (s = transform(t) of row tid), loaded first: its latency sits under
+    // the fold and the Y load instead of after the column IFFT
+    float sres[W];
+    if (a.residual) {
+        load_s_row<W, UP>(a, nullptr, b, c0 + tid / H, tid % H, H, sres);
+    } else {
+#pragma unroll
+        for (int x = 0; x < W; ++x) sres[x] = 0.0f;
+    }
     if (a.has_mix_fold) {
         // the FU's BN of this wave's 2 CPG spectral channels, folded here: 64 / (2 CPG) lanes per
         // channel (ffc::bn_fold_channels), sample 0's waves lead
@@ -450,9 +705,8 @@ __global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
         const int ol = (4 * i) / NB, n = 4 * i - ol * NB;
         const float4 v = ys[i];
         const float sc = bsc[ol], sh = bsh[ol];
-        float* dst = ((ol & 1) ? Yim : Yre) + (ol >> 1) * NB + n;
-        *reinterpret_cast<float4*>(dst) = make_float4(fmaxf(fmaf(v.x, sc, sh), 0.0f), fmaxf(fmaf(v.y, sc, sh), 0.0f),
-                                                      fmaxf(fmaf(v.z, sc, sh), 0.0f), fmaxf(fmaf(v.w, sc, sh), 0.0f));
+        float* dst = ((ol & 1) ? Yim : Yre) + (ol >> 1) * NB;
+        spill_to_plane<H, W, G>(dst, n, v, sc, sh);
     }
     __syncthreads();
     for (int q = tid; q < CPG * WP; q += 64) {   // inverse column C2C over H, ortho scale
@@ -477,26 +731,15 @@ __global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
         const int ch = tid / H, y = tid - ch * H;
         const float* yr = Yre + (ch * H + y) * WP;
         const float* yi = Yim + (ch * H + y) * WP;
-        float re[W], im[W];
-        re[0] = yr[0];
-        im[0] = 0.0f;
+        float xr[WP], xi[WP], re[W];
 #pragma unroll
-        for (int k = 1; k < W / 2; ++k) {
-            const float vr = yr[k], vi = yi[k];
-            re[k] = vr;
-            im[k] = vi;
-            re[W - k] = vr;
-            im[W - k] = -vi;
+        for (int k = 0; k < WP; ++k) {
+            xr[k] = yr[k];
+            xi[k] = yi[k];
         }
-        re[W / 2] = yr[W / 2];
-        im[W / 2] = 0.0f;
-        fft_reg<W, true>(re, im);
-        if (a.residual) {
-            float sres[W];
-            load_s_row<W, UP>(a, nullptr, b, c0 + ch, y, H, sres);
+        irfft_reg<W>(xr, xi, re);   // W/2-point complex inverse FFT (fft_common.h)
 #pragma unroll
-            for (int x = 0; x < W; ++x) re[x] += sres[x];
-        }
+        for (int x = 0; x < W; ++x) re[x] += sres[x];
         store_row<W>(a.out + ((size_t)(b * C + c0 + ch) * H + y) * W, re);
     }
 }
@@ -540,15 +783,52 @@ FuKernel pick_kernel(int H, int W, int up, int pass) {
 
 bool pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
 
-FuKernel pick_split(int H, int W, int up) {
-    if (H != W) return nullptr;
+template <int H, int W, int UP>
+FuKernel pick_split_g(int kgroups) {
+    return kgroups == 2 ? fu_pass1_split_kernel<H, W, UP, 2> : fu_pass1_split_kernel<H, W, UP, 1>;
+}
+FuKernel pick_split(int H, int W, int up, int kgroups) {
+    if (H != W || !(kgroups == 1 || kgroups == 2)) return nullptr;
     switch (H) {
-        case 8: return up == 1 ? fu_pass1_split_kernel<8, 8, 1> : fu_pass1_split_kernel<8, 8, 2>;
-        case 16: return up == 1 ? fu_pass1_split_kernel<16, 16, 1> : fu_pass1_split_kernel<16, 16, 2>;
-        case 32: return up == 1 ? fu_pass1_split_kernel<32, 32, 1> : fu_pass1_split_kernel<32, 32, 2>;
+        case 8: return up == 1 ? pick_split_g<8, 8, 1>(kgroups) : pick_split_g<8, 8, 2>(kgroups);
+        case 16: return up == 1 ? pick_split_g<16, 16, 1>(kgroups) : pick_split_g<16, 16, 2>(kgroups);
+        case 32: return up == 1 ? pick_split_g<32, 32, 1>(kgroups) : pick_split_g<32, 32, 2>(kgroups);
     }
     return nullptr;
 }
+// pass 0 over G = 2 bin groups (fu_pass0_kg_kernel): square 8^2 .. 32^2 planes, pre-split weights
+FuKernel pick_kg(int H, int W, int up) {
+    if (H != W) return nullptr;
+    switch (H) {
+        case 8: return up == 1 ? fu_pass0_kg_kernel<8, 8, 1, 2> : fu_pass0_kg_kernel<8, 8, 2, 2>;
+        case 16: return up == 1 ? fu_pass0_kg_kernel<16, 16, 1, 2> : fu_pass0_kg_kernel<16, 16, 2, 2>;
+        case 32: return up == 1 ? fu_pass0_kg_kernel<32, 32, 1, 2> : fu_pass0_kg_kernel<32, 32, 2, 2>;
+    }
+    return nullptr;
+}
+// LDS of fu_pass0_kg_kernel: Z (2 C H KW0), the split weight when wm (staged), tile statistics
+// (ceil(H KW0 / 32) x 2C x 3), the per-wave 16-row scratch, the folded input affine (2C)
+struct KgLayout {
+    size_t bytes;
+    int wm_lds, scr_off, bn_off;
+};
+KgLayout kg_layout(int C, int H, int W, int G, bool wm) {
+    const int WP = W / 2 + 1, KW0 = (WP + G - 1) / G, ZPL = H * KW0;
+    const size_t z = (size_t)2 * C * ZPL;
+    const size_t wfl = wm ? ((size_t)((2 * C + 31) / 32) * (C / 8) * 768 + 255) / 256 * 256 : 0;
+    const size_t stf = (size_t)((ZPL + 31) / 32) * 2 * C * 3;
+    const size_t floats = z + wfl + stf + FU_KG_SCRATCH + 2 * (size_t)C;
+    return {4 * floats, wm ? 1 : 0, (int)(z + wfl), (int)(z + wfl + stf + FU_KG_SCRATCH)};
+}
+// FFC_FU_KGROUPS: 1 = off (fu_kernel's pass 0, one workgroup or M-tile groups per sample), 2 = on
+int fu_kgroups_env() {
+    static const int v = [] {
+        const char* e = std::getenv("FFC_FU_KGROUPS");
+        return e ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
 // FFC_FU_MFMA=split: the fused mix on the split-bf16 products instead of the exact f32-input MFMA.
 // Off by default: measured neutral (gen64 B = 256 fu_pass0 51 vs 52 us per step, B = 32 the same,
 // r05f) -- the fused mix waits on its LDS operand reads and the per-tile statistics, not the MFMA
@@ -661,7 +941,20 @@ extern "C" int ffc_fu_pack_mix3(const float* wmixT, int C, uint16_t* wmix3, void
 static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
                            const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
                            float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
-                           const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream);
+                           const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, int kgroups,
+                           void* stream);
+
+extern "C" int ffc_fu_kgroups(int B, int C, int H, int W) {
+    const int env = fu_kgroups_env();
+    if (B <= 0 || C <= 0 || C % 8 != 0 || fu_mix_f32_forced() || env == 1 || H != W || !pick_kg(H, W, 1)) return 1;
+    if (kg_layout(C, H, W, 2, false).bytes > 80 * 1024) return 1;   // two workgroups per CU or not at all
+    return 2;
+}
+
+extern "C" int ffc_fu_slab_rows(int B, int C, int H, int W, int kgroups) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+    return B * (kgroups == 2 ? 2 : 1);
+}
 
 extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
                                  const float* in_shift, int in_relu, const float* wmixT, int pass, float* stats_slab,
@@ -669,7 +962,7 @@ extern "C" int ffc_fu_forward_ex(const float* t, int B, int C, int H, int W, int
                                  const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill,
                                  void* stream) {
     return fu_forward_impl(t, B, C, H, W, up, in_scale, in_shift, in_relu, wmixT, nullptr, pass, stats_slab, bn_scale,
-                           bn_shift, residual, out, in_fold, mix_fold, yspill, stream);
+                           bn_shift, residual, out, in_fold, mix_fold, yspill, 1, stream);
 }
 
 extern "C" int ffc_fu_forward_ex3(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
@@ -680,13 +973,31 @@ extern "C" int ffc_fu_forward_ex3(const float* t, int B, int C, int H, int W, in
     FFC_CHECK_ARG(!wmix3 || (C % 8 == 0 && (reinterpret_cast<uintptr_t>(wmix3) & 15) == 0),
                   "ffc_fu_forward_ex3: wmix3 needs C % 8 == 0 and 16-byte alignment");
     return fu_forward_impl(t, B, C, H, W, up, in_scale, in_shift, in_relu, wmixT, wmix3, pass, stats_slab, bn_scale,
-                           bn_shift, residual, out, in_fold, mix_fold, yspill, stream);
+                           bn_shift, residual, out, in_fold, mix_fold, yspill, 1, stream);
+}
+
+extern "C" int ffc_fu_forward_ex4(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                                  const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3,
+                                  int pass, float* stats_slab, const float* bn_scale, const float* bn_shift,
+                                  int residual, float* out, const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold,
+                                  float* yspill, int kgroups, void* stream) {
+    FFC_CHECK_ARG(kgroups == 1 || kgroups == 2, "ffc_fu_forward_ex4: kgroups must be 1 or 2");
+    FFC_CHECK_ARG(kgroups == 1 || ffc_fu_kgroups(B, C, H, W) == 2,
+                  "ffc_fu_forward_ex4: kgroups = 2 unsupported here (ffc_fu_kgroups)");
+    FFC_CHECK_ARG(kgroups == 1 || (wmix3 && (reinterpret_cast<uintptr_t>(wmix3) & 15) == 0),
+                  "ffc_fu_forward_ex4: kgroups = 2 needs the pre-split weight wmix3 (16-byte aligned)");
+    FFC_CHECK_ARG(kgroups == 1 || pass == 1 || yspill, "ffc_fu_forward_ex4: kgroups = 2 pass 0 needs yspill");
+    FFC_CHECK_ARG(!wmix3 || (C % 8 == 0 && (reinterpret_cast<uintptr_t>(wmix3) & 15) == 0),
+                  "ffc_fu_forward_ex4: wmix3 needs C % 8 == 0 and 16-byte alignment");
+    return fu_forward_impl(t, B, C, H, W, up, in_scale, in_shift, in_relu, wmixT, wmix3, pass, stats_slab, bn_scale,
+                           bn_shift, residual, out, in_fold, mix_fold, yspill, kgroups, stream);
 }
 
 static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
                            const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
                            float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
-                           const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream) {
+                           const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, int kgroups,
+                           void* stream) {
     FFC_CHECK_ARG(B > 0 && C > 0, "ffc_fu_forward: B and C must be positive");
     FFC_CHECK_ARG(up == 1 || up == 2, "ffc_fu_forward: up must be 1 or 2");
     FFC_CHECK_ARG(pass == 0 || pass == 1, "ffc_fu_forward: pass must be 0 or 1");
@@ -747,6 +1058,40 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
     // pass 0 of small batches over two workgroups per sample (M-tile groups) while the grid stays
     // within one workgroup per CU; FFC_FU_MGROUPS = 1 keeps one per sample, = 4 four (A/B)
     a.mgroups = 1;
+    a.B = B;
+    a.kgroups = kgroups;
+    if (pass == 0 && kgroups == 2) {
+        // pass 0 over two bin groups per sample (fu_pass0_kg_kernel): the split weight staged in LDS
+        // while two workgroups still fit a CU, else read from L2
+        FFC_CHECK_ARG(packed && yspill, "ffc_fu_forward: kgroups = 2 needs wmix3 and yspill");
+        KgLayout kl = kg_layout(C, H, W, 2, true);
+        if (kl.bytes > 80 * 1024) kl = kg_layout(C, H, W, 2, false);
+        FFC_CHECK_ARG(kl.bytes <= 80 * 1024, "ffc_fu_forward: kgroups = 2 layout exceeds 80 KiB");
+        FFC_CHECK_ARG(!in_fold || (size_t)kl.scr_off * 4 >= sizeof(double) * ffc::bn_fold_scratch_doubles(FU_THREADS),
+                      "ffc_fu_forward: bin-group planes too small for the in-kernel bn1 fold");
+        FuKernel kk = pick_kg(H, W, up);
+        FFC_CHECK_ARG(kk != nullptr, "ffc_fu_forward: no bin-group kernel instance");
+        a.wm_lds = kl.wm_lds;
+        a.w3_lds = kl.wm_lds;
+        a.scr_off = kl.scr_off;
+        a.bn_off = kl.bn_off;
+        if (kl.bytes > 64 * 1024) {
+            static std::mutex mu;
+            static std::set<const void*> raised;
+            std::lock_guard<std::mutex> g(mu);
+            if (!raised.count(reinterpret_cast<const void*>(kk))) {
+                hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kk),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                if (e != hipSuccess) {
+                    ffc::set_error(std::string("ffc_fu_forward: hipFuncSetAttribute: ") + hipGetErrorString(e));
+                    return FFC_E_LAUNCH;
+                }
+                raised.insert(reinterpret_cast<const void*>(kk));
+            }
+        }
+        hipLaunchKernelGGL(kk, dim3((unsigned)B * 2), dim3(FU_THREADS), kl.bytes, (hipStream_t)stream, a);
+        return ffc::launch_status("ffc_fu_forward");
+    }
     if (pass == 0) {
         static const int force = [] {
             const char* e = std::getenv("FFC_FU_MGROUPS");
@@ -787,7 +1132,7 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
     const bool chan_fold = mix_fold && mix_fold->momentum >= 0.0f && (2 * 64 / H) <= 64;
     if (pass == 1 && yspill && (!mix_fold || chan_fold) && fu_split_on() && H * W <= 64 * 64 && H <= 64 &&
         C % (64 / H) == 0) {
-        FuKernel ks = pick_split(H, W, up);
+        FuKernel ks = pick_split(H, W, up, kgroups);
         if (ks) {
             const size_t slds = (size_t)2 * (64 / H) * H * (W / 2 + 1) * sizeof(float);
             hipLaunchKernelGGL(ks, dim3((unsigned)B * (C / (64 / H))), dim3(64), slds, (hipStream_t)stream, a);

@@ -100,8 +100,13 @@ class FourierUnitSN(nn.Module):
         n_r = float(B * C * H * W)              # fused FU moves 4*N_r per read/write
         n_y = float(B * 2 * C * H * (W // 2 + 1))
         sc = sh = mix_fold = yspill = None
+        kg = 1
         if use_batch:
-            slab = torch.empty((B, 2 * C, 4), device=dev, dtype=torch.float32)
+            # pass 0 over two bin groups per sample where the library takes them (ffc_fu_kgroups: half
+            # the spectrum's columns per workgroup, two workgroups per CU); slab rows = B x groups
+            kg = L.ffc_fu_kgroups(B, C, H, W) if (rt.FU_KGROUPS and rt.FU_SPILL and mix3 is not None) else 1
+            rows = L.ffc_fu_slab_rows(B, C, H, W, kg)
+            slab = torch.empty((rows, 2 * C, 4), device=dev, dtype=torch.float32)
             # pass 0 keeps its mix output Y for pass 1 (no second row R2C + column FFT + mix)
             yspill = torch.empty(int(n_y), device=dev, dtype=torch.float32) if rt.FU_SPILL else None
             # bytes: SURVEY.md §8d's algorithmic basis (fused train FU = 12*N_r: x read in each pass,
@@ -109,21 +114,21 @@ class FourierUnitSN(nn.Module):
             # moved: what this kernel pair actually streams (including the Y spill written and read back)
             mv0 = 4.0 * t.numel() + (4.0 * n_y if rt.FU_SPILL else 0.0)
             with rt.observe("fu_pass0", bytes=min(4.0 * n_r, mv0), moved=mv0):
-                check(L.ffc_fu_forward_ex3(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
+                check(L.ffc_fu_forward_ex4(ptr(t), B, C, H, W, up, None if in_fold else ptr(in_scale),
                                            None if in_fold else ptr(in_shift), int(in_relu), ptr(mixT), ptr(mix3), 0,
                                            ptr(slab), None, None, 0, None,
                                            ctypes.byref(in_fold.struct) if in_fold else None, None, ptr(yspill),
-                                           stream), "ffc_fu_forward(pass 0)")
+                                           kg, stream), "ffc_fu_forward(pass 0)")
             if in_fold is not None:          # pass 0's workgroup 0 wrote the folded bn1 affine
                 in_scale, in_shift = in_fold.scale, in_fold.shift
             mix_fold = None
-            if yspill is not None and H == W and H in (8, 16, 32) and C % (64 // H) == 0:
+            if rt.FU_SPLIT and yspill is not None and H == W and H in (8, 16, 32) and C % (64 // H) == 0:
                 # the split pass 1 (one wave per 64 / H channels) folds its 2 * 64 / H channels itself
-                mix_fold = rt.bn_fold_channels(self.bn, 2 * C, slab, B, 1.0, dev, lanes=64 // (2 * 64 // H))
+                mix_fold = rt.bn_fold_channels(self.bn, 2 * C, slab, rows, 1.0, dev, lanes=64 // (2 * 64 // H))
             if mix_fold is None and self._fold_ok(C, H, W):
-                mix_fold = rt.bn_fold(self.bn, 2 * C, slab, B, 1.0, dev)
+                mix_fold = rt.bn_fold(self.bn, 2 * C, slab, rows, 1.0, dev)
             if mix_fold is None:
-                sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, B, 1.0, dev, stream)
+                sc, sh = rt.bn_scale_shift(self.bn, 2 * C, slab, rows, 1.0, dev, stream)
         else:
             if in_fold is not None:
                 in_scale, in_shift = in_fold.materialize(stream)
@@ -131,9 +136,9 @@ class FourierUnitSN(nn.Module):
         out = torch.empty((B, C, H, W), device=dev, dtype=torch.float32)
         mv1 = (4.0 * n_y if yspill is not None else 4.0 * t.numel()) + 4.0 * t.numel() * bool(residual) + 4.0 * n_r
         with rt.observe("fu_pass1", bytes=min(8.0 * n_r, mv1), moved=mv1):
-            check(L.ffc_fu_forward_ex3(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
+            check(L.ffc_fu_forward_ex4(ptr(t), B, C, H, W, up, ptr(in_scale), ptr(in_shift), int(in_relu), ptr(mixT),
                                        ptr(mix3), 1, None, ptr(sc), ptr(sh), int(residual), ptr(out), None,
-                                       ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), stream),
+                                       ctypes.byref(mix_fold.struct) if mix_fold else None, ptr(yspill), kg, stream),
                   "ffc_fu_forward(pass 1)")
         return out
 

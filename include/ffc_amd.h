@@ -439,6 +439,23 @@ int ffc_fu_forward_ex3(const float* t, int B, int C, int H, int W, int up, const
                        const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
                        float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
                        const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, void* stream);
+/* ffc_fu_forward_ex3 with pass 0 over `kgroups` (1 or 2) workgroups per sample, each holding only a
+ * range of the half-spectrum columns (round 6: the whole-spectrum LDS planes capped pass 0 at one
+ * workgroup per CU).  Same FourierUnitSN.forward (fourier_unity.py:32-56); kgroups = 2 needs wmix3,
+ * yspill and ffc_fu_kgroups(B, C, H, W) == 2, and changes two buffer contracts, so pass 0 and pass 1
+ * must be given the same value:
+ *   stats_slab has ffc_fu_slab_rows(B, C, H, W, kgroups) rows (row g B + b: sample b, group g; the
+ *              mix BN's fold / reduce merge them all);
+ *   yspill keeps B x 2C x H(W/2+1) floats, each channel's bins ordered [group][row][column in group]. */
+int ffc_fu_forward_ex4(const float* t, int B, int C, int H, int W, int up, const float* in_scale,
+                       const float* in_shift, int in_relu, const float* wmixT, const uint16_t* wmix3, int pass,
+                       float* stats_slab, const float* bn_scale, const float* bn_shift, int residual, float* out,
+                       const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, int kgroups,
+                       void* stream);
+/* the library's bin-group count for this fused FU (2 where the split layout fits two workgroups per
+ * CU and the pre-split mix applies; FFC_FU_KGROUPS=1 forces 1) and the pass-0 slab rows it implies */
+int ffc_fu_kgroups(int B, int C, int H, int W);
+int ffc_fu_slab_rows(int B, int C, int H, int W, int kgroups);
 /* wmixT (ffc_fu_pack_mix) -> its split bf16 pieces in MFMA fragment order: ffc_fu_mix3_elems(C) uint16
  * (16-byte aligned); 0 when C % 8 != 0 */
 size_t ffc_fu_mix3_elems(int C);

@@ -228,3 +228,57 @@ def test_staged_fu_repeat_bitwise(cin, cout, hw, B):
         outs.append(out[0])
     bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
     assert not bad, f"runs {bad} differ from run 0"
+
+
+# --------------------------------------------------------------------------- round 6: bin groups
+def _run_kg(st, xs, kg):
+    from fastfourierconvolution_amd import _runtime as rt
+    old = rt.FU_KGROUPS, rt.FU_PATH
+    rt.FU_KGROUPS, rt.FU_PATH = kg, "fused"
+    try:
+        with torch.no_grad():
+            outs = [st(x).clone() for x in xs]
+        torch.cuda.synchronize()
+    finally:
+        rt.FU_KGROUPS, rt.FU_PATH = old
+    return outs, {k: v.detach().clone() for k, v in st.state_dict().items()}
+
+
+@pytest.mark.parametrize("momentum", [0.1, None])
+@pytest.mark.parametrize("cin,cout,hw,B", [(256, 128, 4, 64), (128, 64, 8, 86), (64, 32, 16, 256),
+                                           (64, 64, 8, 7), (32, 32, 16, 5)])
+def test_bin_groups_match_one_workgroup_per_sample(momentum, cin, cout, hw, B):
+    """fused FU pass 0 over two bin groups (fu_pass0_kg_kernel: slab rows B x 2, bin-group spill
+    layout, real-input row FFTs on N/2-point complex FFTs) against one workgroup per sample:
+    SpectralTransform train forwards (gen64 ffc1-ffc3 shapes and odd batches), three steps"""
+    from fastfourierconvolution_amd import _runtime as rt
+    L = rt.lib()
+    base = _st(cin, cout, momentum, seed=cin + hw + B)
+    c = cout // 2
+    assert L.ffc_fu_kgroups(B, c, 2 * hw, 2 * hw) == 2
+    g = torch.Generator().manual_seed(hw + B)
+    xs = [torch.randn((B, cin, hw, hw), generator=g).cuda() for _ in range(3)]
+    ref_out, ref_sd = _run_kg(copy.deepcopy(base), xs, False)
+    out, sd = _run_kg(copy.deepcopy(base), xs, True)
+    for a, b in zip(out, ref_out):
+        err = normwise_err(a.double().cpu(), b.double().cpu())
+        assert err <= 2e-6, err
+    for k, v in ref_sd.items():
+        if k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(v), k
+        elif k.endswith("running_mean") or k.endswith("running_var"):
+            torch.testing.assert_close(sd[k], v, rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.parametrize("B", [64, 86, 256])
+def test_bin_groups_repeat_bitwise(B):
+    """the bin-group path repeated at the strong-scaling shard / full batch sizes: bitwise-equal
+    outputs and buffers (no cross-workgroup ordering left to chance)"""
+    base = _st(64, 32, 0.1, seed=B)
+    xs = [torch.randn((B, 64, 16, 16), generator=torch.Generator().manual_seed(B)).cuda()]
+    first, sd0 = _run_kg(copy.deepcopy(base), xs, True)
+    for _ in range(12):
+        o, sd = _run_kg(copy.deepcopy(base), xs, True)
+        assert torch.equal(o[0], first[0])
+        for k in sd0:
+            assert torch.equal(sd[k], sd0[k]), k

@@ -276,3 +276,39 @@ def test_threaded_replicas_bitwise_equal_serial():
     assert len(used) == 2, used.keys()
     insts = {ops.template(ops.layer_spec(m)).instances for m in reps[0].modules() if hasattr(m, "_ffc_ctor")}
     print(f"template instances per spec after the threaded run: {sorted(insts)}")
+
+
+def test_capture_takes_templates_last_used_by_another_thread():
+    """a pooled template last held by another thread (on its own stream) handed to a
+    thread that is capturing a hipGraph.  The hand-over must not wait on an event recorded outside
+    the capture (that invalidates it); the capture succeeds and the replay equals the other
+    thread's eager output."""
+    import threading
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import graphs
+    torch.manual_seed(21)
+    g = _quiet(F.FFCGenerator, 100, 3, 32).to(DEV).eval()
+    z = torch.randn(16, 100, 1, 1, device=DEV)
+    got, errors = [], []
+
+    def worker():
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s), torch.no_grad():
+                got.append(g(z).clone())
+            s.synchronize()
+        except Exception as e:   # reported by the main thread
+            errors.append(e)
+    th = threading.Thread(target=worker)
+    th.start()
+    th.join(timeout=120)
+    assert not errors, errors
+
+    def step():
+        with torch.no_grad():
+            return g(z)
+    graph = graphs.capture_step(step, warmup=0)   # the first take happens inside the capture
+    assert graph is not None, "capture failed"
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(graph.ffc_output, got[0])
