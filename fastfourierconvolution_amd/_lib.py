@@ -70,7 +70,7 @@ class BnFold(ctypes.Structure):
     _fields_ = [("slab", c_void_p), ("nrows", c_int), ("C", c_int), ("gamma", c_void_p), ("beta", c_void_p),
                 ("running_mean", c_void_p), ("running_var", c_void_p), ("num_batches_tracked", c_void_p),
                 ("update_running", c_int), ("momentum", c_float), ("eps", c_float), ("count_mult", c_float),
-                ("scale_out", c_void_p), ("shift_out", c_void_p)]
+                ("scale_out", c_void_p), ("shift_out", c_void_p), ("moments", c_void_p)]
 
 
 class InTf(ctypes.Structure):

@@ -294,9 +294,12 @@ class BnFoldDesc:
     """an ffc_bn_fold for ``bn`` over the partial rows ``slab`` plus the tensors it points at;
     scale / shift receive the folded affine (written by the consumer's workgroup 0)"""
 
-    def __init__(self, bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device):
+    def __init__(self, bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, moments=None):
         _, update = bn_mode(bn)
         self.slab = slab
+        # SyncBN: the slab's raw moments, reduced and all-reduced over the ranks already ([C][3] fp64,
+        # ffc_bn_fold.moments); the consumer finalizes from them
+        self.moments = moments
         self.channel_only = False   # made by bn_fold_channels: too many rows for a whole-slab fold
         self.scale = torch.empty(C, device=device, dtype=torch.float32)
         self.shift = torch.empty(C, device=device, dtype=torch.float32)
@@ -308,25 +311,61 @@ class BnFoldDesc:
             ptr(bn.running_mean) if update else None, ptr(bn.running_var) if update else None,
             ptr(bn.num_batches_tracked) if update else None, int(update),
             -1.0 if bn.momentum is None else float(bn.momentum), float(bn.eps), float(count_mult),
-            ptr(self.scale), ptr(self.shift))
+            ptr(self.scale), ptr(self.shift), ptr(moments) if moments is not None else None)
 
     def materialize(self, stream):
         """(scale, shift) by the separate reduce + finalize launch (consumers without a fold)"""
+        if self.moments is not None:   # SyncBN: only the finalize is left (the moments are merged)
+            bn, C = self.bn, self.struct.C
+            _, update = bn_mode(bn)
+            check(lib().ffc_bn_finalize(ptr(self.moments), C, ptr(bn.weight.detach()) if bn.weight is not None else None,
+                                        ptr(bn.bias.detach()) if bn.bias is not None else None,
+                                        ptr(bn.running_mean) if bn.running_mean is not None else None,
+                                        ptr(bn.running_var) if bn.running_var is not None else None,
+                                        ptr(bn.num_batches_tracked) if bn.num_batches_tracked is not None else None,
+                                        1, int(update), -1.0 if bn.momentum is None else float(bn.momentum),
+                                        float(bn.eps), float(self.struct.count_mult), ptr(self.scale),
+                                        ptr(self.shift), stream), "ffc_bn_finalize")
+            return self.scale, self.shift
         return bn_scale_shift(self.bn, self.struct.C, self.slab, self.struct.nrows, self.struct.count_mult,
                               self.scale.device, stream)
+
+
+def _bn_fold_synced(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, grp):
+    """SyncBN: the slab's raw moments by ffc_bn_reduce, all-reduced over ``grp``
+    (RCCL), handed to the consumer kernel as a moments fold -- its workgroups finalize in-kernel, so
+    the separate ffc_bn_finalize launch of the N > 1 path goes away"""
+    if bn.num_features != C:
+        raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
+    L = lib()
+    stream = torch.cuda.current_stream(device).cuda_stream
+    mbuf = torch.empty(3 * C + L.ffc_bn_reduce_ws_doubles(nrows, C), device=device, dtype=torch.float64)
+    from .distributed import merge_moments
+    with observe("bn_stats"):
+        check(L.ffc_bn_reduce(ptr(slab), nrows, C, ptr(mbuf), stream), "ffc_bn_reduce")
+        merge_moments(mbuf[:3 * C].view(C, 3), group=grp)
+    return BnFoldDesc(bn, C, slab, nrows, count_mult, device, moments=mbuf)
 
 
 def bn_fold(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device):
     """a BnFoldDesc when ``bn`` can be finalized inside its consumer (batch statistics, one rank),
     else None (use bn_scale_shift)"""
     use_batch, _ = bn_mode(bn)
-    if not (BN_FOLD and use_batch and slab is not None and _sync_group() is None):
+    if not (BN_FOLD and use_batch and slab is not None):
         return None
+    grp = _sync_group()
+    if grp is not None:
+        return _bn_fold_synced(bn, C, slab, nrows, count_mult, device, grp) if BN_FOLD_SYNC else None
     if nrows * C > BN_FOLD_MAX:   # every consumer workgroup merges all rows: only small slabs pay
         return None
     if bn.num_features != C:
         raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
     return BnFoldDesc(bn, C, slab, nrows, count_mult, device)
+
+
+# SyncBN: reduce + all-reduce the moments, then finalize inside the consumer (ffc_bn_fold.moments)
+# instead of a separate ffc_bn_finalize launch (FFC_BN_FOLD_SYNC=0: the old path, A/B)
+BN_FOLD_SYNC = __import__("os").environ.get("FFC_BN_FOLD_SYNC", "1") != "0"
 
 
 # Per-channel in-kernel folds (ffc::bn_fold_channels): consumers whose workgroups / waves need only
@@ -354,9 +393,16 @@ def bn_fold_channels(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: f
     BN_CHFOLD_READS slab rows read per channel over its ``consumers`` workgroups (at fgan128's
     B = 512 every 64^2 C2R plane workgroup re-read 1024 rows: C2R 798 -> 1046 us per step, r05l)"""
     use_batch, _ = bn_mode(bn)
-    if not (BN_FOLD and BN_CHFOLD and use_batch and slab is not None and _sync_group() is None):
+    if not (BN_FOLD and BN_CHFOLD and use_batch and slab is not None) or bn.momentum is None:
         return None
-    if bn.momentum is None or -(-nrows // lanes) > BN_CHFOLD_LOADS or nrows * max(1, consumers) > BN_CHFOLD_READS:
+    grp = _sync_group()
+    if grp is not None:   # moments: every consumer reads 3 doubles per channel, no row gating
+        if not BN_FOLD_SYNC:
+            return None
+        d = _bn_fold_synced(bn, C, slab, nrows, count_mult, device, grp)
+        d.channel_only = True
+        return d
+    if -(-nrows // lanes) > BN_CHFOLD_LOADS or nrows * max(1, consumers) > BN_CHFOLD_READS:
         return None
     if bn.num_features != C:
         raise RuntimeError(f"running_mean should contain {C} elements not {bn.num_features}")
@@ -539,11 +585,11 @@ class StreamPool:
         if last is not None and last[0] != me:
             cur = torch.cuda.current_stream()
             if torch.cuda.is_current_stream_capturing():
-                # a wait on an event recorded outside the capture would invalidate it:
-                # drain the previous holder's stream from the host instead (legal under the
-                # thread-local capture mode graphs.capture_step uses)
-                if last[1] != cur:
-                    last[1].synchronize()
+                # a wait on an event recorded outside the capture invalidates it, and so does a host
+                # synchronise from the capturing thread (measured r06d): nothing is done
+                # here -- graphs.capture_step synchronises the device before it captures, so the
+                # previous holder's kernels have retired
+                pass
             else:
                 cur.wait_stream(last[1])
         return obj
@@ -610,7 +656,7 @@ def plan_knobs():
     return (USE_PATCH, PW_KERNEL, CONV_ARITH, PRESPLIT_A, USE_CONVQ, CONVQ_FORCE, USE_OUTER, USE_SMALLM, FORCE_FU2D,
             FU_PATH, FU_FUSED_MIN_BATCH, FU_COLS, FU2D_SPILL, OVERLAP_SPECTRAL, BN_FOLD, BN_FOLD_MAX, FU_SPILL, ST_PATH,
             ST_SPLIT, ST_SPLIT_MAX, SE_SUMS, BN_CHFOLD, BN_CHFOLD_LOADS, BN_CHFOLD_READS, ST_SPLIT_MFMA, FU2D_R2CMIX,
-            FU_SPLIT, _plan.CONVQ_TCMAX, FU_KGROUPS)
+            FU_SPLIT, _plan.CONVQ_TCMAX, FU_KGROUPS, BN_FOLD_SYNC)
 
 
 def algorithmic_flops(plan) -> float:

@@ -21,10 +21,52 @@ __device__ __forceinline__ double shfl_xor_f64(double v, int m) { return __shfl_
 // read it) and stores scale_out / shift_out.  Ends with a barrier.  scratch: bn_fold_scratch().
 __host__ __device__ constexpr int bn_fold_scratch_doubles(int block) { return 3 * block / 4; }
 
+// finalize of channel o from its raw moments {N, S = sum x, Q = sum x^2} (fp64): nn.BatchNorm2d's
+// biased variance for the normalisation, unbiased over N * count_mult for running_var
+__device__ __forceinline__ void bn_fold_finalize(const ffc_bn_fold& f, int o, double N, double S, double Q,
+                                                 bool leader, int64_t nbt, float& scale, float& shift) {
+    const double mu = S / N;
+    double v = Q / N - mu * mu;
+    if (v < 0.0) v = 0.0;
+    const float mean = (float)mu, var = (float)v;
+    const float inv = 1.0f / sqrtf(var + f.eps);
+    const float g = f.gamma ? f.gamma[o] : 1.0f;
+    const float b = f.beta ? f.beta[o] : 0.0f;
+    scale = g * inv;
+    shift = fmaf(-mean, scale, b);   // as bn_se_kernels.hip finalize_channel
+    if (leader) {
+        if (f.update_running) {
+            float fm = f.momentum;
+            if (fm < 0.0f) fm = 1.0f / (float)(nbt + 1);   // momentum=None: cumulative average
+            const double nfull = N * (double)f.count_mult;
+            const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
+            f.running_mean[o] = fmaf(fm, mean, (1.0f - fm) * f.running_mean[o]);
+            f.running_var[o] = fmaf(fm, (float)unb, (1.0f - fm) * f.running_var[o]);
+        }
+        if (f.scale_out) f.scale_out[o] = scale;
+        if (f.shift_out) f.shift_out[o] = shift;
+    }
+}
+
 template <int BLOCK>
 __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool leader, double* scratch) {
     constexpr int NW = BLOCK / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (f.moments) {
+        // SyncBN: the slab was reduced and all-reduced across ranks already (distributed.py); each
+        // channel's finalize reads its three moments
+        const int64_t nbt0 = (leader && f.update_running && f.momentum < 0.0f) ? *f.num_batches_tracked : 0;
+        for (int o = tid; o < f.C; o += BLOCK) {
+            float scale, shift;
+            bn_fold_finalize(f, o, f.moments[3 * o], f.moments[3 * o + 1], f.moments[3 * o + 2], leader, nbt0, scale,
+                             shift);
+            sc[o] = scale;
+            sh[o] = shift;
+        }
+        __syncthreads();   // every channel read num_batches_tracked before the bump
+        if (leader && f.update_running && tid == 0) *f.num_batches_tracked += 1;
+        return;
+    }
     const int oc = lane & 15, rg = lane >> 4;
     const int nb = (f.C + 15) >> 4;                 // 16-channel blocks
     const int wpb = nb >= NW ? 1 : NW / nb;         // waves per block
@@ -83,29 +125,10 @@ __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool l
                     S += d[1];
                     Q += d[2];
                 }
-                const double mu = S / N;
-                double v = Q / N - mu * mu;
-                if (v < 0.0) v = 0.0;
-                const float mean = (float)mu, var = (float)v;
-                const float inv = 1.0f / sqrtf(var + f.eps);
-                const float g = f.gamma ? f.gamma[o2] : 1.0f;
-                const float b = f.beta ? f.beta[o2] : 0.0f;
-                const float scale = g * inv;
-                const float shift = fmaf(-mean, scale, b);   // as bn_se_kernels.hip finalize_channel
+                float scale, shift;
+                bn_fold_finalize(f, o2, N, S, Q, leader, nbt, scale, shift);
                 sc[o2] = scale;
                 sh[o2] = shift;
-                if (leader) {
-                    if (f.update_running) {
-                        float fm = f.momentum;
-                        if (fm < 0.0f) fm = 1.0f / (float)(nbt + 1);   // momentum=None: cumulative average
-                        const double nfull = N * (double)f.count_mult;
-                        const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
-                        f.running_mean[o2] = fmaf(fm, mean, (1.0f - fm) * f.running_mean[o2]);
-                        f.running_var[o2] = fmaf(fm, (float)unb, (1.0f - fm) * f.running_var[o2]);
-                    }
-                    if (f.scale_out) f.scale_out[o2] = scale;
-                    if (f.shift_out) f.shift_out[o2] = shift;
-                }
             }
         }
         __syncthreads();
@@ -168,6 +191,11 @@ __device__ inline void bn_fold_channels(const ffc_bn_fold& f, int o, bool leader
     // zero-count entry (a predicated load would compile to a branch and a wait per row)
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(f.slab, (unsigned long long)f.nrows * f.C * 16);
     double n = 0.0, s = 0.0, q = 0.0;
+    if (f.moments) {   // SyncBN: moments reduced and all-reduced already; every lane reads them
+        bn_fold_finalize(f, o, f.moments[3 * o], f.moments[3 * o + 1], f.moments[3 * o + 2], leader && gl == 0, 0,
+                         scale, shift);
+        return;
+    }
     // up to 8 rows per lane in flight per round: one memory round trip for <= 8 L rows (the usual case)
     for (int r0 = gl; r0 < f.nrows; r0 += 8 * L) {
         floatx4 e[8];
@@ -187,26 +215,7 @@ __device__ inline void bn_fold_channels(const ffc_bn_fold& f, int o, bool leader
     n = group_sum_f64<L>(n);
     s = group_sum_f64<L>(s);
     q = group_sum_f64<L>(q);
-    const double mu = s / n;
-    double v = q / n - mu * mu;
-    if (v < 0.0) v = 0.0;
-    const float mean = (float)mu, var = (float)v;
-    const float inv = 1.0f / sqrtf(var + f.eps);
-    const float g = f.gamma ? f.gamma[o] : 1.0f;
-    const float b = f.beta ? f.beta[o] : 0.0f;
-    scale = g * inv;
-    shift = fmaf(-mean, scale, b);
-    if (leader && gl == 0) {
-        if (f.update_running) {
-            const float fm = f.momentum;
-            const double nfull = n * (double)f.count_mult;
-            const double unb = nfull > 1.0 ? v * nfull / (nfull - 1.0) : v;
-            f.running_mean[o] = fmaf(fm, mean, (1.0f - fm) * f.running_mean[o]);
-            f.running_var[o] = fmaf(fm, (float)unb, (1.0f - fm) * f.running_var[o]);
-        }
-        if (f.scale_out) f.scale_out[o] = scale;
-        if (f.shift_out) f.shift_out[o] = shift;
-    }
+    bn_fold_finalize(f, o, n, s, q, leader && gl == 0, 0, scale, shift);   // momentum >= 0: nbt unused
 }
 
 // one whole wave per channel

@@ -1437,7 +1437,7 @@ extern "C" int ffc_fu2d_r2c(const float* t, int B, int C, int h, int w, const fl
 
 // a per-channel fold (ffc::bn_fold_channel): momentum >= 0 (no num_batches_tracked read), C channels
 static bool channel_fold_ok(const ffc_bn_fold* f, int C) {
-    return f->slab && f->nrows > 0 && f->C == C && (!f->update_running ||
+    return (f->moments || (f->slab && f->nrows > 0)) && f->C == C && (!f->update_running ||
            (f->running_mean && f->running_var && f->num_batches_tracked && f->momentum >= 0.0f));
 }
 

@@ -527,6 +527,7 @@ __device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
     const float* insc = smem + a.bn_off;                  // folded input affine: scale [C] | shift [C]
 
     // 1. row R2C of every (channel, row) on a W/2-point complex FFT (rfft_reg); this group's columns
+    FU_STAMP(1);
     for (int r = tid; r < C * H; r += FU_THREADS) {
         const int ch = r / H, y = r - ch * H;
         float sv[W], re[WP], im[WP];
@@ -544,6 +545,7 @@ __device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
     // copies landed before the barrier, so every wave may read Wm after it
     if (a.wm_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    FU_STAMP(2);
 
     // 2. column C2C over H of this group's columns, ortho scale
     for (int q = tid; q < C * KW; q += FU_THREADS) {
@@ -564,6 +566,7 @@ __device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
         }
     }
     __syncthreads();
+    FU_STAMP(3);
 
     // 3. mix (pre-split weight fragments, split-bf16 products) -> raw Y spill + tile statistics
     const int MT = (C2 + 31) >> 5, QN = C >> 3;
@@ -610,6 +613,7 @@ __device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
         }
     }
     __syncthreads();
+    FU_STAMP(4);
     // 4. the tiles' partials of each channel (Chan et al., tile order) -> slab row GI B + b
     for (int o = tid; o < C2; o += FU_THREADS) {
         float nn = 0.0f, mean = 0.0f, m2 = 0.0f;
@@ -624,6 +628,11 @@ __device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
         }
         reinterpret_cast<float4*>(a.slab)[((size_t)GI * a.B + b) * C2 + o] = make_float4(nn, mean, m2, 0.0f);
     }
+#ifdef FFC_TRACE
+    __syncthreads();
+    FU_STAMP(5);
+    if (tid == 0) g_fu_trace[8 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 template <int H, int W, int UP, int G>
@@ -632,6 +641,10 @@ __global__ __launch_bounds__(FU_THREADS, 4) void fu_pass0_kg_kernel(FuArgs a) { 
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int C = a.C, tid = threadIdx.x;
     const int g = blockIdx.x / a.B;
+#ifdef FFC_TRACE
+    if (tid == 0) g_fu_trace[8 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+    FU_STAMP(0);
     if (a.wm_lds) {
         typedef __attribute__((address_space(1))) void* gptr_t;
         typedef __attribute__((address_space(3))) void* lptr_t;
@@ -1015,12 +1028,12 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
                   "ffc_fu_forward: in_fold is pass 0 only, replaces in_scale/in_shift and needs scale_out/shift_out");
     FFC_CHECK_ARG(!mix_fold || pass == 1, "ffc_fu_forward: mix_fold is pass 1 only");
     for (const ffc_bn_fold* f : {in_fold, mix_fold})
-        FFC_CHECK_ARG(!f || (f->slab && f->nrows > 0 &&
+        FFC_CHECK_ARG(!f || ((f->moments || (f->slab && f->nrows > 0)) &&
                              (!f->update_running || (f->running_mean && f->running_var && f->num_batches_tracked))),
                       "ffc_fu_forward: incomplete ffc_bn_fold");
     FFC_CHECK_ARG(!in_fold || in_fold->C == C, "ffc_fu_forward: in_fold->C != C");
     FFC_CHECK_ARG(!mix_fold || mix_fold->C == 2 * C, "ffc_fu_forward: mix_fold->C != 2C");
-    FFC_CHECK_ARG((!in_fold && !mix_fold) ||
+    FFC_CHECK_ARG(((!in_fold || in_fold->moments) && (!mix_fold || mix_fold->moments)) ||
                       (size_t)16 * C * H * (W / 2 + 1) >= sizeof(double) * ffc::bn_fold_scratch_doubles(FU_THREADS),
                   "ffc_fu_forward: plane too small for an in-kernel BN fold (use bn_scale / in_scale)");
     FuKernel k = pick_kernel(H, W, up, pass);
@@ -1067,7 +1080,7 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
         KgLayout kl = kg_layout(C, H, W, 2, true);
         if (kl.bytes > 80 * 1024) kl = kg_layout(C, H, W, 2, false);
         FFC_CHECK_ARG(kl.bytes <= 80 * 1024, "ffc_fu_forward: kgroups = 2 layout exceeds 80 KiB");
-        FFC_CHECK_ARG(!in_fold || (size_t)kl.scr_off * 4 >= sizeof(double) * ffc::bn_fold_scratch_doubles(FU_THREADS),
+        FFC_CHECK_ARG(!in_fold || in_fold->moments || (size_t)kl.scr_off * 4 >= sizeof(double) * ffc::bn_fold_scratch_doubles(FU_THREADS),
                       "ffc_fu_forward: bin-group planes too small for the in-kernel bn1 fold");
         FuKernel kk = pick_kg(H, W, up);
         FFC_CHECK_ARG(kk != nullptr, "ffc_fu_forward: no bin-group kernel instance");

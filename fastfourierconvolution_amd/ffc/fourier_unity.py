@@ -83,7 +83,8 @@ class FourierUnitSN(nn.Module):
             fused = False
         if fused and staged_ok and (rt.FU_PATH == "staged" or (rt.FU_PATH == "auto" and B < rt.FU_FUSED_MIN_BATCH)):
             fused = False
-        if in_fold is not None and fused and (in_fold.channel_only or not self._fold_ok(C, H, W)):
+        if in_fold is not None and fused and in_fold.moments is None and (in_fold.channel_only or
+                                                                          not self._fold_ok(C, H, W)):
             in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
             in_fold = None
         if not fused:
@@ -158,8 +159,11 @@ class FourierUnitSN(nn.Module):
         workgroup, when that fold applies (rt.bn_fold_channels), else by its own launch"""
         B, C, h, w = t.shape
         if in_fold is not None:
-            chf = rt.bn_fold_channels(in_fold.bn, C, in_fold.slab, in_fold.struct.nrows, in_fold.struct.count_mult,
-                                      t.device, consumers=B)
+            if in_fold.moments is not None:   # SyncBN: already merged over the ranks; per-channel needs momentum
+                chf = in_fold if in_fold.bn.momentum is not None else None
+            else:
+                chf = rt.bn_fold_channels(in_fold.bn, C, in_fold.slab, in_fold.struct.nrows,
+                                          in_fold.struct.count_mult, t.device, consumers=B)
             if chf is None:
                 in_scale, in_shift = in_fold.materialize(rt.stream_of(t))
                 in_fold = None

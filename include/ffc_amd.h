@@ -418,6 +418,10 @@ typedef struct ffc_bn_fold {
     float momentum, eps, count_mult;
     float* scale_out;
     float* shift_out;
+    /* SyncBN (round 6): when non-NULL, [C][3] fp64 raw moments {n, sum x, sum x^2} already merged
+     * over the ranks (ffc_bn_reduce + an all-reduce); slab / nrows are then unused and every
+     * consumer workgroup finalizes from these instead of merging partial rows */
+    const double* moments;
 } ffc_bn_fold;
 
 /* ffc_fu_forward with the BNs folded in and pass 1 fed from pass 0 (no recompute):

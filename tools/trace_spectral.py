@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 
 PHASES = {
     "fu0": ["rows R2C", "col FFT", "mix+stats", "-", "merge+slab"],
+    "fu0kg": ["bn1 fold", "rows R2C", "col FFT", "mix+stats", "merge+slab"],
     "fu1": ["rows R2C", "col FFT", "mix+BN/ReLU", "inv col FFT", "rows C2R+store"],
     "st": ["load x (+w)", "SE gate", "conv1 MFMA", "slab merge"],
 }
@@ -44,15 +45,15 @@ def main():
     for f in (rfu, rst):
         f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     recs = []
-    ofu, ost = L.ffc_fu_forward_ex, L.ffc_st_prologue_ex3
+    ofu, ost = L.ffc_fu_forward_ex4, L.ffc_st_prologue_ex3
 
-    def fu(*a):
+    def fu(*a):   # ffc_fu_forward_ex4: pass a[11], kgroups a[19]
         rc = ofu(*a)
         torch.cuda.synchronize()
-        B = a[1]
-        buf = np.zeros((B, 8), dtype=np.uint64)
+        kg = a[19] if a[11] == 0 else 1
+        buf = np.zeros((a[1] * kg, 8), dtype=np.uint64)
         assert rfu(buf.ctypes.data, buf.nbytes) == 0
-        recs.append((f"fu{a[10]}", f"C={a[2]} {a[3]}x{a[4]} up={a[5]}", buf))
+        recs.append((f"fu{a[11]}" + ("kg" if kg > 1 else ""), f"C={a[2]} {a[3]}x{a[4]} up={a[5]}", buf))
         return rc
 
     def st(*a):
@@ -64,10 +65,10 @@ def main():
         recs.append(("st", f"Cin={a[2]} {a[3]}x{a[4]} c={a[11]} split={a[12]}", buf))
         return rc
 
-    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex3 = fu, st
+    L.ffc_fu_forward_ex4, L.ffc_st_prologue_ex3 = fu, st
     with torch.no_grad():
         G(z)
-    L.ffc_fu_forward_ex, L.ffc_st_prologue_ex3 = ofu, ost
+    L.ffc_fu_forward_ex4, L.ffc_st_prologue_ex3 = ofu, ost
     for kind, desc, buf in recs:
         rt0, rt1 = buf[:, 0].astype(np.float64), buf[:, 1].astype(np.float64)
         dur = (rt1 - rt0) / 100.0
