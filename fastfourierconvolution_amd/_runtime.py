@@ -381,8 +381,9 @@ BN_CHFOLD_READS = int(__import__("os").environ.get("FFC_BN_CHFOLD_READS", "16384
 # (the split pass 1's) must not reach it
 FU_SPLIT = __import__("os").environ.get("FFC_FU_SPLIT", "1")[:1] != "0"
 # fused FU pass 0 over two bin groups per sample where the library takes them (ffc_fu_kgroups, round
-# 6); FFC_FU_KGROUPS=1 (read by the library too) or FU_KGROUPS = False keeps one workgroup per sample
-FU_KGROUPS = __import__("os").environ.get("FFC_FU_KGROUPS", "2")[:1] != "1"
+# 6; off unless FFC_FU_KGROUPS=2, which the library reads too -- measured neutral to slower);
+# FU_KGROUPS = False keeps one workgroup per sample even then
+FU_KGROUPS = True
 
 
 def bn_fold_channels(bn: nn.BatchNorm2d, C: int, slab, nrows: int, count_mult: float, device, lanes: int = 64,

@@ -202,7 +202,13 @@ __device__ inline void bn_fold_channels(const ffc_bn_fold& f, int o, bool leader
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int r = r0 + L * u;
+#ifdef FFC_FOLD_PLAIN_LOADS   // DESIGN 10c probe: plain global loads instead of the buffer descriptor
+            const float4 pv = r < f.nrows ? reinterpret_cast<const float4*>(f.slab)[(size_t)r * f.C + o]
+                                          : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            e[u] = floatx4{pv.x, pv.y, pv.z, pv.w};
+#else
             e[u] = buf_ld4(rs, r < f.nrows ? (unsigned)((r * f.C + o) * 16) : OOB);
+#endif
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {

@@ -921,6 +921,34 @@ struct R2cMixLds {
     static constexpr int FLOATS = WM + SCR + TL + R + 2 * CC;
 };
 
+#ifdef FFC_R2CMIX_DUMP   // DESIGN 10c probe build: Tl after the row FFTs (slot 0) and at the end (slot 1)
+__device__ float g_r2cmix_dump[512 * 2 * 4608];
+#endif
+#if defined(FFC_R2CMIX_DBG) || defined(FFC_R2CMIX_DBGEND)
+// DESIGN 10c probe build: per workgroup, per channel: bn1 scale, shift, sum R, sum |T| after the row
+// FFTs, sum |T| after the column FFTs (thread ch sums its channel in a fixed order)
+__device__ float g_r2cmix_dbg[4096 * 5 * 32];
+#define R2CMIX_DBG(slot, expr_of_ch)                                                        \
+    do {                                                                                    \
+        __syncthreads();                                                                    \
+        if (tid < C) {                                                                      \
+            const int ch = tid;                                                             \
+            g_r2cmix_dbg[((size_t)blockIdx.x * 5 + (slot)) * 32 + ch] = (expr_of_ch);       \
+        }                                                                                   \
+        __syncthreads();                                                                    \
+    } while (0)
+template <int N>
+__device__ float dbg_sum(const float* p, int stride) {
+    float s = 0.0f;
+    for (int i = 0; i < N; ++i) s += fabsf(p[i * stride]);
+    return s;
+}
+#endif
+#ifndef FFC_R2CMIX_DBG
+#undef R2CMIX_DBG
+#define R2CMIX_DBG(slot, e) do { } while (0)
+#endif
+
 template <int MT, int CC, int HT>
 __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra) {
     using LY = R2cMixLds<HT, CC>;
@@ -944,9 +972,19 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
     // 1. the sample's t planes (registers) and the mix weight (LDS-DMA), all in flight
     constexpr int NV = C * HT * HT / 4 / FU2_THREADS;
     const float4* src = reinterpret_cast<const float4*>(ra.t + (size_t)b * C * HT * HT);
+#if defined(FFC_R2CMIX_ZERO_LDS) || defined(FFC_R2CMIX_ZERO_SCR)   // DESIGN 10c probes
+#ifdef FFC_R2CMIX_ZERO_LDS
+    for (int i = tid; i < LY::FLOATS; i += FU2_THREADS) smem[i] = 0.0f;
+#else
+    for (int i = tid; i < LY::SCR; i += FU2_THREADS) scr[i] = 0.0f;
+#endif
+    __syncthreads();
+#endif
     float4 v[NV];
+#ifndef FFC_R2CMIX_LATE_T
 #pragma unroll
     for (int j = 0; j < NV; ++j) v[j] = src[j * FU2_THREADS + tid];
+#endif
     ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
     // 2. bn1 (under the loads' latency): the whole-slab fold, scratch in the (not yet used) tile-stats
     //    area.  The per-channel fold (ffc::bn_fold_channels, as in the staged r2c) was measured
@@ -982,6 +1020,10 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
         fss[C + tid] = ra.in_scale ? ra.in_shift[tid] : 0.0f;
     }
     __syncthreads();
+#ifdef FFC_R2CMIX_LATE_T
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = src[j * FU2_THREADS + tid];
+#endif
     // 3. s0 = relu(t * scale + shift) -> R
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -996,6 +1038,12 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
         reinterpret_cast<float4*>(R)[i] = q;
     }
     __syncthreads();
+    R2CMIX_DBG(0, fss[ch]);
+    R2CMIX_DBG(1, fss[C + ch]);
+    R2CMIX_DBG(2, (dbg_sum<HT * HT>(R + ch * HT * HT, 1)));
+#if FFC_R2CMIX_XB == 3   // DESIGN 10c probes: one extra barrier after step 3 / 4 / 5
+    __syncthreads();
+#endif
     // 4. row FFTs (row r = channel * HT + y), bins 0..HT/2 -> Tl[r * WPt + k]
     for (int r = tid; r < C * HT; r += FU2_THREADS) {
         float re[HT], im[HT];
@@ -1014,6 +1062,15 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
         for (int k = 0; k < WPt; ++k) Tl[r * WPt + k] = make_float2(re[k], im[k]);
     }
     __syncthreads();
+    R2CMIX_DBG(3, (dbg_sum<2 * PT>(reinterpret_cast<const float*>(Tl + ch * PT), 1)));
+#ifdef FFC_R2CMIX_DUMP
+    if (blockIdx.x < 512 && LY::TL <= 4608)
+        for (int i = tid; i < LY::TL; i += FU2_THREADS)
+            g_r2cmix_dump[((size_t)blockIdx.x * 2) * 4608 + i] = reinterpret_cast<const float*>(Tl)[i];
+#endif
+#if FFC_R2CMIX_XB == 4
+    __syncthreads();
+#endif
     // 5. column FFTs (line l = channel * WPt + k)
     for (int l = tid; l < C * WPt; l += FU2_THREADS) {
         const int ch = l / WPt, k = l - ch * WPt;
@@ -1030,6 +1087,10 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
         for (int y = 0; y < HT; ++y) cp[y * WPt] = make_float2(re[y], im[y]);
     }
     __syncthreads();
+    R2CMIX_DBG(4, (dbg_sum<2 * PT>(reinterpret_cast<const float*>(Tl + ch * PT), 1)));
+#if FFC_R2CMIX_XB == 5
+    __syncthreads();
+#endif
 
     // 6. mix pass 0 on T in LDS: raw Y spill + BN partials (as fu2d_mix_kernel<MT, 0, CC>)
     MixA<MT, CC, false> A;
@@ -1087,7 +1148,27 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
             }
         }
         reinterpret_cast<float4*>(a.slab)[(size_t)blockIdx.x * C2 + o] = make_float4(nn, mean, m2, 0.0f);
+#ifdef FFC_R2CMIX_DBGEND   // DESIGN 10c probe: the workgroup's stage checksums, taken at its very end
+        g_r2cmix_dbg[((size_t)blockIdx.x * 5 + 3) * 32 + o] = m2;
+#endif
     }
+#ifdef FFC_R2CMIX_DUMP
+    __syncthreads();
+    if (blockIdx.x < 512 && LY::TL <= 4608)
+        for (int i = tid; i < LY::TL; i += FU2_THREADS)
+            g_r2cmix_dump[((size_t)blockIdx.x * 2 + 1) * 4608 + i] = reinterpret_cast<const float*>(Tl)[i];
+#endif
+#ifdef FFC_R2CMIX_DBGEND
+    __syncthreads();
+    if (tid < C) {
+        const int ch = tid;
+        g_r2cmix_dbg[((size_t)blockIdx.x * 5 + 0) * 32 + ch] = fss[ch];
+        g_r2cmix_dbg[((size_t)blockIdx.x * 5 + 1) * 32 + ch] = fss[C + ch];
+        g_r2cmix_dbg[((size_t)blockIdx.x * 5 + 2) * 32 + ch] = dbg_sum<HT * HT>(R + ch * HT * HT, 1);
+        g_r2cmix_dbg[((size_t)blockIdx.x * 5 + 4) * 32 + ch] =
+            dbg_sum<2 * PT>(reinterpret_cast<const float*>(Tl + ch * PT), 1);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- pass 1 + inverse column FFT
@@ -1507,6 +1588,17 @@ R2cMixKernel pick_r2c_mix(int C, int h, size_t& lds) {
     return nullptr;
 }
 }  // namespace
+
+#ifdef FFC_R2CMIX_DUMP
+extern "C" int ffc_debug_r2cmix_dump(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_r2cmix_dump), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+#if defined(FFC_R2CMIX_DBG) || defined(FFC_R2CMIX_DBGEND)
+extern "C" int ffc_debug_r2cmix_read(void* dst, size_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_r2cmix_dbg), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int ffc_fu2d_r2c_mix_supported(int C, int H, int W, int up) {
     size_t lds = 0;

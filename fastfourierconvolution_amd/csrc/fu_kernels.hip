@@ -244,14 +244,12 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         __syncthreads();
     } else {
 
-    // 1. row R2C (real W-point FFT per (channel,row)), input transform fused
+    // 1. row R2C (real W-point FFT per (channel,row) on a W/2-point complex FFT), input transform fused
     for (int r = tid; r < C * H; r += FU_THREADS) {
         const int ch = r / H, y = r - ch * H;
-        float re[W], im[W];
-        load_s_row<W, UP>(a, insc, b, ch, y, H, re);
-#pragma unroll
-        for (int x = 0; x < W; ++x) im[x] = 0.0f;
-        fft_reg<W, false>(re, im);
+        float sv[W], re[WP], im[WP];
+        load_s_row<W, UP>(a, insc, b, ch, y, H, sv);
+        rfft_reg<W>(sv, re, im);
         float* zr = Zre + (ch * H + y) * WP;
         float* zi = Zim + (ch * H + y) * WP;
 #pragma unroll
@@ -423,20 +421,13 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
             const int ch = r / H, y = r - ch * H;
             const float* yr = Yre + (ch * H + y) * WP;
             const float* yi = Yim + (ch * H + y) * WP;
-            float re[W], im[W];
-            re[0] = yr[0];
-            im[0] = 0.0f;
+            float xr[WP], xi[WP], re[W];
 #pragma unroll
-            for (int k = 1; k < W / 2; ++k) {
-                const float vr = yr[k], vi = yi[k];
-                re[k] = vr;
-                im[k] = vi;
-                re[W - k] = vr;
-                im[W - k] = -vi;
+            for (int k = 0; k < WP; ++k) {
+                xr[k] = yr[k];
+                xi[k] = yi[k];
             }
-            re[W / 2] = yr[W / 2];
-            im[W / 2] = 0.0f;
-            fft_reg<W, true>(re, im);
+            irfft_reg<W>(xr, xi, re);   // W/2-point complex inverse FFT (fft_common.h)
             if (a.residual) {
                 float s[W];
                 load_s_row<W, UP>(a, insc, b, ch, y, H, s);
@@ -833,7 +824,7 @@ KgLayout kg_layout(int C, int H, int W, int G, bool wm) {
     const size_t floats = z + wfl + stf + FU_KG_SCRATCH + 2 * (size_t)C;
     return {4 * floats, wm ? 1 : 0, (int)(z + wfl), (int)(z + wfl + stf + FU_KG_SCRATCH)};
 }
-// FFC_FU_KGROUPS: 1 = off (fu_kernel's pass 0, one workgroup or M-tile groups per sample), 2 = on
+// FFC_FU_KGROUPS: 2 = on, anything else off (fu_kernel's pass 0, one workgroup or M-tile groups per sample)
 int fu_kgroups_env() {
     static const int v = [] {
         const char* e = std::getenv("FFC_FU_KGROUPS");
@@ -957,9 +948,12 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
                            const ffc_bn_fold* in_fold, const ffc_bn_fold* mix_fold, float* yspill, int kgroups,
                            void* stream);
 
+// Off by default (FFC_FU_KGROUPS=2 turns it on): measured on MI355X (r06c / r06e, same-box A/B) the
+// bin-group pass 0 is 0-1 us faster per layer at B = 256 and 64, and its doubled slab rows cost the
+// per-channel fold of ffc3's mix BN at B = 256 (a finalize launch more): gen64 0.4286 -> 0.4309 ms.
 extern "C" int ffc_fu_kgroups(int B, int C, int H, int W) {
     const int env = fu_kgroups_env();
-    if (B <= 0 || C <= 0 || C % 8 != 0 || fu_mix_f32_forced() || env == 1 || H != W || !pick_kg(H, W, 1)) return 1;
+    if (B <= 0 || C <= 0 || C % 8 != 0 || fu_mix_f32_forced() || env != 2 || H != W || !pick_kg(H, W, 1)) return 1;
     if (kg_layout(C, H, W, 2, false).bytes > 80 * 1024) return 1;   // two workgroups per CU or not at all
     return 2;
 }
