@@ -373,7 +373,11 @@ BN_FOLD_SYNC = __import__("os").environ.get("FFC_BN_FOLD_SYNC", "1") != "0"
 # those channels' slab rows -- cheap at any channel count, so the limit is the rows a lane merges.
 # FFC_BN_CHFOLD=0 restores the separate finalize launches (A/B); FFC_BN_CHFOLD_LOADS: max slab rows
 # per lane.
-BN_CHFOLD = __import__("os").environ.get("FFC_BN_CHFOLD", "1") != "0"
+# Off by default since round 6 (FFC_BN_CHFOLD=1 turns it on): the same fold placed inside
+# ffc_fu2d_r2c_mix was reproduced non-deterministic in round 6 (T of whole channels
+# wrong in co-resident workgroups, 39 of 40 repeated forwards) and its mechanism is not isolated, so
+# the single-rank path finalizes these BNs by their own launch (B = 32: +3 %, B = 256: neutral, r05c)
+BN_CHFOLD = __import__("os").environ.get("FFC_BN_CHFOLD", "0") == "1"
 BN_CHFOLD_LOADS = int(__import__("os").environ.get("FFC_BN_CHFOLD_LOADS", "16"))
 BN_CHFOLD_READS = int(__import__("os").environ.get("FFC_BN_CHFOLD_READS", "16384"))
 # mirrors fu_kernels.hip fu_split_on(): FFC_FU_SPLIT=0 runs the fused FU's pass 1 as one workgroup per

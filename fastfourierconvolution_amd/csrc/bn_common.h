@@ -221,6 +221,10 @@ __device__ inline void bn_fold_channels(const ffc_bn_fold& f, int o, bool leader
     n = group_sum_f64<L>(n);
     s = group_sum_f64<L>(s);
     q = group_sum_f64<L>(q);
+#ifdef FFC_FOLD_FIN1   // DESIGN 10c probe: the fp64 finalize in lane 0 of each group only (others: 0)
+    scale = shift = 0.0f;
+    if (gl == 0)
+#endif
     bn_fold_finalize(f, o, n, s, q, leader && gl == 0, 0, scale, shift);   // momentum >= 0: nbt unused
 }
 

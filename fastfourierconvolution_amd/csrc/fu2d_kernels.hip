@@ -985,7 +985,12 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
 #pragma unroll
     for (int j = 0; j < NV; ++j) v[j] = src[j * FU2_THREADS + tid];
 #endif
+#ifdef FFC_R2CMIX_NODMA   // DESIGN 10c probe: the mix weight through registers instead of LDS-DMA
+    for (int i = tid; i < (C2 * a.Mpad) >> 2; i += FU2_THREADS)
+        reinterpret_cast<float4*>(Wm)[i] = reinterpret_cast<const float4*>(a.wmixT)[i];
+#else
     ffc::dma_copy16(a.wmixT, Wm, (C2 * a.Mpad) >> 2, tid, FU2_THREADS);
+#endif
     // 2. bn1 (under the loads' latency): the whole-slab fold, scratch in the (not yet used) tile-stats
     //    area.  The per-channel fold (ffc::bn_fold_channels, as in the staged r2c) was measured
     //    non-deterministic here -- T of two channels wrong in a few workgroups per launch (r05i,
@@ -998,7 +1003,13 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
 #ifdef FFC_R2CMIX_PREBAR
         __syncthreads();
 #endif
+#ifdef FFC_R2CMIX_WAVE0   // DESIGN 10c probe: wave 0 alone folds (64 / C lanes per channel)
+        constexpr int L = 64 / C;
+        if (tid < 64) {
+#else
         constexpr int L = FU2_THREADS / C;
+        {
+#endif
         float s_, h_;
         const int o = tid / L;
 #ifdef FFC_R2CMIX_NOLEAD
@@ -1012,6 +1023,10 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
             fss[C + o] = h_;
         }
         if (lead && tid == 0 && ra.fold.update_running) *ra.fold.num_batches_tracked += 1;
+        }
+#ifdef FFC_R2CMIX_NOP
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
 #else
         ffc::bn_fold_block<FU2_THREADS>(ra.fold, fss, fss + C, blockIdx.x == 0, reinterpret_cast<double*>(scr));
 #endif
@@ -1067,6 +1082,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
     if (blockIdx.x < 512 && LY::TL <= 4608)
         for (int i = tid; i < LY::TL; i += FU2_THREADS)
             g_r2cmix_dump[((size_t)blockIdx.x * 2) * 4608 + i] = reinterpret_cast<const float*>(Tl)[i];
+    __syncthreads();   // every wave's dump reads precede the column pass's writes
 #endif
 #if FFC_R2CMIX_XB == 4
     __syncthreads();
@@ -1617,6 +1633,9 @@ extern "C" int ffc_fu2d_r2c_mix(const float* t, int B, int C, int H, int W, int 
                   "scale_out / shift_out");
     size_t lds = 0;
     R2cMixKernel k = pick_r2c_mix(C, H / up, lds);
+#ifdef FFC_R2CMIX_ONEWG   // DESIGN 10c probe: a dynamic LDS request that admits one workgroup per CU
+    lds = 90 * 1024;
+#endif
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c_mix");
     if (rc) return rc;
     R2cMixArgs ra;

@@ -213,21 +213,29 @@ def test_r2c_mix_matches_separate_launches(chfold, cin, cout, hw, B):
             torch.testing.assert_close(sd[k], v, rtol=1e-6, atol=1e-7, msg=k)
 
 
-@pytest.mark.parametrize("cin,cout,hw,B", [(64, 32, 16, 64), (64, 32, 16, 86), (128, 64, 8, 86)])
-def test_staged_fu_repeat_bitwise(cin, cout, hw, B):
-    """the staged Fourier unit at the strong-scaling shard sizes, twelve fresh train forwards of one
-    SpectralTransform on one input: bitwise equal outputs (r05i: a per-channel bn1 fold inside
-    ffc_fu2d_r2c_mix corrupted T of two channels in a few workgroups of some launches; one-run parity
-    checks passed it)"""
+@pytest.mark.parametrize("path", ["staged", "fused"])
+@pytest.mark.parametrize("cin,cout,hw,B", [(64, 32, 16, 32), (64, 32, 16, 64), (64, 32, 16, 86), (128, 64, 8, 32),
+                                           (128, 64, 8, 86), (256, 128, 4, 32)])
+def test_fu_repeat_bitwise(path, cin, cout, hw, B):
+    """both Fourier-unit paths (staged: r2c_mix + c2r; fused: pass 0 + split pass 1) at the
+    strong-scaling shard sizes, with the library's default BN folds, twenty fresh train forwards of
+    one SpectralTransform on one input: bitwise equal outputs and buffers (a
+    per-channel bn1 fold inside ffc_fu2d_r2c_mix corrupted T of whole channels in co-resident
+    workgroups; one-run parity checks passed it)"""
+    from fastfourierconvolution_amd import _runtime as rt
     torch.manual_seed(cin + hw + B)
     base = _st(cin, cout, 0.1, seed=cin + B)
     x = torch.randn((B, cin, hw, hw), generator=torch.Generator().manual_seed(B)).cuda()
-    outs = []
-    for _ in range(12):
-        out, _sd = _run_chfold(copy.deepcopy(base), [x], True, "staged")
+    outs, sds = [], []
+    for _ in range(20):
+        out, sd = _run_chfold(copy.deepcopy(base), [x], rt.BN_CHFOLD, path)
         outs.append(out[0])
+        sds.append(sd)
     bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
     assert not bad, f"runs {bad} differ from run 0"
+    for sd in sds[1:]:
+        for k in sd:
+            assert torch.equal(sd[k], sds[0][k]), k
 
 
 # --------------------------------------------------------------------------- round 6: bin groups

@@ -138,3 +138,33 @@ def test_paired_syncbn_one_collective(rccl_world1):
     for (b, *_), (t, *_) in zip(items, twins):
         for k, v in b.state_dict().items():
             assert torch.equal(v, t.state_dict()[k]), k
+
+
+@pytest.mark.parametrize("path", ["staged", "fused"])
+@pytest.mark.parametrize("B", [32, 64])
+def test_syncbn_moments_fold_repeat_bitwise(rccl_world1, path, B):
+    """SyncBN with the consumers finalizing from the all-reduced moments (ffc_bn_fold.moments, round
+    6): twenty fresh SpectralTransform train forwards (gen64 ffc3 shape) bitwise equal, and within
+    1e-6 of the single-rank path (same fp64 moments, another merge / finalize route)"""
+    import copy
+    import fastfourierconvolution_amd as F
+    from fastfourierconvolution_amd import distributed as D
+    from fastfourierconvolution_amd import _runtime as rt
+    torch.manual_seed(B)
+    with contextlib.redirect_stdout(io.StringIO()):
+        st = F.SpectralTransform(64, 32, stride=2, upsample=True).cuda().train()
+    x = torch.randn((B, 64, 16, 16), generator=torch.Generator().manual_seed(B + 1)).cuda()
+    old = rt.FU_PATH
+    rt.FU_PATH = path
+    try:
+        with torch.no_grad():
+            ref = copy.deepcopy(st)(x).clone()
+            D.enable_sync_bn(even_world1=True)
+            outs = [copy.deepcopy(st)(x).clone() for _ in range(20)]
+        torch.cuda.synchronize()
+    finally:
+        rt.FU_PATH = old
+        D.disable_sync_bn()
+    bad = [i for i, o in enumerate(outs) if not torch.equal(o, outs[0])]
+    assert not bad, f"runs {bad} differ from run 0"
+    torch.testing.assert_close(outs[0], ref, rtol=1e-6, atol=1e-6)

@@ -40,7 +40,7 @@ for rep in range(30):
     bad = T != T[0:1]
     if not bad.any():
         continue
-    for sp, b in sorted({(int(a), int(c)) for a, c in zip(*np.nonzero(bad.any(axis=(2, 3, 4, 5, 6))))})[:6]:
+    for sp, b in sorted({(int(a), int(c)) for a, c in zip(*np.nonzero(bad.any(axis=(2, 3, 4, 5, 6))))})[:3]:
         for slot, name in ((0, "after rows"), (1, "at end")):
             d = bad[sp, b, slot]
             if not d.any():
