@@ -24,7 +24,7 @@ int launch_status(const char* what) {
 
 extern "C" const char* ffc_last_error(void) { return ffc::g_err.c_str(); }
 
-extern "C" int ffc_abi_version(void) { return 3; }
+extern "C" int ffc_abi_version(void) { return 4; }   // 4: ffc_bn_fold.moments, ffc_fu_forward_ex4 (round 6)
 
 // sizes of the ABI structs, so bindings can verify their mirror layouts
 extern "C" int ffc_struct_sizes(int* out, int n) {

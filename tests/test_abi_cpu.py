@@ -20,7 +20,7 @@ def declared_functions():
 
 def test_library_builds_and_loads():
     lib = _lib.load()
-    assert lib.ffc_abi_version() == 3
+    assert lib.ffc_abi_version() == 4
 
 
 def test_every_declared_symbol_is_exported():
