@@ -198,8 +198,8 @@ __device__ __forceinline__ void tile_row_stats(const floatx16& acc, int nv, floa
 
 // LDS-DMA copy of n4 16-byte groups from 16-byte aligned global memory into LDS by whole 64-lane
 // wave instructions (global_load_lds_dwordx4; lane i of an instruction lands at dst + 16 i bytes):
-// dst needs room for n4 rounded up to 64 groups.  Completion: the issuing waves' vmcnt (the next
-// __syncthreads waits for it).
+// dst needs room for n4 rounded up to 64 groups.  Completion: the issuing waves' vmcnt -- call
+// dma_wait() before the barrier after which other waves read dst.
 __device__ __forceinline__ void dma_copy16(const float* src, float* dst, int n4, int tid, int nthreads) {
     typedef __attribute__((address_space(1))) void* gptr_t;
     typedef __attribute__((address_space(3))) void* lptr_t;
@@ -211,6 +211,13 @@ __device__ __forceinline__ void dma_copy16(const float* src, float* dst, int n4,
         }
     }
 }
+
+// Retire this wave's LDS-DMA copies (dma_copy16) before the barrier that publishes them to the other
+// waves: LDS-DMA data is ordered for another wave's ds_read only by the issuing wave's vmcnt wait
+// followed by a barrier (MI355X_MICROARCH.md item 7).  __syncthreads() emits that vmcnt(0) today
+// whenever a copy is pending; the explicit wait keeps the order if a later edit makes the barrier a
+// raw s_barrier.
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

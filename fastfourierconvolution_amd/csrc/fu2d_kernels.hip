@@ -811,6 +811,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_kernel(MixArgs a) {
             bnss[C2 + i] = a.bn_shift[i];
         }
     }
+    ffc::dma_wait();
     __syncthreads();
     MixA<MT, CC, F16> A;
     A.load(Wm, a.wmixT, a.Mpad, C2, hh, col);
@@ -1034,6 +1035,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
         fss[tid] = ra.in_scale ? ra.in_scale[tid] : 1.0f;
         fss[C + tid] = ra.in_scale ? ra.in_shift[tid] : 0.0f;
     }
+    ffc::dma_wait();
     __syncthreads();
 #ifdef FFC_R2CMIX_LATE_T
 #pragma unroll
@@ -1211,6 +1213,7 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_mix_cols_kernel(MixArgs a) {
         bnss[i] = a.bn_scale[i];
         bnss[C2 + i] = a.bn_shift[i];
     }
+    ffc::dma_wait();
     __syncthreads();
     MixA<MT, CC, F16, false, false> A;   // f32-input MFMA here: the split measured slower (fewer waves)
     A.load(Wm, a.wmixT, a.Mpad, C2, hh, col);

@@ -259,6 +259,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         }
     }
     FU_STAMP(1);
+    if (a.wm_lds) ffc::dma_wait();   // the weight's LDS-DMA retired before the barrier (ffc_internal.h)
     __syncthreads();
 
     // 2. column C2C over H, ortho scale 1/sqrt(HW)
@@ -534,7 +535,7 @@ __device__ __forceinline__ void fu_kg_body(const FuArgs& a, float* smem) {
     }
     // the mix weight's LDS-DMA (the kernel's first loads) is tracked by vmcnt only: this wave's
     // copies landed before the barrier, so every wave may read Wm after it
-    if (a.wm_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.wm_lds) ffc::dma_wait();
     __syncthreads();
     FU_STAMP(2);
 

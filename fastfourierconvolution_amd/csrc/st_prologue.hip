@@ -96,6 +96,7 @@ __global__ __launch_bounds__(ST_THREADS) void st_prologue_kernel(StArgs a) {
             xs[i] = (((q[0] + q[1]) + q[a.W]) + q[a.W + 1]) * 0.25f;
         }
     }
+    ffc::dma_wait();
     __syncthreads();
     ST_STAMP(1);
 
