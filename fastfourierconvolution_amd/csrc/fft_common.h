@@ -147,4 +147,169 @@ __device__ __forceinline__ void irfft_reg(const float (&Xr)[N / 2 + 1], const fl
     }
 }
 
+// ---- Column DFTs across lanes (wave-64 butterfly exchanges, round 6)
+// The fused Fourier unit holds one spectrum row per lane after its row R2C (fu_kernels.hip: lane
+// y of an aligned group of N lanes = row y of one channel, re[k] / im[k] = bin k of that row).
+// The column DFT of bin k then runs ACROSS the group's lanes: a radix-2 butterfly pairs lane y with
+// lane y ^ D, and the partner's value comes through a lane exchange instead of an LDS write /
+// barrier / strided read / write round trip:
+//   D = 1, 2   one DPP quad_perm move,
+//   D = 4      row_half_mirror (y ^ 7) then quad_perm [3,2,1,0] (^ 3),
+//   D = 8      row_mirror (y ^ 15) then row_half_mirror (^ 7),
+//   D = 16     ds_swizzle in bit-mask mode (xor 16 within 32 lanes; no LDS memory access).
+// Both lanes of a pair compute one output each, branch-free: t = p + sg v with sg = +1 on the
+// lower lane (a + b) and -1 on the upper (a - b), then the upper lane's twiddle.
+// Measured on MI355X (gen64 B = 256, same-box A/B): the DPP composites cost VALU issue
+// and wait states in a VALU-bound phase; ds_swizzle for every distance (the exchange on the LDS
+// pipe, no memory access) with packed (re, im) arithmetic is the fastest form (FFC_LANE_SWZ = 2,
+// FFC_LANE_PK), level with the LDS column pass, which stays the default (FFC_FU_SHUF=1 selects this).
+#ifndef FFC_LANE_NOPK
+#define FFC_LANE_PK
+#endif
+template <int D>
+__device__ __forceinline__ float lane_xor(float v) {
+    static_assert(D == 1 || D == 2 || D == 4 || D == 8 || D == 16, "partner distance within 32 lanes");
+    const int iv = __builtin_bit_cast(int, v);
+    int r;
+#ifndef FFC_LANE_SWZ
+#define FFC_LANE_SWZ 2   // 2: ds_swizzle for every D; 1: for D >= 4; 0: the DPP moves above (A/B)
+#endif
+    if constexpr (FFC_LANE_SWZ == 2 || (FFC_LANE_SWZ == 1 && D >= 4)) {
+        r = __builtin_amdgcn_ds_swizzle(iv, (D << 10) | 0x1F);
+    } else if constexpr (D == 1) {
+        r = __builtin_amdgcn_update_dpp(0, iv, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (D == 2) {
+        r = __builtin_amdgcn_update_dpp(0, iv, 0x4E, 0xF, 0xF, false);
+    } else if constexpr (D == 4) {
+        r = __builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, iv, 0x141, 0xF, 0xF, false), 0x1B, 0xF,
+                                        0xF, false);
+    } else if constexpr (D == 8) {
+        r = __builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, iv, 0x140, 0xF, 0xF, false), 0x141, 0xF,
+                                        0xF, false);
+    } else {
+        r = __builtin_amdgcn_ds_swizzle(iv, 0x401F);   // and_mask 0x1F, or_mask 0, xor_mask 16
+    }
+    return __builtin_bit_cast(float, r);
+}
+
+// row index bitrev(y) over log2(N) bits (the DIF output order)
+template <int N>
+__device__ __forceinline__ int lane_brev(int y) {
+    return (int)(__builtin_bitreverse32((unsigned)y) >> (32 - ilog2c(N)));
+}
+
+// twiddle of lane y at the stage of half-size D (sub-transforms of length 2D): W_{2D}^{y mod D} on the
+// upper lane of the pair (y & D), 1 on the lower.  Forward exp(-2 pi i j / 2D), INV exp(+..)
+template <int D, bool INV>
+__device__ __forceinline__ void lane_tw(int y, float& c, float& s) {
+    const int j = y & (D - 1);
+    const bool up = (y & D) != 0;
+    const float tc = c_twc[j * (64 / D)], ts = c_tws[j * (64 / D)];
+    c = up ? tc : 1.0f;
+    s = up ? (INV ? ts : -ts) : 0.0f;
+}
+
+// decimation-in-frequency stage D: exchange, add / subtract, twiddle (D = 1: the factor `scale`)
+template <int D, int K>
+__device__ __forceinline__ void lane_dif_stage(float (&re)[K], float (&im)[K], int y, float scale) {
+    const float sg = (y & D) ? -1.0f : 1.0f;
+    float c, s;
+    lane_tw<D, false>(y, c, s);
+#ifdef FFC_LANE_PK   // the add / subtract and the twiddle on packed (re, im) pairs (FFC_LANE_NOPK: scalar)
+    typedef float lf2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const lf2 v = {re[k], im[k]};
+        const lf2 p = {lane_xor<D>(re[k]), lane_xor<D>(im[k])};
+        const lf2 t = __builtin_elementwise_fma(lf2{sg, sg}, v, p);
+        lf2 o;
+        if constexpr (D == 1) {
+            o = t * scale;
+        } else {
+            o = __builtin_elementwise_fma(lf2{t.y, t.x}, lf2{-s, s}, t * c);
+        }
+        re[k] = o.x;
+        im[k] = o.y;
+    }
+    return;
+#endif
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const float pr = lane_xor<D>(re[k]), pi = lane_xor<D>(im[k]);
+        const float tr = fmaf(sg, re[k], pr), ti = fmaf(sg, im[k], pi);
+        if constexpr (D == 1) {
+            re[k] = tr * scale;
+            im[k] = ti * scale;
+        } else {
+            re[k] = fmaf(tr, c, -ti * s);
+            im[k] = fmaf(tr, s, ti * c);
+        }
+    }
+}
+
+// decimation-in-time inverse stage D: twiddle (D = 1: the factor `scale` on both lanes), exchange,
+// add / subtract
+template <int D, int K>
+__device__ __forceinline__ void lane_dit_inv_stage(float (&re)[K], float (&im)[K], int y, float scale) {
+    const float sg = (y & D) ? -1.0f : 1.0f;
+    float c, s;
+    lane_tw<D, true>(y, c, s);
+#ifdef FFC_LANE_PK
+    typedef float lf2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const lf2 v = {re[k], im[k]};
+        lf2 u;
+        if constexpr (D == 1) {
+            u = v * scale;
+        } else {
+            u = __builtin_elementwise_fma(lf2{v.y, v.x}, lf2{-s, s}, v * c);
+        }
+        const lf2 p = {lane_xor<D>(u.x), lane_xor<D>(u.y)};
+        const lf2 o = __builtin_elementwise_fma(lf2{sg, sg}, u, p);
+        re[k] = o.x;
+        im[k] = o.y;
+    }
+    return;
+#endif
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        float ur, ui;
+        if constexpr (D == 1) {
+            ur = re[k] * scale;
+            ui = im[k] * scale;
+        } else {
+            ur = fmaf(re[k], c, -im[k] * s);
+            ui = fmaf(re[k], s, im[k] * c);
+        }
+        const float pr = lane_xor<D>(ur), pi = lane_xor<D>(ui);
+        re[k] = fmaf(sg, ur, pr);
+        im[k] = fmaf(sg, ui, pi);
+    }
+}
+
+// Forward N-point DFT over the N lanes of an aligned lane group, K columns at once: lane y holds x[y]
+// (per column) and ends with scale * X[bitrev(y)].  Every lane of the group must be active.
+template <int N, int K>
+__device__ __forceinline__ void lane_fft_dif(float (&re)[K], float (&im)[K], int y, float scale) {
+    static_assert(N >= 2 && N <= 32 && (N & (N - 1)) == 0, "2 .. 32 lanes");
+    if constexpr (N > 16) lane_dif_stage<16, K>(re, im, y, scale);
+    if constexpr (N > 8) lane_dif_stage<8, K>(re, im, y, scale);
+    if constexpr (N > 4) lane_dif_stage<4, K>(re, im, y, scale);
+    if constexpr (N > 2) lane_dif_stage<2, K>(re, im, y, scale);
+    lane_dif_stage<1, K>(re, im, y, scale);
+}
+
+// Inverse (unnormalised, times `scale`) N-point DFT over the lane group: lane y holds X[bitrev(y)]
+// and ends with scale * x[y], x[n] = sum_k X[k] exp(+2 pi i k n / N).
+template <int N, int K>
+__device__ __forceinline__ void lane_ifft_dit(float (&re)[K], float (&im)[K], int y, float scale) {
+    static_assert(N >= 2 && N <= 32 && (N & (N - 1)) == 0, "2 .. 32 lanes");
+    lane_dit_inv_stage<1, K>(re, im, y, scale);
+    if constexpr (N > 2) lane_dit_inv_stage<2, K>(re, im, y, scale);
+    if constexpr (N > 4) lane_dit_inv_stage<4, K>(re, im, y, scale);
+    if constexpr (N > 8) lane_dit_inv_stage<8, K>(re, im, y, scale);
+    if constexpr (N > 16) lane_dit_inv_stage<16, K>(re, im, y, scale);
+}
+
 }  // namespace

@@ -77,6 +77,7 @@ struct FuArgs {
     int mgroups;                     // pass 0: workgroups per sample, each mixing MT / mgroups M-tiles
     int B;
     int kgroups;                     // bin groups of pass 0 (fu_pass0_kg_kernel): slab rows, spill layout
+    int shuf;                        // column DFTs across lanes (fft_common.h lane_fft_dif / lane_ifft_dit)
 };
 
 constexpr int FU_THREADS = 512;
@@ -244,6 +245,31 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         __syncthreads();
     } else {
 
+    if (a.shuf) {
+        // 1+2. row R2C in registers, then the column DFTs across the H lanes that hold the channel's
+        //      rows (lane_fft_dif: DPP / ds_swizzle butterfly exchanges, ortho scale folded in): no LDS
+        //      round trip and no barrier between the row and column transforms.  Lane y ends with
+        //      spectrum row bitrev(y), stored to its natural place.
+        for (int r = tid; r < C * H; r += FU_THREADS) {
+            const int ch = r / H, y = r - ch * H;
+            float sv[W], re[WP], im[WP];
+            load_s_row<W, UP>(a, insc, b, ch, y, H, sv);
+            rfft_reg<W>(sv, re, im);
+            lane_fft_dif<H, WP>(re, im, y, a.norm);
+            const int yo = lane_brev<H>(y);
+            float* zr = Zre + (ch * H + yo) * WP;
+            float* zi = Zim + (ch * H + yo) * WP;
+#pragma unroll
+            for (int k = 0; k < WP; ++k) {
+                zr[k] = re[k];
+                zi[k] = im[k];
+            }
+        }
+        FU_STAMP(1);
+        if (a.wm_lds) ffc::dma_wait();
+        __syncthreads();
+        FU_STAMP(2);
+    } else {
     // 1. row R2C (real W-point FFT per (channel,row) on a W/2-point complex FFT), input transform fused
     for (int r = tid; r < C * H; r += FU_THREADS) {
         const int ch = r / H, y = r - ch * H;
@@ -282,6 +308,7 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
     }
     __syncthreads();
     FU_STAMP(2);
+    }   // !a.shuf
 
     // 3. spectral mix on MFMA: Y[o][n] = sum_i Wmix[o][i] Z[i][n], Z[2c+h] = (h ? Im : Re)(channel c)
     //    k-step s feeds k-slot h = lane>>5 with channel s, component h.
@@ -395,6 +422,30 @@ __global__ __launch_bounds__(FU_THREADS) void fu_kernel(FuArgs a) {
         if (tid == 0) g_fu_trace[8 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
         return;
+    } else if (a.shuf) {
+        // 4+5. lane y reads spectrum row bitrev(y), the inverse column DFTs run across the channel's H
+        //      lanes (lane_ifft_dit, ortho scale folded in) and leave row y in lane y for its C2R
+        for (int r = tid; r < C * H; r += FU_THREADS) {
+            const int ch = r / H, y = r - ch * H;
+            const int yo = lane_brev<H>(y);
+            const float* yr = Yre + (ch * H + yo) * WP;
+            const float* yi = Yim + (ch * H + yo) * WP;
+            float xr[WP], xi[WP], re[W];
+#pragma unroll
+            for (int k = 0; k < WP; ++k) {
+                xr[k] = yr[k];
+                xi[k] = yi[k];
+            }
+            lane_ifft_dit<H, WP>(xr, xi, y, a.norm);
+            irfft_reg<W>(xr, xi, re);
+            if (a.residual) {
+                float s[W];
+                load_s_row<W, UP>(a, insc, b, ch, y, H, s);
+#pragma unroll
+                for (int x = 0; x < W; ++x) re[x] += s[x];
+            }
+            store_row<W>(a.out + ((size_t)(b * C + ch) * H + y) * W, re);
+        }
     } else {
         // 4. inverse column C2C over H, ortho scale
         for (int q = tid; q < C * WP; q += FU_THREADS) {
@@ -714,6 +765,24 @@ __global__ __launch_bounds__(64) void fu_pass1_split_kernel(FuArgs a) {
         spill_to_plane<H, W, G>(dst, n, v, sc, sh);
     }
     __syncthreads();
+    if (a.shuf) {   // lane (ch, y): row bitrev(y) in, inverse column DFTs across the H lanes, row y out
+        const int ch = tid / H, y = tid - ch * H;
+        const int yo = lane_brev<H>(y);
+        const float* yr = Yre + (ch * H + yo) * WP;
+        const float* yi = Yim + (ch * H + yo) * WP;
+        float xr[WP], xi[WP], re[W];
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+            xr[k] = yr[k];
+            xi[k] = yi[k];
+        }
+        lane_ifft_dit<H, WP>(xr, xi, y, a.norm);
+        irfft_reg<W>(xr, xi, re);
+#pragma unroll
+        for (int x = 0; x < W; ++x) re[x] += sres[x];
+        store_row<W>(a.out + ((size_t)(b * C + c0 + ch) * H + y) * W, re);
+        return;
+    }
     for (int q = tid; q < CPG * WP; q += 64) {   // inverse column C2C over H, ortho scale
         const int ch = q / WP, k = q - ch * WP;
         float* yr = Yre + ch * NB + k;
@@ -850,6 +919,17 @@ bool fu_mix_f32_forced() {
     static const bool on = [] {
         const char* e = std::getenv("FFC_FU_MFMA");
         return e && e[0] == 'f';
+    }();
+    return on;
+}
+// FFC_FU_SHUF=1: the column DFTs across lanes (fft_common.h lane_fft_dif / lane_ifft_dit) instead of
+// through LDS (one lane per column line).  Off by default: measured level with the LDS column pass at
+// gen64 B = 256 and B = 32 (round 6) -- the row / column phases are VALU-issue bound, and
+// the lane form spends in butterfly arithmetic on every lane what it saves in LDS traffic and barriers
+bool fu_shuf_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("FFC_FU_SHUF");
+        return e && e[0] == '1';
     }();
     return on;
 }
@@ -1068,6 +1148,7 @@ static int fu_forward_impl(const float* t, int B, int C, int H, int W, int up, c
     a.mgroups = 1;
     a.B = B;
     a.kgroups = kgroups;
+    a.shuf = fu_shuf_on() && H >= 2 && H <= 32 ? 1 : 0;
     if (pass == 0 && kgroups == 2) {
         // pass 0 over two bin groups per sample (fu_pass0_kg_kernel): the split weight staged in LDS
         // while two workgroups still fit a CU, else read from L2

@@ -223,7 +223,7 @@ static void shape_queries() {
     int sizes[6];
     EXPECT_EQ(ffc_struct_sizes(sizes, 6), FFC_OK);
     EXPECT_EQ(ffc_struct_sizes(sizes, 5), FFC_E_INVALID);
-    EXPECT_EQ(ffc_abi_version(), 3);
+    EXPECT_EQ(ffc_abi_version(), 4);
 }
 
 // ffc_last_error is thread-local: concurrent failing calls each see their own message
