@@ -925,6 +925,9 @@ struct R2cMixLds {
 #ifdef FFC_R2CMIX_DUMP   // DESIGN 10c probe build: Tl after the row FFTs (slot 0) and at the end (slot 1)
 __device__ float g_r2cmix_dump[512 * 2 * 4608];
 #endif
+#ifdef FFC_R2CMIX_CANARY
+__device__ int g_r2cmix_canary_hits;
+#endif
 #if defined(FFC_R2CMIX_DBG) || defined(FFC_R2CMIX_DBGEND)
 // DESIGN 10c probe build: per workgroup, per channel: bn1 scale, shift, sum R, sum |T| after the row
 // FFTs, sum |T| after the column FFTs (thread ch sums its channel in a fixed order)
@@ -980,6 +983,13 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
     for (int i = tid; i < LY::SCR; i += FU2_THREADS) scr[i] = 0.0f;
 #endif
     __syncthreads();
+#endif
+#ifdef FFC_R2CMIX_CANARY   // DESIGN 10c probe: a canary in the LDS padding behind the layout (FFC_R2CMIX_PAD)
+    for (int i = tid; i < FFC_R2CMIX_PAD / 4; i += FU2_THREADS) smem[LY::FLOATS + i] = __int_as_float(0x7fc0dead);
+    __syncthreads();
+#endif
+#ifdef FFC_R2CMIX_V192    // DESIGN 10c probe: 192 VGPRs reserved -> at most two workgroups per CU, layout unpadded
+    asm volatile("" ::: "v191");
 #endif
     float4 v[NV];
 #ifndef FFC_R2CMIX_LATE_T
@@ -1175,6 +1185,20 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
     if (blockIdx.x < 512 && LY::TL <= 4608)
         for (int i = tid; i < LY::TL; i += FU2_THREADS)
             g_r2cmix_dump[((size_t)blockIdx.x * 2 + 1) * 4608 + i] = reinterpret_cast<const float*>(Tl)[i];
+#endif
+#ifdef FFC_R2CMIX_CANARY
+    __syncthreads();
+    {
+        int first = -1, cnt = 0;
+        for (int i = tid; i < FFC_R2CMIX_PAD / 4; i += FU2_THREADS)
+            if (__float_as_int(smem[LY::FLOATS + i]) != 0x7fc0dead) {
+                if (first < 0) first = i;
+                ++cnt;
+            }
+        if (cnt && atomicAdd(&g_r2cmix_canary_hits, 1) < 40)
+            printf("r2cmix canary: blk %d tid %d first pad float %d (layout float %d) count %d\n", (int)blockIdx.x,
+                   tid, first, LY::FLOATS + first, cnt);
+    }
 #endif
 #ifdef FFC_R2CMIX_DBGEND
     __syncthreads();
@@ -1638,6 +1662,9 @@ extern "C" int ffc_fu2d_r2c_mix(const float* t, int B, int C, int H, int W, int 
     R2cMixKernel k = pick_r2c_mix(C, H / up, lds);
 #ifdef FFC_R2CMIX_ONEWG   // DESIGN 10c probe: a dynamic LDS request that admits one workgroup per CU
     lds = 90 * 1024;
+#endif
+#ifdef FFC_R2CMIX_PAD     // DESIGN 10c probe: unused LDS behind the layout, still two workgroups per CU
+    lds += FFC_R2CMIX_PAD;
 #endif
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c_mix");
     if (rc) return rc;
