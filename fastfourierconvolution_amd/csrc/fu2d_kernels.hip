@@ -960,7 +960,12 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
     static_assert((CC & (CC - 1)) == 0 && CC <= FU2_THREADS / 4 && (C * HT * HT) % (4 * FU2_THREADS) == 0,
                   "whole float4 rounds of the sample");
     const MixArgs& a = ra.m;
+#ifdef FFC_R2CMIX_FRONTPAD   // DESIGN 10c probe: unused LDS IN FRONT of the layout
+    extern __shared__ __attribute__((aligned(16))) float smem_front[];
+    float* const smem = smem_front + FFC_R2CMIX_FRONTPAD / 4;
+#else
     extern __shared__ __attribute__((aligned(16))) float smem[];
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int hh = lane >> 5, col = lane & 31;
     const int b = blockIdx.x % a.B;
@@ -1665,6 +1670,9 @@ extern "C" int ffc_fu2d_r2c_mix(const float* t, int B, int C, int H, int W, int 
 #endif
 #ifdef FFC_R2CMIX_PAD     // DESIGN 10c probe: unused LDS behind the layout, still two workgroups per CU
     lds += FFC_R2CMIX_PAD;
+#endif
+#ifdef FFC_R2CMIX_FRONTPAD
+    lds += FFC_R2CMIX_FRONTPAD;
 #endif
     int rc = raise_lds(reinterpret_cast<const void*>(k), lds, "ffc_fu2d_r2c_mix");
     if (rc) return rc;
