@@ -48,6 +48,9 @@ __device__ __forceinline__ void bn_fold_finalize(const ffc_bn_fold& f, int o, do
     }
 }
 
+template <bool SWAP16>
+__device__ __forceinline__ double permlane_sum_f64(double v);
+
 template <int BLOCK>
 __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool leader, double* scratch) {
     constexpr int NW = BLOCK / 64;
@@ -101,12 +104,13 @@ __device__ void bn_fold_block(const ffc_bn_fold& f, float* sc, float* sh, bool l
                 q += (double)e.z + en * em * em;
             }
         }
-        n += shfl_xor_f64(n, 16);
-        s += shfl_xor_f64(s, 16);
-        q += shfl_xor_f64(q, 16);
-        n += shfl_xor_f64(n, 32);
-        s += shfl_xor_f64(s, 32);
-        q += shfl_xor_f64(q, 32);
+        // v + v(lane ^ 16), then ^ 32: v_permlane16/32_swap, the same sums as a __shfl_xor pair
+        n = permlane_sum_f64<true>(n);
+        s = permlane_sum_f64<true>(s);
+        q = permlane_sum_f64<true>(q);
+        n = permlane_sum_f64<false>(n);
+        s = permlane_sum_f64<false>(s);
+        q = permlane_sum_f64<false>(q);
         if (live && rg == 0) {
             double* d = scratch + 3 * (wave * 16 + oc);
             d[0] = n;

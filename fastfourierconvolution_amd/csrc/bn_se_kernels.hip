@@ -5,6 +5,7 @@
 // (torch/nn/modules/batchnorm.py as called from layers/ffc/*.py) are reproduced exactly.
 // SE: SELayer (layers/ffc/spectral_transform.py:12-28).
 #include "ffc_internal.h"
+#include "bn_common.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -15,10 +16,20 @@ namespace {
 
 constexpr int RED_THREADS = 256;
 
+// whole-wave fp64 sum, bit-identical in every lane: the DPP / v_permlane*_swap tree of bn_common.h
+// (ffc::group_sum_f64<64>) -- the reductions stay in the VALU; the ds_bpermute tree it replaces
+// (__shfl_xor, two LDS-pipe round trips per level and double) was most of a finalize launch's
+// latency chain.  FFC_BN_SHFL=1 keeps the __shfl_xor tree (A/B).
+#ifndef FFC_BN_SHFL
+#define FFC_BN_SHFL 0
+#endif
 __device__ __forceinline__ double wave_sum_f64(double v) {
+    if constexpr (FFC_BN_SHFL) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        return v;
+    }
+    return ffc::group_sum_f64<64>(v);
 }
 
 // one block per channel: merge rows of a {n, mean, M2} slab into fp64 raw moments {n, sum, sumsq}
@@ -350,12 +361,14 @@ __global__ __launch_bounds__(256) void bn_partial16_kernel(const float4* __restr
         s += en * em;
         q += (double)e.z + en * em * em;
     }
-#pragma unroll
-    for (int m = 16; m <= 32; m <<= 1) {
-        n += __shfl_xor(n, m, 64);
-        s += __shfl_xor(s, m, 64);
-        q += __shfl_xor(q, m, 64);
-    }
+    // the 4 row groups of the wave: v + v(lane ^ 16), then ^ 32, on v_permlane16/32_swap (the same sums
+    // as the __shfl_xor pairs, without the ds_bpermute round trips)
+    n = ffc::permlane_sum_f64<true>(n);
+    s = ffc::permlane_sum_f64<true>(s);
+    q = ffc::permlane_sum_f64<true>(q);
+    n = ffc::permlane_sum_f64<false>(n);
+    s = ffc::permlane_sum_f64<false>(s);
+    q = ffc::permlane_sum_f64<false>(q);
     __shared__ double sh[4][16][3];
     if (lane < 16) {
         sh[wave][oc][0] = n;
