@@ -283,7 +283,18 @@ def _pow2_floor(v: int) -> int:
 # cap, rounded to 2^k: 2 since the SE gate went thread-per-channel (B = 32: 0.1755 -> 0.1731 ms with 4
 # instead of 8, profiles/r05/an; B = 64 0.2105 -> 0.2092 ms with 2 instead of 4, r05/av; r04 had
 # measured them level)
-ST_SPLIT_MAX = _pow2_floor(__import__("os").environ.get("FFC_ST_SPLIT_MAX", "2"))
+# (FFC_ST_SPLIT_MAX fixes it for every batch).  Round 6: 4 at B <= 32 -- the per-rank batch of the
+# 8-way strong split -- B = 32 0.1790 / 0.1798 -> 0.1771 / 0.1774 ms (8: 0.1774 / 0.1777), B = 64 level
+# (profiles/r06/st)
+_ST_SPLIT_ENV = __import__("os").environ.get("FFC_ST_SPLIT_MAX")
+ST_SPLIT_MAX = _pow2_floor(_ST_SPLIT_ENV) if _ST_SPLIT_ENV else 0   # 0: by batch (st_split_max)
+
+
+def st_split_max(B: int) -> int:
+    """the ST prologue's cap on workgroups per sample at batch B"""
+    if ST_SPLIT_MAX:
+        return ST_SPLIT_MAX
+    return 4 if B <= 32 else 2
 # ST prologue conv1 on the split-bf16 MFMA products (FFC_ST_MFMA=f32: the exact f32-input MFMA, A/B)
 ST_SPLIT_MFMA = __import__("os").environ.get("FFC_ST_MFMA", "split") != "f32"
 # the fused FU's pass 1 reads pass 0's mix output instead of recomputing it (FFC_FU_SPILL=0: recompute)

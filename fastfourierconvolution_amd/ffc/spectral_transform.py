@@ -148,7 +148,7 @@ class SpectralTransform(nn.Module):
             se2 = rt.require(self.se_block.fc[2].weight.detach(), "se.fc.2.weight") if hid > 0 else None
             wc = self._conv1_T(stream)
             # small batches: several workgroups per sample, each with a share of conv1's tiles
-            split = min(L.ffc_st_prologue_split(B, Cin, H, W, int(pool), c), rt.ST_SPLIT_MAX) if rt.ST_SPLIT else 1
+            split = min(L.ffc_st_prologue_split(B, Cin, H, W, int(pool), c), rt.st_split_max(B)) if rt.ST_SPLIT else 1
             nrows = B * split
             slab = torch.empty((nrows, c, 4), device=dev, dtype=torch.float32)
             wc3 = self._conv1_3(stream)
