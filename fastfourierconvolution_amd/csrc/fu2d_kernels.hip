@@ -925,7 +925,7 @@ struct R2cMixLds {
 #ifdef FFC_R2CMIX_DUMP   // DESIGN 10c probe build: Tl after the row FFTs (slot 0) and at the end (slot 1)
 __device__ float g_r2cmix_dump[512 * 2 * 4608];
 #endif
-#ifdef FFC_R2CMIX_CANARY
+#if defined(FFC_R2CMIX_CANARY) || defined(FFC_R2CMIX_FCANARY)
 __device__ int g_r2cmix_canary_hits;
 #endif
 #if defined(FFC_R2CMIX_DBG) || defined(FFC_R2CMIX_DBGEND)
@@ -991,6 +991,10 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
 #endif
 #ifdef FFC_R2CMIX_CANARY   // DESIGN 10c probe: a canary in the LDS padding behind the layout (FFC_R2CMIX_PAD)
     for (int i = tid; i < FFC_R2CMIX_PAD / 4; i += FU2_THREADS) smem[LY::FLOATS + i] = __int_as_float(0x7fc0dead);
+    __syncthreads();
+#endif
+#ifdef FFC_R2CMIX_FCANARY  // DESIGN 10c probe: a canary in the LDS padding in front of the layout (FFC_R2CMIX_FRONTPAD)
+    for (int i = tid; i < FFC_R2CMIX_FRONTPAD / 4; i += FU2_THREADS) smem_front[i] = __int_as_float(0x7fc0beef);
     __syncthreads();
 #endif
 #ifdef FFC_R2CMIX_V192    // DESIGN 10c probe: 192 VGPRs reserved -> at most two workgroups per CU, layout unpadded
@@ -1203,6 +1207,20 @@ __global__ __launch_bounds__(FU2_THREADS) void fu2d_r2c_mix_kernel(R2cMixArgs ra
         if (cnt && atomicAdd(&g_r2cmix_canary_hits, 1) < 40)
             printf("r2cmix canary: blk %d tid %d first pad float %d (layout float %d) count %d\n", (int)blockIdx.x,
                    tid, first, LY::FLOATS + first, cnt);
+    }
+#endif
+#ifdef FFC_R2CMIX_FCANARY
+    __syncthreads();
+    {
+        int last = -1, cnt = 0;
+        for (int i = tid; i < FFC_R2CMIX_FRONTPAD / 4; i += FU2_THREADS)
+            if (__float_as_int(smem_front[i]) != 0x7fc0beef) {
+                last = i;
+                ++cnt;
+            }
+        if (cnt && atomicAdd(&g_r2cmix_canary_hits, 1) < 40)
+            printf("r2cmix front canary: blk %d tid %d last pad float %d (layout offset %d) count %d\n",
+                   (int)blockIdx.x, tid, last, last - FFC_R2CMIX_FRONTPAD / 4, cnt);
     }
 #endif
 #ifdef FFC_R2CMIX_DBGEND
